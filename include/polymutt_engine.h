@@ -1,0 +1,199 @@
+/*
+ * polymutt_engine.h -- C ABI of the MI355X-native polyMutt per-site family-likelihood engine.
+ *
+ * The reference (genome-vendor/polymutt v0.13) has no plugin/FFI boundary; its hot path is the C++
+ * class surface FamilyLikelihoodSeq (-> NucFamGenotypeLikelihood -> ScalarMinimizer) driven once per
+ * site by the OpenMP site loop of src/main.cpp:325-594.  This header is the drop-in replacement for
+ * that loop body: the host driver (polymutt_amd/host, or any FFI caller) packs a batch of sites into a
+ * dense block and one call evaluates, per site, everything main.cpp:327-589 computes:
+ *
+ *   CalcReadStats + depth/PS/MQ filters ........ src/NucFamGenotypeLikelihood.cpp:520-546, main.cpp:343-348
+ *   MonomorphismLogLikelihood(_denovo) ......... NucFamGenotypeLikelihood.cpp:502-517, FamilyLikelihoodSeq.cpp:68-72
+ *   PolymorphismLogLikelihood x3 (+x3) ......... FamilyLikelihoodSeq.cpp:91-104 -> OptimizeFrequency
+ *                                                 NucFamGenotypeLikelihood.cpp:432-444 -> Brent core/MathGold.cpp:81-177
+ *   CalcVarPosterior(4 | 7) .................... NucFamGenotypeLikelihood.cpp:1693-1749
+ *   allele switch / counters / de-novo LR ...... main.cpp:539-574
+ *   CalcPostProb (genotype posteriors, GQ, DS) . FamilyLikelihoodSeq.cpp:74-89, NucFamGenotypeLikelihood.cpp:590-868
+ *   CalculateAB ................................ NucFamGenotypeLikelihood.cpp:1006-1039
+ *
+ * VCF text formatting (OutputVCF, NucFamGenotypeLikelihood.cpp:1751-1915) stays on the host.
+ *
+ * Conventions: plain C types, caller-owned buffers, no global state except the thread-local last-error
+ * string.  Every entry point returns 0 on success and a negative pm_status on failure; the message is
+ * available from pm_last_error().  All computation is FP64 on the GPU; there is no CPU fallback -- a
+ * missing/failed HIP device makes pm_engine_create fail loudly.
+ */
+#ifndef POLYMUTT_ENGINE_H
+#define POLYMUTT_ENGINE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PM_ABI_VERSION 1
+#define PM_NCFG 7           /* varllk slots: 0 mono, 1 ref/ts, 2 ref/tv1, 3 ref/tv2, 4 ts/tv1, 5 ts/tv2, 6 tv1/tv2 */
+
+typedef enum { PM_OK = 0, PM_EINVAL = -1, PM_EHIP = -2, PM_ENOMEM = -3, PM_EBRENT = -4, PM_EPED = -5 } pm_status;
+
+/* chromosome class of the current GLF section (main.cpp:312-315) */
+typedef enum { PM_CHR_AUTO = 0, PM_CHR_X = 1, PM_CHR_Y = 2, PM_CHR_MT = 3 } pm_chrom;
+
+/* How FamilyLikelihoodSeq::CalcAllFamLogLikelihood treats a family (FamilyLikelihoodSeq.cpp:228-234):
+ * all-founder families -> product of single-person likelihoods (NucFamGenotypeLikelihood.cpp:943-949),
+ * isNuclear() families -> closed form over 9 parental genotype pairs (:1041-1084),
+ * everything else       -> Elston-Stewart peeling (FamilyLikelihoodES.cpp:1013-1057). */
+typedef enum { PM_FAM_NUCLEAR = 0, PM_FAM_FOUNDERS = 1, PM_FAM_EXTENDED = 2 } pm_fam_kind;
+
+/* One Elston-Stewart peeling step (ES_Peeling::from/to/peelingType, FamilyLikelihoodES.h:29-31).
+ * Indices are family-local positions in Family::path (founders first). */
+typedef struct {
+  int32_t type;           /* 1 offspring->parents, 2 spouse->spouse, 3 parents->only offspring */
+  int32_t from0, from1;   /* from1 = -1 unless type 3 (father, mother)            */
+  int32_t to0, to1;       /* to1   = -1 unless type 1 (father, mother)            */
+} pm_peel_step;
+
+/* Flattened pedigree.  Persons are numbered in VCF column order: families in Pedigree order, members
+ * in Family::path order (core/PedigreeFamily.cpp:11-85) -- i.e. exactly pedGLF->glf[i][j]. */
+typedef struct {
+  int32_t n_fam;
+  int32_t n_person;
+  const int32_t *fam_start;    /* [n_fam+1] first person of each family                         */
+  const int32_t *fam_founders; /* [n_fam]  Family::founders                                      */
+  const int32_t *fam_kind;     /* [n_fam]  pm_fam_kind                                           */
+  const int8_t  *sex;          /* [n_person] 0 unknown, 1 male, 2 female (PedigreeGLF::sexes)    */
+  const int8_t  *is_founder;   /* [n_person] Person::isFounder()                                 */
+  const int32_t *peel_start;   /* [n_fam+1] offsets into steps (empty range for non-extended)    */
+  const pm_peel_step *steps;   /* ES_Peeling::BuildPeelingOrder output, per extended family      */
+  int32_t n_founders;          /* PedigreeGLF::nFounders   (sum of Family::founders)             */
+  int32_t male_founders;       /* PedigreeGLF::maleFounders                                      */
+  int32_t female_founders;     /* PedigreeGLF::femaleFounders                                    */
+} pm_pedigree;
+
+/* Command-line parameters that reach the model (CmdLinePar, src/CmdLinePar.h; defaults main.cpp:59-85). */
+typedef struct {
+  double  theta;               /* --theta 1e-3 */
+  double  poly_tstv;           /* --poly_tstv 2 */
+  double  precision;           /* --prec 1e-4 (Brent tol) */
+  double  posterior;           /* -c 0.5 */
+  int32_t min_total_depth;     /* --minDepth */
+  int32_t max_total_depth;     /* --maxDepth (0 = off) */
+  double  min_ps;              /* --minPercSampleWithData */
+  int32_t min_map_quality;     /* --minMapQuality */
+  int32_t denovo;              /* --denovo */
+  double  denovo_mut_rate;     /* --rate_denovo 1.5e-8 */
+  double  denovo_tstv;         /* --tstv_denovo 2 */
+  double  denovo_min_llr;      /* --minLLR_denovo 0.01 */
+  int32_t force_call;          /* set by --pos */
+  int32_t all_sites;           /* --all_sites */
+  int32_t quick_call;          /* --quick_call */
+} pm_params;
+
+/* Site status codes (which `continue` of main.cpp:300-594 was taken). */
+typedef enum {
+  PM_SITE_CALLED = 0,          /* evaluated; see emit */
+  PM_SITE_MIN_DEPTH = 1, PM_SITE_MAX_DEPTH = 2, PM_SITE_MIN_PS = 3, PM_SITE_MIN_MAPQ = 4,
+  PM_SITE_BAD_REF = 5,         /* refBase not in 1..4 (main.cpp:340) */
+  PM_SITE_QUICK_SKIP = 7       /* rejected by the --quick_call pre-filter (main.cpp:432-433) */
+} pm_site_status;
+
+/* Genotype-label flavour of a person in an emitted record (the four labellers of
+ * NucFamGenotypeLikelihood.cpp:1573-1608 plus the chrY-female "."). */
+typedef enum { PM_LBL_VCF_DIPLOID = 0, PM_LBL_VCF_HAPLOID = 1, PM_LBL_ALLELES = 2, PM_LBL_GENO10 = 3, PM_LBL_DOT = 4 } pm_label_kind;
+
+/* Per-site result (8-byte aligned, 224 bytes). */
+typedef struct {
+  int32_t status;              /* pm_site_status */
+  int32_t n_cfg;               /* 4 or 7 configurations evaluated */
+  int32_t maxidx;              /* CalcVarPosterior argmax */
+  int32_t emit;                /* 1: a VCF record is written for this site */
+  int32_t total_depth;
+  int32_t num_samp_with_data;
+  double  avg_map_qual;
+  double  perc_samp_with_data;
+  double  var_post_prob;
+  double  poly_qual;
+  double  varllk[PM_NCFG];
+  double  varfreq[PM_NCFG];    /* Brent minimiser per configuration (1.0 for mono) */
+  int32_t evals[PM_NCFG];      /* objective evaluations per configuration */
+  int32_t allele1, allele2;    /* famlk[0] alleles at output time (1..4) */
+  int32_t is_mono;             /* famlk[0].isMono for the record (BA= tag) */
+  int32_t denovo_mono;         /* OutputVCF_denovo prints ALT=allele1 */
+  double  af;                  /* GetMinimizer() printed as AF */
+  double  ab;                  /* CalculateAB */
+  double  denovo_lr;           /* DQ */
+  int32_t call_row;            /* row of pm_geno_call output for this site, -1 if none */
+  int32_t _pad;
+} pm_site_result;
+
+/* Per-person genotype call of an emitted record (16 bytes). */
+typedef struct {
+  double  dosage;              /* DS */
+  int16_t best;                /* bestGenoIdx (0..2, or 0..9 for de-novo kids) */
+  int16_t gq;                  /* GQ */
+  int8_t  label;               /* pm_label_kind */
+  int8_t  _pad[3];
+} pm_geno_call;
+
+/* Summary counters of one section (main.cpp:264-282, printed :596-619); summed over shards/GPUs. */
+typedef struct {
+  int64_t ref_base_counts[5];
+  int64_t min_total_depth_filter, max_total_depth_filter, min_ps_filter, min_map_qual_filter;
+  int64_t homo_ref, transitions, transversions, tstvs1, tstvs2, tvs1tvs2, nocall;
+} pm_counters;
+
+typedef struct pm_engine pm_engine;
+
+/* Create an engine on HIP device `device` (one engine per GPU; engines are independent and thread-safe
+ * with respect to each other).  max_batch bounds the sites per pm_engine_run call. */
+int pm_engine_create(const pm_pedigree *ped, const pm_params *par, int device, int max_batch, pm_engine **out);
+void pm_engine_destroy(pm_engine *eng);
+
+/* Start a GLF section: sets the chromosome class, recomputes the polymorphism prior
+ * (GetPolyPrior, NucFamGenotypeLikelihood.cpp:295-304) and zeroes the section counters. */
+int pm_engine_begin_section(pm_engine *eng, int32_t chrom);
+
+/* Evaluate n sites.  Inputs are the dense per-site block, persons in pm_pedigree order:
+ *   pl  [n][n_person][10]  phred genotype likelihoods AA,AC,AG,AT,CC,CG,CT,GG,GT,TT (0 when absent)
+ *   dm  [n][n_person]      depth (bits 0-23) | mapQ << 24   (0 when absent)
+ *   ref [n]                refBase 1..4 (anything else -> PM_SITE_BAD_REF)
+ * inputs_on_device != 0: pl/dm/ref are device pointers on this engine's GPU, else host pointers.
+ * Outputs are host pointers: res[n]; calls[n_rows * n_person] receives one row per emitted site
+ * (row index = res[i].call_row, rows numbered in site order); *n_rows is set to the row count.
+ * Counters accumulate into the section totals.  Synchronous. */
+int pm_engine_run(pm_engine *eng, int32_t n, const uint8_t *pl, const uint32_t *dm, const uint8_t *ref,
+                  int32_t inputs_on_device, pm_site_result *res, pm_geno_call *calls, int32_t *n_rows);
+
+/* Device-resident variant for benchmarking / multi-GPU sharding: all pointers are device pointers,
+ * results stay on the device (d_res[n], d_calls[n * n_person] indexed by site), launched on the
+ * engine's stream; returns immediately.  pm_engine_sync waits. */
+int pm_engine_run_device(pm_engine *eng, int32_t n, const uint8_t *d_pl, const uint32_t *d_dm, const uint8_t *d_ref,
+                         pm_site_result *d_res, pm_geno_call *d_calls);
+int pm_engine_sync(pm_engine *eng);
+
+/* Section counters accumulated so far (device -> host copy). */
+int pm_engine_counters(pm_engine *eng, pm_counters *out);
+
+/* Deterministic synthetic GLF block generator on the device (SURVEY.md section 8(d) recipe):
+ * families shaped by the engine's pedigree, 10% polymorphic sites, depth U{8..29}, error 1%. */
+int pm_engine_synth(pm_engine *eng, int32_t n, uint64_t seed, uint64_t site_offset,
+                    uint8_t *d_pl, uint32_t *d_dm, uint8_t *d_ref);
+
+/* Device allocation helpers (so FFI callers need no HIP runtime of their own). */
+int pm_device_alloc(pm_engine *eng, uint64_t bytes, void **d_ptr);
+int pm_device_free(pm_engine *eng, void *d_ptr);
+int pm_copy_to_host(pm_engine *eng, void *h_dst, const void *d_src, uint64_t bytes);
+
+/* Timing of the dominant (Brent) kernel over the last run: launches, summed kernel ms (HIP events on the
+ * engine stream), total objective evaluations and family-evaluations (for roofline accounting). */
+typedef struct { int64_t launches; double kernel_ms; int64_t evals; int64_t fam_evals; double total_ms; } pm_kernel_stats;
+int pm_engine_kernel_stats(pm_engine *eng, pm_kernel_stats *out, int32_t reset);
+
+const char *pm_last_error(void);
+int pm_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* POLYMUTT_ENGINE_H */

@@ -1,0 +1,236 @@
+// driver.cpp -- see driver.h.
+#include "driver.h"
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
+#include "glf.h"
+#include "vcf.h"
+
+namespace pmhost {
+
+pm_params Options::params() const {
+  pm_params p;
+  memset(&p, 0, sizeof(p));
+  p.theta = theta; p.poly_tstv = tstv; p.precision = precision; p.posterior = posterior;
+  p.min_total_depth = minTotalDepth; p.max_total_depth = maxTotalDepth; p.min_ps = minPS; p.min_map_quality = minMapQuality;
+  p.denovo = denovo; p.denovo_mut_rate = denovo_rate; p.denovo_tstv = denovo_tstv; p.denovo_min_llr = denovo_llr;
+  p.force_call = force_call; p.all_sites = all_sites; p.quick_call = quick_call;
+  return p;
+}
+
+Options parse_command_line(int argc, char** argv) {
+  Options o;
+  for (int a = 0; a < argc; a++) { o.cmd += argv[a]; o.cmd += " "; }
+  struct Flag { const char* name; char kind; void* ptr; };   // kind: s string, d double, i int, b bool
+  Flag longFlags[] = {
+      {"in_vcf", 's', &o.vcfInFile}, {"theta", 'd', &o.theta}, {"indel_theta", 'd', &o.theta_indel},
+      {"poly_tstv", 'd', &o.tstv}, {"chrX", 's', &o.chrX}, {"chrY", 's', &o.chrY}, {"MT", 's', &o.MT},
+      {"denovo", 'b', &o.denovo}, {"rate_denovo", 'd', &o.denovo_rate}, {"tstv_denovo", 'd', &o.denovo_tstv},
+      {"minLLR_denovo", 'd', &o.denovo_llr}, {"prec", 'd', &o.precision}, {"nthreads", 'i', &o.nthreads},
+      {"chr2process", 's', &o.chrs2process}, {"minMapQuality", 'i', &o.minMapQuality}, {"minDepth", 'i', &o.minTotalDepth},
+      {"maxDepth", 'i', &o.maxTotalDepth}, {"minPercSampleWithData", 'd', &o.minPS}, {"out_vcf", 's', &o.vcfOutFile},
+      {"pos", 's', &o.positionFile}, {"all_sites", 'b', &o.all_sites}, {"gl_off", 'b', &o.gl_off},
+      {"quick_call", 'b', &o.quick_call},
+      // engine options (not in the reference)
+      {"gpu", 'i', &o.device}, {"batch", 'i', &o.batch},
+  };
+  auto assign = [](Flag& f, const char* v) {
+    switch (f.kind) {
+      case 's': *(std::string*)f.ptr = v; break;
+      case 'd': *(double*)f.ptr = atof(v); break;
+      case 'i': *(int*)f.ptr = atoi(v); break;
+    }
+  };
+  for (int a = 1; a < argc; a++) {
+    const char* s = argv[a];
+    if (s[0] == '-' && s[1] == '-') {
+      std::string name = s + 2, val;
+      size_t eq = name.find('=');
+      bool hasEq = eq != std::string::npos;
+      if (hasEq) { val = name.substr(eq + 1); name = name.substr(0, eq); }
+      bool found = false;
+      for (auto& f : longFlags) {
+        if (name != f.name) continue;
+        found = true;
+        if (f.kind == 'b') { *(bool*)f.ptr = true; break; }
+        if (!hasEq) {
+          if (a + 1 >= argc) throw FatalError(std::string("Missing value for option --") + name + "\n");
+          val = argv[++a];
+        }
+        assign(f, val.c_str());
+        break;
+      }
+      if (!found) throw FatalError(std::string("Unrecognized option --") + name + "\n");
+    } else if (s[0] == '-' && s[1] && strchr("pdgc", s[1])) {
+      const char* v = s[2] ? s + 2 : (a + 1 < argc ? argv[++a] : "");
+      switch (s[1]) {
+        case 'p': o.pedFile = v; break;
+        case 'd': o.datFile = v; break;
+        case 'g': o.glfListFile = v; break;
+        case 'c': o.posterior = atof(v); break;
+      }
+    } else {
+      throw FatalError(std::string("Unrecognized argument ") + s + "\n");
+    }
+  }
+  return o;
+}
+
+namespace {
+
+void print_status(const Options& o) {   // abbreviated ParameterList::Status banner
+  printf("\nThe following parameters are in effect:\n");
+  printf("%30s : %s\n%30s : %s\n%30s : %s\n%30s : %g\n", "pedfile", o.pedFile.c_str(), "datfile", o.datFile.c_str(), "glfIndexFile",
+         o.glfListFile.c_str(), "posterior cutoff", o.posterior);
+  printf("%30s : theta=%g poly_tstv=%g prec=%g denovo=%s rate_denovo=%g minDepth=%d maxDepth=%d minMapQuality=%d out_vcf=%s\n\n",
+         "Additional Options", o.theta, o.tstv, o.precision, o.denovo ? "ON" : "OFF", o.denovo_rate, o.minTotalDepth, o.maxTotalDepth,
+         o.minMapQuality, o.vcfOutFile.c_str());
+}
+
+std::map<std::string, int> load_positions(const std::string& file) {   // LoadPositionFile, main.cpp:39-55
+  std::map<std::string, int> m;
+  FILE* fh = fopen(file.c_str(), "r");
+  if (!fh) throw FatalError("Open position file " + file + " failed!\n");
+  char line[65536];
+  while (fgets(line, sizeof(line), fh)) {
+    char a[4096], b[4096];
+    if (sscanf(line, "%4095s %4095s", a, b) < 2) {
+      if (sscanf(line, "%4095s", a) == 1) m[std::string(a) + ":"]++;
+      continue;
+    }
+    m[std::string(a) + ":" + b]++;
+  }
+  fclose(fh);
+  return m;
+}
+
+struct Batch {
+  int n = 0, cap = 0, np = 0;
+  std::vector<uint8_t> pl, ref;
+  std::vector<uint32_t> dm;
+  std::vector<int> pos;
+  std::vector<pm_site_result> res;
+  std::vector<pm_geno_call> calls;
+  void init(int capacity, int nperson) {
+    cap = capacity; np = nperson; n = 0;
+    pl.resize((size_t)cap * np * 10); dm.resize((size_t)cap * np); ref.resize(cap); pos.resize(cap);
+    res.resize(cap); calls.resize((size_t)cap * np);
+  }
+};
+
+}  // namespace
+
+int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval) {
+  print_status(opt);
+  if (opt.vcfInFile == opt.vcfOutFile) throw FatalError("Input and output VCF files are the same!\n");
+  if (opt.pedFile.empty()) throw FatalError("pedFile not provided for input!\n");
+  if (opt.glfListFile.empty() && opt.vcfInFile.empty()) throw FatalError("glfListFile or input VCF file not provided for input!\n");
+  if (opt.vcfOutFile.empty()) throw FatalError("vcfOutFile not provided for output!\n");
+  if (!opt.vcfInFile.empty()) throw FatalError("--in_vcf is not supported by this build yet\n");
+  if (opt.denovo && opt.denovo_llr < 0) throw FatalError("denovo_min_LLR can only be greater than 0 !\n");
+
+  std::map<std::string, int> positionMap;
+  if (!opt.positionFile.empty()) positionMap = load_positions(opt.positionFile);
+
+  SiteSource src;
+  src.open(ped, opt.glfListFile);
+  FILE* vcf = fopen(opt.vcfOutFile.c_str(), "w");
+  if (!vcf) throw FatalError("vcfOutFile can not be opened for output!\n");
+
+  VcfWriter W;
+  W.fh = vcf; W.ped = &ped; W.cmd = opt.cmd; W.minMapQuality = opt.minMapQuality; W.minTotalDepth = opt.minTotalDepth;
+  W.maxTotalDepth = opt.maxTotalDepth; W.posterior = opt.posterior; W.gl_off = opt.gl_off; W.force_call = opt.force_call;
+  W.denovo = opt.denovo;
+
+  std::map<std::string, int> chrSel;
+  {
+    size_t i = 0;
+    const std::string& s = opt.chrs2process;
+    while (i < s.size()) {
+      size_t j = s.find(',', i);
+      if (j == std::string::npos) j = s.size();
+      if (j > i) chrSel[s.substr(i, j - i)]++;
+      i = j + 1;
+    }
+  }
+  const size_t chrSelCount = chrSel.size();
+  time_t t0; time(&t0);
+  printf("Analysis started on %s\n", ctime(&t0));
+
+  const int np = (int)ped.column_pid.size();
+  Batch B;
+  B.init(opt.batch > 0 ? opt.batch : 4096, np);
+  int out_cnt = 0;
+  size_t chrDone = 0;
+
+  while (src.nextSection()) {
+    if (!chrSel.empty() && chrDone >= chrSelCount) break;
+    const std::string label = src.label();
+    if (!chrSel.empty() && chrSel[label] < 1) { while (src.nextBaseEntry()) {} continue; }
+    int chrom = label == opt.chrX ? PM_CHR_X : label == opt.chrY ? PM_CHR_Y : label == opt.MT ? PM_CHR_MT : PM_CHR_AUTO;
+    eval.begin_section(chrom);
+    W.chrom = chrom;
+    chrDone++;
+    int entries = 0;
+    bool stop = false;
+
+    auto flush = [&]() {
+      if (B.n == 0) return;
+      int rows = 0;
+      eval.run(B.n, B.pl.data(), B.dm.data(), B.ref.data(), B.res.data(), B.calls.data(), &rows);
+      for (int i = 0; i < B.n && !stop; i++) {
+        const pm_site_result& r = B.res[i];
+        if (!r.emit) continue;
+        W.output(label, B.pos[i], B.ref[i], r, B.calls.data() + (size_t)r.call_row * np, B.pl.data() + (size_t)i * np * 10,
+                 B.dm.data() + (size_t)i * np);
+        out_cnt++;
+        if (opt.force_call && out_cnt >= (int)positionMap.size()) stop = true;   // main.cpp:593 returns without a summary
+      }
+      B.n = 0;
+    };
+
+    while (src.nextBaseEntry()) {
+      if (entries == 0) entries = src.maxPosition();
+      if (!opt.positionFile.empty()) {
+        std::string key = label + ":" + std::to_string(src.currentPos + 1);
+        if (!positionMap.count(key)) continue;
+      }
+      int i = B.n++;
+      B.pos[i] = src.currentPos + 1;
+      B.ref[i] = (uint8_t)src.refBase;
+      src.fill(B.pl.data() + (size_t)i * np * 10, B.dm.data() + (size_t)i * np);
+      if (B.n == B.cap) flush();
+      if (stop) break;
+    }
+    flush();
+    if (stop) { fflush(vcf); return 0; }
+
+    pm_counters C;
+    eval.counters(&C);
+    long total = 0;
+    for (int k = 0; k < 5; k++) total += C.ref_base_counts[k];
+    long other = C.tstvs1 + C.tstvs2 + C.tvs1tvs2;
+    printf("Summary of reference -- %s\n", label.c_str());
+    printf("Total Entry Count: %9d\n", entries);
+    printf("Total Base Cout: %9ld\n", total);
+    printf("Non-Polymorphic Count: %9ld\n", (long)C.homo_ref);
+    printf("Transition Count: %9ld\n", (long)C.transitions);
+    printf("Transversion Count: %9ld\n", (long)C.transversions);
+    printf("Other Polymorphism Count: %9ld\n", other);
+    printf("Filter counts:\n");
+    printf("\tminMapQual %u\n", (unsigned)C.min_map_qual_filter);
+    printf("\tminTotalDepth %u\n", (unsigned)C.min_total_depth_filter);
+    printf("\tmaxTotalDepth %u\n", (unsigned)C.max_total_depth_filter);
+    printf("Hard to call: %9ld\n", (long)C.nocall);
+    printf("Skipped bases: %u\n", (unsigned)(entries - C.homo_ref - C.transitions - C.transversions - other));
+    time_t t1; time(&t1);
+    printf("Analysis ended on %s\n", ctime(&t1));
+    printf("Running time is %u seconds\n\n", (unsigned)(t1 - t0));
+    fflush(vcf);
+  }
+  fclose(vcf);
+  return 0;
+}
+
+}  // namespace pmhost

@@ -1,0 +1,31 @@
+// vcf.h -- VCF text output, restating NucFamGenotypeLikelihood::OutputVCF / OutputVCF_denovo
+// (src/NucFamGenotypeLikelihood.cpp:1751-1915) from engine results.
+#pragma once
+#include <cstdio>
+#include <string>
+#include "../../include/polymutt_engine.h"
+#include "pedigree.h"
+
+namespace pmhost {
+
+struct VcfWriter {
+  FILE* fh = nullptr;
+  const Pedigree* ped = nullptr;
+  std::string cmd;             // argv joined with single spaces + trailing space (main.cpp:159-164)
+  double minMapQuality = 0;    // printed %f (CmdLinePar::minMapQuality is a double)
+  int minTotalDepth = 0, maxTotalDepth = 0;
+  double posterior = 0.5;
+  bool gl_off = false, force_call = false, denovo = false;
+  bool header_written = false;
+  int chrom = PM_CHR_AUTO;
+
+  // One OutputVCF(_denovo) call: writes the header on first use, then the record unless suppressed.
+  void output(const std::string& label, int pos1, int refBase, const pm_site_result& r, const pm_geno_call* calls,
+              const uint8_t* pl, const uint32_t* dm);
+
+ private:
+  void header();
+  bool singleNuclear() const;
+};
+
+}  // namespace pmhost
