@@ -64,6 +64,8 @@ typedef struct {
   const int32_t *fam_kind;     /* [n_fam]  pm_fam_kind                                           */
   const int8_t  *sex;          /* [n_person] 0 unknown, 1 male, 2 female (PedigreeGLF::sexes)    */
   const int8_t  *is_founder;   /* [n_person] Person::isFounder()                                 */
+  const int32_t *father;       /* [n_person] person index of the father, -1 for founders          */
+  const int32_t *mother;       /* [n_person] person index of the mother, -1 for founders          */
   const int32_t *peel_start;   /* [n_fam+1] offsets into steps (empty range for non-extended)    */
   const pm_peel_step *steps;   /* ES_Peeling::BuildPeelingOrder output, per extended family      */
   int32_t n_founders;          /* PedigreeGLF::nFounders   (sum of Family::founders)             */
@@ -102,12 +104,12 @@ typedef enum {
  * NucFamGenotypeLikelihood.cpp:1573-1608 plus the chrY-female "."). */
 typedef enum { PM_LBL_VCF_DIPLOID = 0, PM_LBL_VCF_HAPLOID = 1, PM_LBL_ALLELES = 2, PM_LBL_GENO10 = 3, PM_LBL_DOT = 4 } pm_label_kind;
 
-/* Per-site result (8-byte aligned, 224 bytes). */
+/* Per-site result (240 bytes, naturally aligned, no implicit padding). */
 typedef struct {
   int32_t status;              /* pm_site_status */
   int32_t n_cfg;               /* 4 or 7 configurations evaluated */
   int32_t maxidx;              /* CalcVarPosterior argmax */
-  int32_t emit;                /* 1: a VCF record is written for this site */
+  int32_t emit;                /* 1: a VCF record is written; 2: OutputVCF_denovo called but record suppressed */
   int32_t total_depth;
   int32_t num_samp_with_data;
   double  avg_map_qual;
@@ -116,15 +118,14 @@ typedef struct {
   double  poly_qual;
   double  varllk[PM_NCFG];
   double  varfreq[PM_NCFG];    /* Brent minimiser per configuration (1.0 for mono) */
+  double  af;                  /* GetMinimizer() printed as AF */
+  double  ab;                  /* CalculateAB */
+  double  denovo_lr;           /* DQ */
   int32_t evals[PM_NCFG];      /* objective evaluations per configuration */
   int32_t allele1, allele2;    /* famlk[0] alleles at output time (1..4) */
   int32_t is_mono;             /* famlk[0].isMono for the record (BA= tag) */
   int32_t denovo_mono;         /* OutputVCF_denovo prints ALT=allele1 */
-  double  af;                  /* GetMinimizer() printed as AF */
-  double  ab;                  /* CalculateAB */
-  double  denovo_lr;           /* DQ */
   int32_t call_row;            /* row of pm_geno_call output for this site, -1 if none */
-  int32_t _pad;
 } pm_site_result;
 
 /* Per-person genotype call of an emitted record (16 bytes). */

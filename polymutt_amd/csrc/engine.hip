@@ -1,0 +1,1412 @@
+// engine.hip -- MI355X (gfx950) engine for polyMutt's per-site family likelihood.
+//
+// One call (pm_engine_run / pm_engine_run_device) replaces the body of the reference's site loop
+// (src/main.cpp:327-589) for a whole batch of sites resident in HBM.  Pipeline per batch:
+//
+//   k_prep      block/site   CalcReadStats + filters + MonomorphismLogLikelihood (exact serial sum)
+//                            -> enqueue Brent work items (site, configuration)
+//   k_brent     block/item   OptimizeFrequency + Brent (core/MathGold.cpp:81-177) over the objective
+//                            -CalcAllFamLogLikelihood(freq) (src/FamilyLikelihoodSeq.cpp:222-240):
+//                            families spread over the block's lanes, the freq-independent part of every
+//                            family term hoisted into registers once per item, FP64 throughout, one
+//                            deterministic block reduction per objective evaluation
+//   k_select    thread/site  CalcVarPosterior(4) (NucFamGenotypeLikelihood.cpp:1693-1749) -> 3 more items
+//   k_brent                  the less-likely configurations (main.cpp:499-537)
+//   k_finalize  thread/site  CalcVarPosterior(7), allele switch, counters, de-novo LR (main.cpp:539-574)
+//   k_brent                  (--denovo) the non-de-novo re-optimisation of main.cpp:569-572
+//   k_final_dn  thread/site  (--denovo) denovoLR
+//   k_posterior block/site   CalcPostProb (genotype posteriors), GQ, DS, CalculateAB for emitted sites
+//
+// Design notes: the path is FP64-VALU/transcendental bound, not a GEMM, so no MFMA.
+// Compiled with -ffp-contract=off so every multiply/add rounds exactly like the reference's SSE2 code;
+// the only deviations from the reference's arithmetic are OCML log10/exp10 (<=1 ulp) and the order of
+// the cross-family reduction inside the Brent objective (a fixed tree, deterministic for any batch).
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+#include "../../include/polymutt_engine.h"
+#include "synth_core.h"
+
+#define MALE 1
+#define FEMALE 2
+
+// ------------------------------------------------------------------------------------------------
+// error reporting (thread-local, C ABI)
+static thread_local std::string g_last_error;
+extern "C" void pm_set_last_error(const char* msg) { g_last_error = msg ? msg : ""; }
+extern "C" const char* pm_last_error(void) { return g_last_error.c_str(); }
+extern "C" int pm_abi_version(void) { return PM_ABI_VERSION; }
+
+#define HIP_TRY(expr)                                                                       \
+  do {                                                                                      \
+    hipError_t _e = (expr);                                                                 \
+    if (_e != hipSuccess) {                                                                 \
+      char _b[512];                                                                         \
+      snprintf(_b, sizeof(_b), "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__, __LINE__); \
+      pm_set_last_error(_b);                                                                \
+      return PM_EHIP;                                                                       \
+    }                                                                                       \
+  } while (0)
+
+// ------------------------------------------------------------------------------------------------
+// work-unit plan: families are dealt to the lanes of a Brent block; each lane owns up to S units
+enum UnitType { U_NONE = 0, U_NUC = 1, U_FP = 2 /* founders-only chunk of <=3 persons */, U_EXT = 3 };
+// unit = int4 {type, family, first person (global), count | FIRST<<8 | LAST<<9}
+#define UF_FIRST 0x100
+#define UF_LAST 0x200
+
+// Brent item encoding: site << 3 | cfg.  cfg 0: de-novo monomorphism (single eval at 1.0);
+// 1..6: the six allele configurations; 7: non-de-novo re-optimisation for the de-novo LR.
+#define N_LISTS 3
+
+struct DevArgs {
+  // pedigree
+  int n_fam, n_person, n_fam_gt1, single_nuclear;
+  int chrom, denovo;
+  const int* fam_start;
+  const int* fam_kind;
+  const int8_t* sex;
+  const int32_t* fa_local;
+  const int32_t* mo_local;
+  const int4* units;       // [S][T]
+  int T, S;
+  // tables
+  const double* lktab;     // [256]
+  const double* M;         // [100] genotype mutation matrix
+  const pm_synth_tables* syn;
+  // parameters
+  double precision, posterior, theta;
+  int min_total_depth, max_total_depth, min_map_quality;
+  double min_ps, denovo_min_llr, log10_denovo_min_llr;
+  int force_call, all_sites;
+  double lp_mono, lp_ts, lp_tv, lp_other, np_ts, np_tv;   // log10 prior constants (host glibc)
+  // batch
+  int n;
+  const uint8_t* pl;
+  const uint32_t* dm;
+  const uint8_t* ref;
+  pm_site_result* res;
+  pm_geno_call* calls;
+  double* raw;             // [n][8] log-likelihood per configuration (without prior)
+  double* minv;            // [n][8] Brent minimiser
+  int* evals;              // [n][8]
+  double* mono_plain;      // [n] MonomorphismLogLikelihood
+  int8_t* item_sex;        // [n] member `sex` of famlk[0] for the cfg-7 item
+  int* items[N_LISTS];
+  int* counts;             // [N_LISTS] + [3] rows + [4] first_emit + [5] err + [6] evals_total(lo)
+  unsigned long long* eval_total;
+  int* row_site;           // [n] emitted row -> site
+  unsigned long long* counters;   // pm_counters as 16 x u64
+  int carry_postprob;      // famlk[0].CalcPostProb ran in an earlier batch
+};
+
+// ------------------------------------------------------------------------------------------------
+// small helpers (restating src/PedigreeGLF.h:14-53, core/glfHandler.h:102-106)
+__device__ __forceinline__ int d_gi(int b1, int b2) {
+  return b1 < b2 ? (b1 - 1) * (10 - b1) / 2 + (b2 - b1) : (b2 - 1) * (10 - b2) / 2 + (b1 - b2);
+}
+__device__ __forceinline__ int d_ts(int r) { return r == 1 ? 3 : r == 2 ? 4 : r == 3 ? 1 : 2; }
+__device__ __forceinline__ int d_tv1(int r) { return (r == 1 || r == 3) ? 2 : 1; }
+__device__ __forceinline__ int d_tv2(int r) { return (r == 1 || r == 3) ? 4 : 3; }
+__device__ __forceinline__ double d_sign(double a, double b) { return b >= 0 ? fabs(a) : -fabs(a); }
+
+__device__ __forceinline__ void cfg_alleles(int cfg, int r, int* a1, int* a2) {
+  const int ts = d_ts(r), tv1 = d_tv1(r), tv2 = d_tv2(r);
+  switch (cfg) {
+    case 0: *a1 = r; *a2 = (r == 4) ? 3 : r + 1; break;   // main.cpp:458
+    case 1: *a1 = r; *a2 = ts; break;
+    case 2: *a1 = r; *a2 = tv1; break;
+    case 3: *a1 = r; *a2 = tv2; break;
+    case 4: *a1 = ts; *a2 = tv1; break;
+    case 5: *a1 = ts; *a2 = tv2; break;
+    default: *a1 = tv1; *a2 = tv2; break;
+  }
+}
+
+// likelihoodONEKid, NucFamGenotypeLikelihood.cpp:1202-1264 (member `sex`, X/Y/MT branches)
+__device__ __forceinline__ double d_one_kid(int k, int chrom, int sex, double l11, double l12, double l22) {
+  const bool X = chrom == PM_CHR_X, Y = chrom == PM_CHR_Y, MT = chrom == PM_CHR_MT;
+  switch (k) {
+    case 0: return (Y && sex == FEMALE) ? 1.0 : l11;
+    case 1: if (X) return sex == MALE ? 0.5 * (l11 + l22) : 0.5 * (l11 + l12);
+            if (Y) return sex == MALE ? l11 : 1.0;
+            if (MT) return 0.5 * (l11 + l22);
+            return 0.5 * (l11 + l12);
+    case 2: if (X) return sex == MALE ? l22 : l12;
+            if (Y) return sex == MALE ? l11 : 1.0;
+            if (MT) return l22;
+            return l12;
+    case 3: if (X || Y || MT) return 0.0; return 0.5 * (l11 + l12);
+    case 4: if (X || Y || MT) return 0.0; return 0.25 * l11 + 0.5 * l12 + 0.25 * l22;
+    case 5: if (X || Y || MT) return 0.0; return 0.5 * (l12 + l22);
+    case 6: if (X) return sex == MALE ? l11 : l12;
+            if (Y) return sex == MALE ? l22 : 1.0;
+            if (MT) return l11;
+            return l12;
+    case 7: if (X) return sex == MALE ? 0.5 * (l11 + l22) : 0.5 * (l12 + l22);
+            if (Y) return sex == MALE ? l22 : 1.0;
+            if (MT) return 0.5 * (l11 + l22);
+            return 0.5 * (l12 + l22);
+    default: return (Y && sex == FEMALE) ? 1.0 : l22;
+  }
+}
+
+// likelihoodONEKid_denovo (:1266-1296) from the three CalcDenovoMutLk dot products (:1553-1562)
+__device__ __forceinline__ double d_one_kid_dn(int k, double D11, double D12, double D22) {
+  switch (k) {
+    case 0: return D11;
+    case 1: case 3: return 0.5 * (D11 + D12);
+    case 2: case 6: return D12;
+    case 4: return 0.25 * D11 + 0.5 * D12 + 0.25 * D22;
+    case 5: case 7: return 0.5 * (D12 + D22);
+    default: return D22;
+  }
+}
+
+// Prior modes of the nuclear closed form
+enum PriorMode { PR_AUTO = 0, PR_X, PR_Y, PR_MT, PR_TRIO, PR_DN_SINGLE };
+
+// SetParentPrior (:318-368), SetParentPrior_denovo (:370-381), SetParentPriorSingleTrio(_denovo) (:383-420)
+__device__ __forceinline__ void d_parent_prior(int mode, double f, double* p) {
+  if (mode == PR_DN_SINGLE) mode = (f != 1.0) ? PR_TRIO : PR_AUTO;
+  const double g = 1 - f;
+  switch (mode) {
+    case PR_AUTO:
+      p[0] = (f * f) * (f * f);
+      p[1] = f * f * f * g * 2;
+      p[2] = f * f * g * g;
+      p[3] = f * g * 2 * f * f;
+      p[4] = f * g * 2 * f * g * 2;
+      p[5] = f * g * 2 * g * g;
+      p[6] = g * g * f * f;
+      p[7] = g * g * f * g * 2;
+      p[8] = g * g * g * g;
+      break;
+    case PR_X:
+      p[0] = (f * f) * f; p[1] = f * f * g * 2; p[2] = f * g * g; p[3] = 0; p[4] = 0; p[5] = 0;
+      p[6] = g * f * f; p[7] = g * f * g * 2; p[8] = g * g * g;
+      break;
+    case PR_Y:
+      p[0] = f; p[1] = f; p[2] = f; p[3] = 0; p[4] = 0; p[5] = 0; p[6] = g; p[7] = g; p[8] = g;
+      break;
+    case PR_MT:
+      p[0] = f * f; p[1] = 0.0; p[2] = f * g; p[3] = 0; p[4] = 0; p[5] = 0; p[6] = g * f; p[7] = 0; p[8] = g * g;
+      break;
+    default:
+      p[0] = 0.0; p[1] = 0.24; p[2] = 0.04; p[3] = 0.24; p[4] = 0.16; p[5] = 0.08; p[6] = 0.04; p[7] = 0.08; p[8] = 0.12;
+      break;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// hoisting: the freq-independent part of one unit for one (site, allele pair, model)
+struct ItemCtx {
+  int a1, a2, g11, g12, g22;
+  int denovo;      // objective uses the de-novo model
+  int sex;         // member sex of the evaluating object
+  int chrom;
+};
+
+__device__ __forceinline__ void hoist_nuc(const DevArgs& A, const ItemCtx& I, const uint8_t* pl, const double* lk, const double* M,
+                                          int p0, int n, double* cond) {
+  const uint8_t* F = pl + (size_t)p0 * 10;
+  const uint8_t* Mo = F + 10;
+  double F11 = lk[F[I.g11]], F12 = lk[F[I.g12]], F22 = lk[F[I.g22]];
+  double M11 = lk[Mo[I.g11]], M12 = lk[Mo[I.g12]], M22 = lk[Mo[I.g22]];
+  if (!I.denovo) {   // CalcParentMarginal :1049-1051
+    if (I.chrom == PM_CHR_X) F12 = 0.0;
+    if (I.chrom == PM_CHR_Y) { M11 = M12 = M22 = 1.0; F12 = 0.0; }
+    if (I.chrom == PM_CHR_MT) F12 = M12 = 0.0;
+  }
+  double kids[9];
+#pragma unroll
+  for (int k = 0; k < 9; k++) kids[k] = 1.0;
+  for (int j = 2; j < n; j++) {
+    const uint8_t* K = pl + (size_t)(p0 + j) * 10;
+    if (!I.denovo) {
+      const double l11 = lk[K[I.g11]], l12 = lk[K[I.g12]], l22 = lk[K[I.g22]];
+#pragma unroll
+      for (int k = 0; k < 9; k++) kids[k] *= d_one_kid(k, I.chrom, I.sex, l11, l12, l22);
+    } else {
+      double D11 = 0.0, D12 = 0.0, D22 = 0.0;
+#pragma unroll
+      for (int g = 0; g < 10; g++) {
+        const double pg = lk[K[g]];
+        D11 += M[I.g11 * 10 + g] * pg;
+        D12 += M[I.g12 * 10 + g] * pg;
+        D22 += M[I.g22 * 10 + g] * pg;
+      }
+#pragma unroll
+      for (int k = 0; k < 9; k++) kids[k] *= d_one_kid_dn(k, D11, D12, D22);
+    }
+  }
+  const double lF[3] = {F11, F12, F22}, lM[3] = {M11, M12, M22};
+#pragma unroll
+  for (int a = 0; a < 3; a++)
+#pragma unroll
+    for (int b = 0; b < 3; b++) cond[3 * a + b] = kids[3 * a + b] * (lF[a] * lM[b]);
+}
+
+// founders-only chunk: per person (l11, l12, l22) + per-person flags (bit0 haploid, bit1 skip)
+__device__ __forceinline__ int hoist_fp(const DevArgs& A, const ItemCtx& I, const uint8_t* pl, const double* lk, int p, int cnt,
+                                        double* cond) {
+  int fl = 0;
+  for (int j = 0; j < 3; j++) {
+    if (j >= cnt) { cond[3 * j] = cond[3 * j + 1] = cond[3 * j + 2] = 0.0; fl |= 2 << (2 * j); continue; }
+    const uint8_t* R = pl + (size_t)(p + j) * 10;
+    double l11 = lk[R[I.g11]], l12 = lk[R[I.g12]], l22 = lk[R[I.g22]];
+    const int sx = A.sex[p + j];
+    int hap = 0, skip = 0;   // lkSinglePerson :987-1004
+    if (I.chrom == PM_CHR_X && sx == MALE) { l12 = 0; hap = 1; }
+    if (I.chrom == PM_CHR_Y) { if (sx == MALE) { l12 = 0; hap = 1; } else skip = 1; }
+    if (I.chrom == PM_CHR_MT) { l12 = 0; hap = 1; }
+    cond[3 * j] = l11; cond[3 * j + 1] = l12; cond[3 * j + 2] = l22;
+    fl |= (hap | (skip << 1)) << (2 * j);
+  }
+  return fl;
+}
+
+// ------------------------------------------------------------------------------------------------
+template <int T>
+__device__ __forceinline__ double block_sum(double x, double* red, int& par) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);   // commutative butterfly: identical in all lanes
+  if (T == 64) return x;
+  constexpr int W = T / 64;
+  if ((threadIdx.x & 63) == 0) red[par * 16 + (threadIdx.x >> 6)] = x;
+  __syncthreads();
+  double s = red[par * 16];
+#pragma unroll
+  for (int i = 1; i < W; i++) s += red[par * 16 + i];
+  par ^= 1;
+  return s;
+}
+
+template <int T>
+__device__ __forceinline__ void block_sum3(double& x, double& y, double& z, double* red, int& par) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { x += __shfl_xor(x, o, 64); y += __shfl_xor(y, o, 64); z += __shfl_xor(z, o, 64); }
+  if (T == 64) return;
+  constexpr int W = T / 64;
+  if ((threadIdx.x & 63) == 0) {
+    red[par * 16 + (threadIdx.x >> 6)] = x;
+    red[32 + par * 16 + (threadIdx.x >> 6)] = y;
+    red[64 + par * 16 + (threadIdx.x >> 6)] = z;
+  }
+  __syncthreads();
+  double sx = red[par * 16], sy = red[32 + par * 16], sz = red[64 + par * 16];
+#pragma unroll
+  for (int i = 1; i < W; i++) { sx += red[par * 16 + i]; sy += red[32 + par * 16 + i]; sz += red[64 + par * 16 + i]; }
+  x = sx; y = sy; z = sz;
+  par ^= 1;
+}
+
+// per-lane partial of CalcAllFamLogLikelihood(freq) over the lane's units
+template <int S>
+__device__ __forceinline__ double lane_loglik(double f, const int4* unit, const double (*cond)[9], const int* fl, int pmode) {
+  double pp[9];
+  d_parent_prior(pmode, f, pp);
+  const double g = 1 - f;
+  const double P0 = f * f, P1 = f * g * 2, P2 = g * g;   // lkSinglePerson priors
+  double part = 0.0, prod = 1.0;
+#pragma unroll
+  for (int s = 0; s < S; s++) {
+    const int ty = unit[s].x;
+    if (ty == U_NUC) {
+      double v = 0.0;   // lkSingleFam :950-955
+#pragma unroll
+      for (int k = 0; k < 9; k++) v += cond[s][k] * pp[k];
+      part += log10(v);
+    } else if (ty == U_FP) {
+      if (unit[s].w & UF_FIRST) prod = 1.0;
+#pragma unroll
+      for (int j = 0; j < 3; j++) {
+        const int b = (fl[s] >> (2 * j)) & 3;
+        if (b & 2) continue;
+        double sp = 0.0;
+        if (b & 1) sp = sp + cond[s][3 * j] * f + cond[s][3 * j + 1] * 0 + cond[s][3 * j + 2] * g;
+        else sp = sp + cond[s][3 * j] * P0 + cond[s][3 * j + 1] * P1 + cond[s][3 * j + 2] * P2;
+        prod *= sp;
+      }
+      if (unit[s].w & UF_LAST) part += log10(prod);
+    }
+  }
+  return part;
+}
+
+template <int T, int S>
+__global__ void __launch_bounds__(T) k_brent(DevArgs A, int list) {
+  __shared__ double s_lk[256];
+  __shared__ double s_M[100];
+  __shared__ double s_red[96];
+  for (int i = threadIdx.x; i < 256; i += T) s_lk[i] = A.lktab[i];
+  for (int i = threadIdx.x; i < 100; i += T) s_M[i] = A.M[i];
+  __syncthreads();
+  int4 unit[S];
+#pragma unroll
+  for (int s = 0; s < S; s++) unit[s] = A.units[s * T + threadIdx.x];
+  const int nItems = A.counts[list];
+  const int* items = A.items[list];
+  int par = 0;
+  for (int it = blockIdx.x; it < nItems; it += gridDim.x) {
+    const int item = items[it];
+    const int site = item >> 3, cfg = item & 7;
+    const int r = A.ref[site];
+    ItemCtx I;
+    if (cfg == 7) { I.a1 = A.res[site].allele1; I.a2 = A.res[site].allele2; }
+    else cfg_alleles(cfg, r, &I.a1, &I.a2);
+    I.g11 = d_gi(I.a1, I.a1); I.g12 = d_gi(I.a1, I.a2); I.g22 = d_gi(I.a2, I.a2);
+    I.denovo = A.denovo && cfg != 7;
+    I.sex = (cfg == 7) ? A.item_sex[site] : 0;
+    I.chrom = A.chrom;
+    int pmode;
+    if (I.denovo) pmode = A.n_fam_gt1 ? PR_AUTO : PR_DN_SINGLE;
+    else if (!A.n_fam_gt1) pmode = PR_TRIO;   // isMono is never set on the evaluating objects
+    else pmode = A.chrom == PM_CHR_X ? PR_X : A.chrom == PM_CHR_Y ? PR_Y : A.chrom == PM_CHR_MT ? PR_MT : PR_AUTO;
+
+    const uint8_t* pl = A.pl + (size_t)site * A.n_person * 10;
+    double cond[S][9];
+    int fl[S];
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      fl[s] = 0;
+      if (unit[s].x == U_NUC) hoist_nuc(A, I, pl, s_lk, s_M, unit[s].z, unit[s].w, cond[s]);
+      else if (unit[s].x == U_FP) fl[s] = hoist_fp(A, I, pl, s_lk, unit[s].z, unit[s].w & 0xFF, cond[s]);
+    }
+    double* raw = A.raw + (size_t)site * 8;
+    const bool single = (cfg == 0) || A.single_nuclear;
+    // One evaluation site for the objective: the three bracketing evaluations of OptimizeFrequency
+    // (:432-444) and every Brent step (core/MathGold.cpp:81-177) run through the same loop body.
+    const double tol = A.precision;
+    double a = 0.0001, b = 0.9999, c = 0.5;
+    double mn = 0, fmin = 0, w = 0, v = 0, fw = 0, fv = 0, delta = 0.0, d = 0.0;
+    double x = single ? ((cfg == 0) ? 1.0 : 0.5) : a;   // MonomorphismLogLikelihood_denovo / single nuclear family at 0.5
+    int phase = 0, iter = 0, nev = 0;
+    bool ok = false;
+    for (;;) {
+      const double tot = block_sum<T>(lane_loglik<S>(x, unit, cond, fl, pmode), s_red, par);
+      nev++;
+      if (single) { mn = 0.0; fmin = -tot; ok = true; break; }
+      const double fx = -tot;
+      if (phase == 0) { phase = 1; x = b; continue; }
+      if (phase == 1) { fmin = fx; phase = 2; x = c; continue; }
+      if (phase == 2) { phase = 3; mn = b; w = b; v = b; fw = fmin; fv = fmin; }   // min = b, fmin = fb
+      else {
+        const double u = x, fu = fx;
+        if (fu <= fmin) {
+          if (u >= mn) a = mn; else c = mn;
+          v = w; w = mn; mn = u;
+          fv = fw; fw = fmin; fmin = fu;
+        } else {
+          if (u < mn) a = u; else c = u;
+          if (fu <= fw || w == mn) { v = w; w = u; fv = fw; fw = fu; }
+          else if (fu <= fv || v == mn || v == w) { v = u; fv = fu; }
+        }
+      }
+      if (++iter > 200) break;   // ITMAX: numerror("ScalarMinimizer::Brent got stuck")
+      const double middle = 0.5 * (a + c);
+      const double tol1 = tol * fabs(mn) + 3.0e-10;
+      const double tol2 = 2.0 * tol1;
+      if (fabs(mn - middle) <= (tol2 - 0.5 * (c - a))) { ok = true; break; }
+      if (fabs(delta) > tol1) {
+        double rr = (mn - w) * (fmin - fv);
+        double q = (mn - v) * (fmin - fw);
+        double p = (mn - v) * q - (mn - w) * rr;
+        q = 2.0 * (q - rr);
+        if (q > 0.0) p = -p;
+        q = fabs(q);
+        const double temp = delta;
+        delta = d;
+        if (fabs(p) >= fabs(0.5 * q * temp) || p <= q * (a - mn) || p >= q * (c - mn)) {
+          delta = mn >= middle ? a - mn : c - mn;
+          d = 0.38196601 * delta;
+        } else {
+          d = p / q;
+          const double u = mn + d;
+          if (u - a < tol2 || c - u < tol2) d = d_sign(tol1, middle - mn);
+        }
+      } else {
+        delta = mn >= middle ? a - mn : c - mn;
+        d = 0.38196601 * delta;
+      }
+      x = fabs(d) >= tol1 ? mn + d : mn + d_sign(tol1, d);
+    }
+    if (threadIdx.x == 0) {
+      raw[cfg] = -fmin;
+      A.minv[site * 8 + cfg] = mn;
+      A.evals[site * 8 + cfg] = nev;
+      if (!single) atomicAdd(A.eval_total, (unsigned long long)nev);
+      if (!ok) atomicExch(&A.counts[5], 1);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_prep: one block per site
+__global__ void __launch_bounds__(256) k_prep(DevArgs A) {
+  __shared__ long long s_sum[4][4];
+  __shared__ uint8_t s_hr[4096];
+  const int site = blockIdx.x;
+  if (site >= A.n) return;
+  const int r = A.ref[site];
+  const int np = A.n_person;
+  const uint8_t* pl = A.pl + (size_t)site * np * 10;
+  const uint32_t* dm = A.dm + (size_t)site * np;
+  pm_site_result* R = A.res + site;
+  const bool okref = r >= 1 && r <= 4;
+  const int h = okref ? d_gi(r, r) : 0;
+  long long dsum = 0, mqsum = 0, nsd = 0;
+  for (int p = threadIdx.x; p < np; p += 256) {
+    const uint32_t x = dm[p];
+    const int d = (int)(x & 0xFFFFFF);
+    dsum += d; mqsum += (x >> 24); nsd += d > 0;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { dsum += __shfl_xor(dsum, o, 64); mqsum += __shfl_xor(mqsum, o, 64); nsd += __shfl_xor(nsd, o, 64); }
+  if ((threadIdx.x & 63) == 0) { s_sum[0][threadIdx.x >> 6] = dsum; s_sum[1][threadIdx.x >> 6] = mqsum; s_sum[2][threadIdx.x >> 6] = nsd; }
+  // MonomorphismLogLikelihood (:502-517): exact serial sum over persons, staged through LDS
+  double mono = 0.0;
+  for (int base = 0; base < np; base += 4096) {
+    const int cnt = min(4096, np - base);
+    __syncthreads();
+    for (int p = threadIdx.x; p < cnt; p += 256) s_hr[p] = pl[(size_t)(base + p) * 10 + h];
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int p = 0; p < cnt; p++) mono += -(double)(s_hr[p]) / 10;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  dsum = s_sum[0][0] + s_sum[0][1] + s_sum[0][2] + s_sum[0][3];
+  mqsum = s_sum[1][0] + s_sum[1][1] + s_sum[1][2] + s_sum[1][3];
+  nsd = s_sum[2][0] + s_sum[2][1] + s_sum[2][2] + s_sum[2][3];
+  memset(R, 0, sizeof(*R));
+  R->maxidx = -2; R->call_row = -1; R->ab = 0.5; R->denovo_lr = -1;
+  A.mono_plain[site] = mono;
+  if (!okref) { R->status = PM_SITE_BAD_REF; return; }
+  atomicAdd(&A.counters[r], 1ull);
+  // CalcReadStats :520-546
+  const int td = (int)dsum, n = (int)nsd;
+  double avgmq = 0., ps = 0.;
+  if (n > 0) { avgmq = (double)mqsum / (double)n; ps = (double)n / (double)np; }
+  R->total_depth = td; R->num_samp_with_data = n; R->avg_map_qual = avgmq; R->perc_samp_with_data = ps;
+  // filters, main.cpp:345-348
+  int st = 0;
+  if (td < A.min_total_depth) st = PM_SITE_MIN_DEPTH;
+  else if (A.max_total_depth > 0 && td > A.max_total_depth) st = PM_SITE_MAX_DEPTH;
+  else if (ps * 100 < A.min_ps) st = PM_SITE_MIN_PS;
+  else if (avgmq < A.min_map_quality) st = PM_SITE_MIN_MAPQ;
+  if (st) { R->status = st; atomicAdd(&A.counters[4 + st], 1ull); return; }
+  R->status = PM_SITE_CALLED;
+  const int nit = A.denovo ? 4 : 3;
+  const int slot = atomicAdd(&A.counts[0], nit);
+  for (int k = 0; k < nit; k++) A.items[0][slot + k] = (site << 3) | (A.denovo ? k : k + 1);
+}
+
+// CalcVarPosterior (:1693-1749); returns maxidx, sets vpp/qual/alleles
+__device__ int d_var_posterior(const double* v, int n, int r, double* vpp, double* qual, int* a1, int* a2) {
+  int idx = 0; double mx = v[0];
+  for (int i = 0; i < n; i++) if (mx < v[i]) { mx = v[i]; idx = i; }
+  double sum = 0.0;
+  for (int i = 0; i < n; i++) sum += exp10(v[i] - v[idx]);
+  *vpp = 1 / sum;
+  const int ts = d_ts(r), tv1 = d_tv1(r), tv2 = d_tv2(r);
+  if (idx == 0) {
+    int k = 1; double m = v[1];
+    for (int i = 1; i < 4; i++) if (m < v[i]) { m = v[i]; k = i; }
+    *a1 = r; *a2 = (k == 1) ? ts : (k == 2) ? tv1 : tv2;
+  } else if (idx == 1) { *a1 = r; *a2 = ts; }
+  else if (idx == 2) { *a1 = r; *a2 = tv1; }
+  else if (idx == 3) { *a1 = r; *a2 = tv2; }
+  else if (idx == 4) { *a1 = ts; *a2 = tv1; }
+  else if (idx == 5) { *a1 = ts; *a2 = tv2; }
+  else { *a1 = tv1; *a2 = tv2; }
+  *qual = (*vpp > 0.9999999999) ? 100 : -10 * log10(1 - *vpp);
+  return idx;
+}
+
+__device__ __forceinline__ void fill_varllk(const DevArgs& A, int site, int n, double* v) {
+  const double* raw = A.raw + (size_t)site * 8;
+  v[0] = A.lp_mono + (A.denovo ? raw[0] : A.mono_plain[site]);
+  v[1] = A.lp_ts + raw[1];
+  v[2] = A.lp_tv + raw[2];
+  v[3] = A.lp_tv + raw[3];
+  for (int k = 4; k < n; k++) v[k] = A.lp_other + raw[k];
+}
+
+__global__ void k_select(DevArgs A) {
+  const int site = blockIdx.x * blockDim.x + threadIdx.x;
+  if (site >= A.n) return;
+  pm_site_result* R = A.res + site;
+  if (R->status != PM_SITE_CALLED) return;
+  double v[7], vpp, q; int a1, a2;
+  fill_varllk(A, site, 4, v);
+  d_var_posterior(v, 4, A.ref[site], &vpp, &q, &a1, &a2);
+  if (vpp < 0.99) {
+    const int slot = atomicAdd(&A.counts[1], 3);
+    for (int k = 0; k < 3; k++) A.items[1][slot + k] = (site << 3) | (4 + k);
+    R->n_cfg = 7;
+  } else R->n_cfg = 4;
+}
+
+// main.cpp:539-574 per site; counters aggregated per block
+__global__ void __launch_bounds__(256) k_finalize(DevArgs A) {
+  __shared__ unsigned long long s_c[16];
+  if (threadIdx.x < 16) s_c[threadIdx.x] = 0;
+  __syncthreads();
+  const int site = blockIdx.x * blockDim.x + threadIdx.x;
+  if (site < A.n && A.res[site].status == PM_SITE_CALLED) {
+    pm_site_result* R = A.res + site;
+    const int r = A.ref[site], ncfg = R->n_cfg;
+    double v[7], vpp, q; int a1, a2;
+    fill_varllk(A, site, ncfg, v);
+    const int maxidx = d_var_posterior(v, ncfg, r, &vpp, &q, &a1, &a2);
+    const double* raw = A.raw + (size_t)site * 8;
+    R->maxidx = maxidx; R->var_post_prob = vpp; R->poly_qual = q;
+    for (int k = 0; k < 7; k++) {
+      R->varllk[k] = k < ncfg ? v[k] : 0.0;
+      R->varfreq[k] = k == 0 ? 1.0 : (k < ncfg ? A.minv[site * 8 + k] : 0.0);
+      R->evals[k] = k < ncfg ? A.evals[site * 8 + k] : 0;
+    }
+    if (!A.denovo) R->evals[0] = 0;
+    R->allele1 = a1; R->allele2 = a2;
+    bool emit = true;
+    const bool fa = A.force_call || A.all_sites;
+    if (vpp < A.posterior) { atomicAdd(&s_c[15], 1ull); if (!fa) emit = false; }
+    double af = 0.0;
+    if (emit) {
+      const int cidx[7] = {9, 10, 11, 11, 12, 13, 14};   // homo_ref, transitions, transversions x2, tstvs1, tstvs2, tvs1tvs2
+      atomicAdd(&s_c[cidx[maxidx]], 1ull);
+      if (maxidx == 0) af = fa ? 1.0 : 0.0;
+      else af = A.minv[site * 8 + maxidx];
+      if (maxidx == 0 && !A.denovo && !fa) emit = false;
+    }
+    if (emit && A.denovo) {
+      if (maxidx == 0) {
+        af = 1.0;
+        // noprior[0] = varllk[0] - log10(1-prior)  (main.cpp:460), lk_mono = MonomorphismLogLikelihood
+        const double dlr = (v[0] - A.lp_mono) - A.mono_plain[site];
+        R->denovo_lr = dlr;
+        if (dlr <= A.log10_denovo_min_llr && !fa) emit = false;
+      }
+    }
+    R->af = af;
+    if (emit) {
+      R->emit = 1;
+      R->is_mono = (!A.denovo && maxidx == 0) ? 1 : 0;
+      R->denovo_mono = (A.denovo && maxidx == 0) ? 1 : 0;
+      atomicMin(&A.counts[4], site);
+      if (A.denovo && maxidx != 0) {
+        const int slot = atomicAdd(&A.counts[2], 1);
+        A.items[2][slot] = (site << 3) | 7;
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 16 && threadIdx.x >= 9 && s_c[threadIdx.x]) {
+    // map to pm_counters layout: [9] homo_ref .. [14] tvs1tvs2, [15] nocall
+    atomicAdd(&A.counters[threadIdx.x], s_c[threadIdx.x]);
+  }
+}
+
+// member `sex` of famlk[0] before site `site`'s CalcPostProb / re-optimisation (non-de-novo only
+// changes it; stale-state quirk of NucFamGenotypeLikelihood::likelihoodONEKid)
+__device__ __forceinline__ int d_member_sex_before(const DevArgs& A, int site) {
+  if (A.denovo) return 0;
+  const bool seen = A.carry_postprob || A.counts[4] < site;
+  return seen ? A.sex[A.n_person - 1] : 0;
+}
+
+__global__ void k_prepare_items7(DevArgs A) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= A.counts[2]) return;
+  const int site = A.items[2][i] >> 3;
+  A.item_sex[site] = (int8_t)d_member_sex_before(A, site);
+}
+
+// --denovo: denovoLR = varllk_noprior[maxidx] - lk_poly (main.cpp:567-573); famlk[0].min is overwritten
+// by that re-optimisation (the printed AF) whenever a Brent ran.
+__global__ void k_final_dn(DevArgs A) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= A.counts[2]) return;
+  const int site = A.items[2][i] >> 3;
+  pm_site_result* R = A.res + site;
+  const int mx = R->maxidx;
+  const double* raw = A.raw + (size_t)site * 8;
+  const double npc = (mx == 1) ? A.np_ts : (mx <= 3 ? A.np_tv : A.lp_other);
+  const double noprior = R->varllk[mx] - npc;
+  R->denovo_lr = noprior - raw[7];
+  if (!A.single_nuclear) R->af = A.minv[site * 8 + 7];
+}
+
+// ------------------------------------------------------------------------------------------------
+// posteriors: one block per emitted site, families across lanes
+__device__ __forceinline__ int d_best3(double p11, double p12, double p22) {
+  int b = 0; double m = p11;
+  if (p12 > m) { m = p12; b = 1; }
+  if (p22 > m) { m = p22; b = 2; }
+  return b;
+}
+__device__ __forceinline__ int8_t d_vcf_label(int chrom, int membersex) {
+  if (chrom == PM_CHR_Y || chrom == PM_CHR_MT) return PM_LBL_VCF_HAPLOID;
+  if (chrom == PM_CHR_X && membersex == MALE) return PM_LBL_VCF_HAPLOID;
+  return PM_LBL_VCF_DIPLOID;
+}
+__device__ __forceinline__ void d_emit_call(pm_geno_call* C, const double* post, int best, int8_t label, double dosage) {
+  const double pb = post[best];
+  const int gq = (pb > 0.9999999999) ? 100 : (int)(-10. * log10(1. - pb) + 0.5);   // OutputVCF :1818-1820
+  pm_geno_call c;
+  c.dosage = dosage; c.best = (int16_t)best; c.gq = (int16_t)gq; c.label = label;
+  c._pad[0] = c._pad[1] = c._pad[2] = 0;
+  *C = c;
+}
+
+// likelihoodKidGenotype, :1334-1443
+__device__ void d_kid_geno(int chrom, const uint8_t* pl, const double* lk, int p0, int n, const int8_t* sexv, int g11, int g12, int g22,
+                           int kid, int k, double* out) {
+  const bool X = chrom == PM_CHR_X, Y = chrom == PM_CHR_Y, MT = chrom == PM_CHR_MT;
+  double G11 = 1.0, G12 = 1.0, G22 = 1.0, l = 0.0, q11 = 0, q12 = 0, q22 = 0;
+  for (int i = 2; i < n; i++) {
+    const uint8_t* R = pl + (size_t)(p0 + i) * 10;
+    const double l11 = lk[R[g11]], l12 = lk[R[g12]], l22 = lk[R[g22]];
+    const int sex = sexv[p0 + i];
+    switch (k) {
+      case 0: l = l11; q11 = l11; q12 = q22 = 0; break;
+      case 1:
+        if (X) { l = sex == MALE ? 0.5 * (l11 + l22) : 0.5 * (l11 + l12);
+                 if (sex == MALE) { q11 = 0.5 * l11; q12 = 0.0; q22 = 0.5 * l22; } else { q11 = 0.5 * l11; q12 = 0.5 * l12; q22 = 0; } }
+        else if (Y) { l = sex == MALE ? l11 : 1.0; if (sex == MALE) { q11 = l11; q12 = q22 = 0.0; } else { q11 = q12 = q22 = 0.0; } }
+        else if (MT) { l = 0.5 * (l11 + l22); q11 = 0.5 * l11; q22 = 0.5 * l22; q12 = 0.0; }
+        else { l = 0.5 * (l11 + l12); q11 = l11 * 0.5; q12 = l12 * 0.5; q22 = 0; }
+        break;
+      case 2:
+        if (X) { l = sex == MALE ? l22 : l12; if (sex == MALE) { q11 = q12 = 0; q22 = l22; } else { q11 = q22 = 0; q12 = l12; } }
+        else if (Y) { l = sex == MALE ? l11 : 1.0; if (sex == MALE) { q11 = l11; q12 = q22 = 0; } else { q11 = q12 = q22 = 0.; } }
+        else if (MT) { l = l22; q11 = q12 = 0; q22 = l22; }
+        else { l = l12; q11 = 0; q12 = l12; q22 = 0; }
+        break;
+      case 3:
+        if (X || Y || MT) { l = 0.0; q11 = q12 = q22 = 0.0; }
+        else { l = 0.5 * (l11 + l12); q11 = l11 * 0.5; q12 = l12 * 0.5; q22 = 0; }
+        break;
+      case 4:
+        if (X || Y || MT) { l = 0.0; q11 = q12 = q22 = 0.0; }
+        else { l = 0.25 * l11 + 0.5 * l12 + 0.25 * l22; q11 = l11 * 0.25; q12 = l12 * 0.5; q22 = l22 * 0.25; }
+        break;
+      case 5:
+        if (X || Y || MT) { l = 0.0; q11 = q12 = q22 = 0.0; }
+        else { l = 0.5 * (l12 + l22); q11 = 0; q12 = l12 * 0.5; q22 = l22 * 0.5; }
+        break;
+      case 6:
+        if (X) { l = sex == MALE ? l11 : l12; if (sex == MALE) { q11 = l11; q12 = q22 = 0.0; } else { q11 = q22 = 0.0; q12 = l12; } }
+        else if (Y) { l = sex == MALE ? l22 : 1.0; if (sex == MALE) { q11 = q12 = 0.0; q22 = l22; } else { q11 = q12 = q22 = 0.0; } }
+        else if (MT) { l = l11; q11 = l11; q12 = q22 = 0.0; }
+        else { l = l12; q11 = 0; q12 = l12; q22 = 0; }
+        break;
+      case 7:
+        if (X) { l = sex == MALE ? 0.5 * (l11 + l22) : 0.5 * (l12 + l22);
+                 if (sex == MALE) { q11 = 0.5 * l11; q22 = 0.5 * l22; q12 = 0.0; } else { q11 = 0.0; q12 = 0.5 * l12; q22 = 0.5 * l22; } }
+        else if (Y) { l = sex == MALE ? l22 : 1.0; if (sex == MALE) { q11 = q12 = 0.0; q22 = l22; } else { q11 = q12 = q22 = 0.0; } }
+        else if (MT) { l = 0.5 * (l11 + l22); q11 = 0.5 * l11; q22 = 0.5 * l22; q12 = 0.0; }
+        else { l = 0.5 * (l12 + l22); q11 = 0; q12 = l12 * 0.5; q22 = l22 * 0.5; }
+        break;
+      default:   // if/if/if-else chain of :1416-1422
+        if (X) { l = l22; q11 = 0.0; q22 = l22; }
+        if (Y) { l = sex == MALE ? l22 : 1.0; if (sex == MALE) { q11 = q12 = 0.0; q22 = l22; } else { q11 = q22 = q12 = 0.0; } }
+        if (MT) { l = l22; q11 = q12 = 0.0; q22 = l22; }
+        else { l = l22; q11 = 0; q12 = 0; q22 = l22; }
+        break;
+    }
+    if (i != kid) { G11 *= l; G12 *= l; G22 *= l; }
+    else { G11 *= q11; G12 *= q12; G22 *= q22; }
+  }
+  out[0] = G11; out[1] = G12; out[2] = G22;
+}
+
+__global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
+  __shared__ double s_lk[256];
+  __shared__ double s_M[100];
+  __shared__ double s_ab[2][256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) s_lk[i] = A.lktab[i];
+  for (int i = threadIdx.x; i < 100; i += blockDim.x) s_M[i] = A.M[i];
+  __syncthreads();
+  const int rows = A.counts[3];
+  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+    const int site = A.row_site[row];
+    const pm_site_result* R = A.res + site;
+    const int np = A.n_person;
+    const uint8_t* pl = A.pl + (size_t)site * np * 10;
+    const uint32_t* dm = A.dm + (size_t)site * np;
+    pm_geno_call* out = A.calls + (size_t)row * np;
+    const int a1 = R->allele1, a2 = R->allele2;
+    const int g11 = d_gi(a1, a1), g12 = d_gi(a1, a2), g22 = d_gi(a2, a2);
+    const int chrom = A.chrom, dn = A.denovo;
+    // CalcPostProb freq (main.cpp:576-587)
+    const double freq = (R->maxidx == 0) ? (dn ? 1.0 : 1 - A.theta) : R->af;
+    const int is_mono = (R->maxidx == 0 && !dn) ? 1 : 0;
+    const int sex_carry = d_member_sex_before(A, site);
+    for (int f = threadIdx.x; f < A.n_fam; f += blockDim.x) {
+      const int p0 = A.fam_start[f], n = A.fam_start[f + 1] - p0, kind = A.fam_kind[f];
+      // member sex when family f's CalcParentMarginal runs: last member of family f-1 (non-de-novo)
+      const int msex = dn ? 0 : (f == 0 ? sex_carry : A.sex[p0 - 1]);
+      if (kind == PM_FAM_FOUNDERS) {
+        for (int j = 0; j < n; j++) {   // CalcPostProb_SinglePerson :754-795
+          const int p = p0 + j, sx = A.sex[p];
+          const uint8_t* Rr = pl + (size_t)p * 10;
+          const double l11 = s_lk[Rr[g11]], l12 = s_lk[Rr[g12]], l22 = s_lk[Rr[g22]];
+          const double fq = freq, gq = 1 - freq;
+          double pr0 = fq * fq, pr1 = fq * gq * 2, pr2 = gq * gq;
+          if (chrom == PM_CHR_X) { if (sx == MALE) { pr0 = fq; pr1 = 0.; pr2 = 1 - fq; } else { pr0 = fq * fq; pr1 = 2 * fq * gq; pr2 = gq * gq; } }
+          if (chrom == PM_CHR_Y) { if (sx == MALE) { pr0 = fq; pr1 = 0.; pr2 = 1 - fq; } else { pr0 = pr1 = pr2 = 1.0; } }
+          if (chrom == PM_CHR_MT) { pr0 = fq; pr1 = 0; pr2 = 1 - fq; }
+          const double m11 = l11 * pr0, m12 = l12 * pr1, m22 = l22 * pr2;
+          const double sum = m11 + m12 + m22;
+          double post[3] = {0, 0, 0};
+          if (sum != 0) { post[0] = m11 / sum; post[1] = m12 / sum; post[2] = m22 / sum; }
+          const bool yf = chrom == PM_CHR_Y && sx == FEMALE;
+          if (yf) post[0] = post[1] = post[2] = 0.0;
+          const int best = d_best3(m11, m12, m22);
+          // label: own sex (non-de-novo sets member sex first); de novo leaves it stale (0)
+          const int8_t lab = yf ? PM_LBL_DOT : d_vcf_label(chrom, dn ? 0 : sx);
+          d_emit_call(out + p, post, best, lab, post[1] + post[2] * 2);
+        }
+        continue;
+      }
+      if (kind != PM_FAM_NUCLEAR) continue;   // extended pedigrees: k_posterior_ext
+      // CalcParentMarginal(_denovo) at freq
+      ItemCtx I;
+      I.a1 = a1; I.a2 = a2; I.g11 = g11; I.g12 = g12; I.g22 = g22; I.denovo = dn; I.sex = msex; I.chrom = chrom;
+      double cond[9], pp[9], pg[9];
+      hoist_nuc(A, I, pl, s_lk, s_M, p0, n, cond);
+      int pmode;
+      if (dn) pmode = A.n_fam_gt1 ? PR_AUTO : PR_DN_SINGLE;
+      else if (!A.n_fam_gt1 && !is_mono) pmode = PR_TRIO;
+      else pmode = chrom == PM_CHR_X ? PR_X : chrom == PM_CHR_Y ? PR_Y : chrom == PM_CHR_MT ? PR_MT : PR_AUTO;
+      d_parent_prior(pmode, freq, pp);
+      {
+        const uint8_t* F = pl + (size_t)p0 * 10;
+        const uint8_t* Mo = F + 10;
+        double F11 = s_lk[F[g11]], F12 = s_lk[F[g12]], F22 = s_lk[F[g22]];
+        double M11 = s_lk[Mo[g11]], M12 = s_lk[Mo[g12]], M22 = s_lk[Mo[g22]];
+        if (!dn) {
+          if (chrom == PM_CHR_X) F12 = 0.0;
+          if (chrom == PM_CHR_Y) { M11 = M12 = M22 = 1.0; F12 = 0.0; }
+          if (chrom == PM_CHR_MT) F12 = M12 = 0.0;
+        }
+        const double lF[3] = {F11, F12, F22}, lM[3] = {M11, M12, M22};
+        for (int x = 0; x < 3; x++) for (int y = 0; y < 3; y++) pg[3 * x + y] = lF[x] * lM[y];
+      }
+      double m[9];
+      for (int k = 0; k < 9; k++) m[k] = cond[k] * pp[k];
+      for (int j = 0; j < n; j++) {
+        const int p = p0 + j;
+        const int sx = A.sex[p];
+        if (j < 2) {
+          double q11, q12, q22;
+          if (j == 0) { q11 = m[0] + m[1] + m[2]; q12 = m[3] + m[4] + m[5]; q22 = m[6] + m[7] + m[8]; }
+          else { q11 = m[0] + m[3] + m[6]; q12 = m[1] + m[4] + m[7]; q22 = m[2] + m[5] + m[8]; }
+          const double sum = q11 + q12 + q22;
+          double post[3] = {0, 0, 0};
+          if (sum != 0) { post[0] = q11 / sum; post[1] = q12 / sum; post[2] = q22 / sum; }
+          const int best = d_best3(q11, q12, q22);
+          const int8_t lab = dn ? (int8_t)PM_LBL_ALLELES : ((chrom == PM_CHR_Y && sx == FEMALE) ? (int8_t)PM_LBL_DOT : d_vcf_label(chrom, sx));
+          d_emit_call(out + p, post, best, lab, post[1] + post[2] * 2);
+        } else if (!dn) {   // KidJointGenoLikelihood :798-835
+          double J[9][3];
+          for (int k = 0; k < 9; k++) {
+            d_kid_geno(chrom, pl, s_lk, p0, n, A.sex, g11, g12, g22, j, k, J[k]);
+            const double w = pg[k] * pp[k];
+            J[k][0] *= w; J[k][1] *= w; J[k][2] *= w;
+          }
+          double g[3];
+          for (int t = 0; t < 3; t++) g[t] = J[0][t] + J[1][t] + J[2][t] + J[3][t] + J[4][t] + J[5][t] + J[6][t] + J[7][t] + J[8][t];
+          const double sum = g[0] + g[1] + g[2];
+          double post[3] = {0, 0, 0};
+          if (sum != 0.0) { post[0] = g[0] / sum; post[1] = g[1] / sum; post[2] = g[2] / sum; }
+          const int best = d_best3(post[0], post[1], post[2]);
+          const int8_t lab = (chrom == PM_CHR_Y && sx == FEMALE) ? (int8_t)PM_LBL_DOT : d_vcf_label(chrom, sx);
+          d_emit_call(out + p, post, best, lab, post[1] + post[2] * 2);
+        } else {   // KidJointGenoLikelihood_denovo :838-868
+          double gsum[10];
+          for (int t = 0; t < 10; t++) gsum[t] = 0.0;
+          for (int k = 0; k < 9; k++) {
+            double Jk[10];
+            for (int t = 0; t < 10; t++) Jk[t] = 1.0;
+            for (int i = 2; i < n; i++) {
+              const uint8_t* K = pl + (size_t)(p0 + i) * 10;
+              if (i != j) {
+                double D11 = 0.0, D12 = 0.0, D22 = 0.0;
+                for (int gg = 0; gg < 10; gg++) {
+                  const double pv = s_lk[K[gg]];
+                  D11 += s_M[g11 * 10 + gg] * pv; D12 += s_M[g12 * 10 + gg] * pv; D22 += s_M[g22 * 10 + gg] * pv;
+                }
+                const double l = d_one_kid_dn(k, D11, D12, D22);
+                for (int t = 0; t < 10; t++) Jk[t] *= l;
+              } else {   // GetJointGenoLk_denovo :1480-1551
+                for (int t = 0; t < 10; t++) {
+                  double mm;
+                  switch (k) {
+                    case 0: mm = s_M[g11 * 10 + t]; break;
+                    case 1: case 3: mm = 0.5 * s_M[g11 * 10 + t] + 0.5 * s_M[g12 * 10 + t]; break;
+                    case 2: case 6: mm = s_M[g12 * 10 + t]; break;
+                    case 4: mm = 0.25 * s_M[g11 * 10 + t] + 0.5 * s_M[g12 * 10 + t] + 0.25 * s_M[g22 * 10 + t]; break;
+                    case 5: case 7: mm = 0.5 * s_M[g12 * 10 + t] + 0.5 * s_M[g22 * 10 + t]; break;
+                    default: mm = s_M[g22 * 10 + t]; break;
+                  }
+                  Jk[t] *= mm * s_lk[K[t]];
+                }
+              }
+            }
+            const double w = pg[k] * pp[k];
+            for (int t = 0; t < 10; t++) gsum[t] += Jk[t] * w;
+          }
+          double sum = 0.0;
+          for (int t = 0; t < 10; t++) sum += gsum[t];
+          double post[10];
+          for (int t = 0; t < 10; t++) post[t] = (sum == 0.0) ? 0.0 : gsum[t] / sum;
+          int best = 0; double mx = 0.0;
+          for (int t = 0; t < 10; t++) if (mx < post[t]) { mx = post[t]; best = t; }
+          d_emit_call(out + p, post, best, PM_LBL_GENO10, 0.0);
+        }
+      }
+    }
+    // CalculateAB (:1006-1039), autosomes only, exact serial sums staged through LDS
+    if (!dn && chrom == PM_CHR_AUTO) {
+      const double fr = R->af;
+      const double p11 = fr * fr, p12 = 2 * fr * (1 - fr), p22 = (1 - fr) * (1 - fr);
+      double Asum = 0.0, Bsum = 0.0;
+      for (int base = 0; base < np; base += 256) {
+        const int p = base + threadIdx.x;
+        double ta = 0.0, tb = 0.0;
+        bool use = false;
+        if (p < np) {
+          const int depth = (int)(dm[p] & 0xFFFFFF);
+          const uint8_t* Rr = pl + (size_t)p * 10;
+          const double l11 = s_lk[Rr[g11]], l12 = s_lk[Rr[g12]], l22 = s_lk[Rr[g22]];
+          const int k11 = Rr[g11], k12 = Rr[g12], k22 = Rr[g22];
+          const double PHet = (p12 * l12) / (p11 * l11 + p12 * l12 + p22 * l22);
+          if (PHet > 1e-05 && depth > 0) {
+            int scale = k22 + k11 - 2 * k12 + 6 * depth;
+            const int minimum = abs(k22 - k11);
+            if (scale < 4) scale = 4;
+            if (scale < minimum) scale = minimum;
+            const int nRef = (int)(0.5 * depth * (1 + (k22 - k11) / (scale + 1e-30)));
+            ta = PHet * nRef; tb = PHet * depth; use = true;
+          }
+        }
+        s_ab[0][threadIdx.x] = use ? ta : 0.0;
+        s_ab[1][threadIdx.x] = use ? tb : -1.0;   // -1 marks "no contribution"
+        __syncthreads();
+        if (threadIdx.x == 0) {
+          const int cnt = min(256, np - base);
+          for (int i = 0; i < cnt; i++) if (s_ab[1][i] >= 0.0) { Asum += s_ab[0][i]; Bsum += s_ab[1][i]; }
+        }
+        __syncthreads();
+      }
+      if (threadIdx.x == 0) A.res[site].ab = (0.05 + Asum) / (0.1 + Bsum);
+    }
+  }
+}
+
+__global__ void k_rows(DevArgs A) {
+  // emitted sites -> rows, in site order (single block scan; batches are <= a few million sites)
+  __shared__ int s_base;
+  if (threadIdx.x == 0) s_base = 0;
+  __syncthreads();
+  for (int base = 0; base < A.n; base += blockDim.x) {
+    const int site = base + threadIdx.x;
+    const int e = (site < A.n && A.res[site].emit) ? 1 : 0;
+    // wave-level exclusive scan via ballot
+    const unsigned long long bal = __ballot(e);
+    const int lane = threadIdx.x & 63;
+    const int wpre = __popcll(bal & ((1ull << lane) - 1ull));
+    __shared__ int s_w[16];
+    if (lane == 0) s_w[threadIdx.x >> 6] = __popcll(bal);
+    __syncthreads();
+    int off = s_base;
+    for (int w = 0; w < (int)(threadIdx.x >> 6); w++) off += s_w[w];
+    if (e) { const int row = off + wpre; A.res[site].call_row = row; A.row_site[row] = site; }
+    __syncthreads();
+    if (threadIdx.x == 0) { int t = 0; for (int w = 0; w < (int)(blockDim.x >> 6); w++) t += s_w[w]; s_base += t; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) A.counts[3] = s_base;
+}
+
+// ------------------------------------------------------------------------------------------------
+// synthetic generator: one thread per (site, family)
+__global__ void k_synth(DevArgs A, int n, uint64_t seed, uint64_t off, uint8_t* pl, uint32_t* dm, uint8_t* ref) {
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long long)n * A.n_fam) return;
+  const int i = (int)(gid / A.n_fam), f = (int)(gid % A.n_fam);
+  int r; double af;
+  pm_syn_site(seed, off + (uint64_t)i, &r, &af);
+  if (f == 0) ref[i] = (uint8_t)r;
+  const int s = A.fam_start[f], cnt = A.fam_start[f + 1] - s;
+  uint8_t hap[32];
+  if (cnt > 32) return;
+  pm_syn_family(A.syn, seed, off + (uint64_t)i, r, af, cnt, A.fa_local + s, A.mo_local + s, (uint64_t)s,
+                pl + ((size_t)i * A.n_person + s) * 10, dm + (size_t)i * A.n_person + s, hap);
+}
+
+// ================================================================================================
+// host side
+struct pm_engine {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  pm_params par;
+  int n_fam = 0, n_person = 0, max_batch = 0;
+  int chrom = PM_CHR_AUTO;
+  int T = 64, S = 1;
+  int grid_brent = 1024;
+  int n_cu = 256;
+  bool carry_postprob = false;
+  std::vector<int> fam_start_h;
+  std::vector<int8_t> sex_h;
+  int single_nuclear = 0;
+  double prior = 0;
+  int n_founders = 0, male_founders = 0, female_founders = 0;
+  // device buffers
+  int *d_fam_start = nullptr, *d_fam_kind = nullptr, *d_fa = nullptr, *d_mo = nullptr;
+  int8_t* d_sex = nullptr;
+  int4* d_units = nullptr;
+  double *d_lktab = nullptr, *d_M = nullptr;
+  pm_synth_tables* d_syn = nullptr;
+  uint8_t *d_pl = nullptr, *d_ref = nullptr;
+  uint32_t* d_dm = nullptr;
+  pm_site_result* d_res = nullptr;
+  pm_geno_call* d_calls = nullptr;
+  double *d_raw = nullptr, *d_minv = nullptr, *d_mono = nullptr;
+  int* d_evals = nullptr;
+  int8_t* d_item_sex = nullptr;
+  int* d_items[N_LISTS] = {nullptr, nullptr, nullptr};
+  int* d_counts = nullptr;
+  unsigned long long* d_eval_total = nullptr;
+  int* d_row_site = nullptr;
+  unsigned long long* d_counters = nullptr;
+  double M_h[100];
+  // stats
+  pm_kernel_stats stats{};
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> brent_events;
+};
+
+static void geno_mut_matrix(double mu, double tstv, double* out) {   // src/MutationModel.cpp:15-90
+  double A[4][4];
+  for (int i = 0; i < 4; i++) for (int j = 0; j < 4; j++) A[i][j] = (i == j) ? 1 - mu : (1 - mu) / 3;
+  if (tstv != 0.0) {
+    A[0][2] = A[2][0] = A[1][3] = A[3][1] = mu / 3 * (3 - 3 / (1 + tstv));
+    A[0][1] = A[0][3] = A[1][0] = A[1][2] = A[2][1] = A[2][3] = A[3][0] = A[3][2] = mu / 3 * (0.5 / (1 + tstv) * 3);
+  }
+  double R[16][16];
+  int from = -1;
+  for (int i = 0; i < 4; i++) for (int j = 0; j < 4; j++) {
+    from++; int to = -1;
+    for (int ii = 0; ii < 4; ii++) for (int jj = 0; jj < 4; jj++) { to++; R[from][to] = A[i][ii] * A[j][jj]; }
+  }
+  static const int h1[6] = {2, 3, 4, 7, 8, 12}, h2[6] = {5, 9, 13, 10, 14, 15};
+  for (int i = 0; i < 6; i++) for (int j = 0; j < 16; j++) R[j][h1[i] - 1] += R[j][h2[i] - 1];
+  static const int un[10] = {1, 2, 3, 4, 6, 7, 8, 11, 12, 16};
+  for (int i = 0; i < 10; i++) for (int j = 0; j < 10; j++) out[i * 10 + j] = R[un[i] - 1][un[j] - 1];
+}
+
+template <typename X>
+static int dalloc(X** p, size_t count) {
+  if (count == 0) count = 1;
+  hipError_t e = hipMalloc((void**)p, count * sizeof(X));
+  if (e != hipSuccess) {
+    char b[256]; snprintf(b, sizeof(b), "hipMalloc(%zu bytes) failed: %s", count * sizeof(X), hipGetErrorString(e));
+    pm_set_last_error(b);
+    return PM_ENOMEM;
+  }
+  return PM_OK;
+}
+#define DALLOC(p, n) do { int _r = dalloc(&(p), (n)); if (_r) { pm_engine_destroy(E); return _r; } } while (0)
+
+static const struct { int T, S; } kVariants[] = {{64, 1}, {64, 2}, {64, 4}, {128, 4}, {256, 4}, {512, 4}, {1024, 4}, {1024, 8}};
+
+// Deal families to lanes: family-major round robin; founders-only families are split into <=3-person chunks
+// kept on one lane.  Returns false if the plan does not fit T x S.
+static bool plan_units(const pm_pedigree* ped, int T, int S, std::vector<int4>& units) {
+  units.assign((size_t)T * S, make_int4(U_NONE, -1, 0, 0));
+  std::vector<int> used(T, 0);
+  int lane = 0;
+  for (int f = 0; f < ped->n_fam; f++) {
+    const int p0 = ped->fam_start[f], n = ped->fam_start[f + 1] - p0, kind = ped->fam_kind[f];
+    std::vector<int4> us;
+    if (kind == PM_FAM_NUCLEAR) us.push_back(make_int4(U_NUC, f, p0, n));
+    else if (kind == PM_FAM_FOUNDERS) {
+      for (int j = 0; j < n; j += 3) {
+        int c = std::min(3, n - j), fl = c;
+        if (j == 0) fl |= UF_FIRST;
+        if (j + 3 >= n) fl |= UF_LAST;
+        us.push_back(make_int4(U_FP, f, p0 + j, fl));
+      }
+    } else return false;   // extended pedigrees are not planned here
+    // choose the lane: next in round-robin order with enough room
+    int tries = 0;
+    while (used[lane] + (int)us.size() > S && tries < T) { lane = (lane + 1) % T; tries++; }
+    if (tries >= T) return false;
+    for (auto& u : us) units[(size_t)used[lane]++ * T + lane] = u;
+    lane = (lane + 1) % T;
+  }
+  return true;
+}
+
+extern "C" {
+
+void pm_engine_destroy(pm_engine* E) {
+  if (!E) return;
+  hipSetDevice(E->device);
+  void* bufs[] = {E->d_fam_start, E->d_fam_kind, E->d_fa, E->d_mo, E->d_sex, E->d_units, E->d_lktab, E->d_M, E->d_syn,
+                  E->d_pl, E->d_ref, E->d_dm, E->d_res, E->d_calls, E->d_raw, E->d_minv, E->d_mono, E->d_evals,
+                  E->d_item_sex, E->d_items[0], E->d_items[1], E->d_items[2], E->d_counts, E->d_eval_total, E->d_row_site,
+                  E->d_counters};
+  for (void* b : bufs) if (b) hipFree(b);
+  for (auto& pr : E->brent_events) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
+  if (E->ev0) hipEventDestroy(E->ev0);
+  if (E->ev1) hipEventDestroy(E->ev1);
+  if (E->stream) hipStreamDestroy(E->stream);
+  delete E;
+}
+
+int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, int max_batch, pm_engine** out) {
+  if (!ped || !par || !out || ped->n_fam <= 0 || ped->n_person <= 0 || max_batch <= 0) {
+    pm_set_last_error("pm_engine_create: invalid arguments");
+    return PM_EINVAL;
+  }
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    pm_set_last_error("pm_engine_create: no HIP device available (the engine has no CPU fallback)");
+    return PM_EHIP;
+  }
+  if (device < 0 || device >= ndev) { pm_set_last_error("pm_engine_create: device index out of range"); return PM_EINVAL; }
+  for (int f = 0; f < ped->n_fam; f++) {
+    if (ped->fam_kind[f] == PM_FAM_EXTENDED) {
+      pm_set_last_error("pm_engine_create: extended pedigrees (Elston-Stewart peeling) are not supported by this engine build yet");
+      return PM_EPED;
+    }
+    if (ped->fam_start[f + 1] - ped->fam_start[f] > 32 && ped->fam_kind[f] == PM_FAM_NUCLEAR) {
+      // fine: nuclear families of any size are supported
+    }
+  }
+  if (par->quick_call) { pm_set_last_error("pm_engine_create: --quick_call is not supported by this engine build yet"); return PM_EINVAL; }
+  pm_engine* E = new pm_engine;
+  E->device = device;
+  E->par = *par;
+  E->n_fam = ped->n_fam;
+  E->n_person = ped->n_person;
+  E->max_batch = max_batch;
+  E->n_founders = ped->n_founders; E->male_founders = ped->male_founders; E->female_founders = ped->female_founders;
+  E->single_nuclear = (ped->n_fam == 1 && ped->fam_kind[0] == PM_FAM_NUCLEAR) ? 1 : 0;
+  E->fam_start_h.assign(ped->fam_start, ped->fam_start + ped->n_fam + 1);
+  E->sex_h.assign(ped->sex, ped->sex + ped->n_person);
+  HIP_TRY(hipSetDevice(device));
+  HIP_TRY(hipStreamCreateWithFlags(&E->stream, hipStreamNonBlocking));
+  HIP_TRY(hipEventCreate(&E->ev0));
+  HIP_TRY(hipEventCreate(&E->ev1));
+  // plan
+  std::vector<int4> units;
+  bool planned = false;
+  for (auto v : kVariants) {
+    if (plan_units(ped, v.T, v.S, units)) { E->T = v.T; E->S = v.S; planned = true; break; }
+  }
+  if (!planned) { pm_engine_destroy(E); pm_set_last_error("pm_engine_create: pedigree too large for the lane plan"); return PM_EPED; }
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  const int blocksPerCU = std::max(1, 1024 / E->T);   // ~16 waves per CU
+  E->n_cu = prop.multiProcessorCount;
+  E->grid_brent = prop.multiProcessorCount * blocksPerCU;
+  // tables
+  double lk[256];
+  for (int i = 0; i <= 255; i++) lk[i] = pow(0.1, i * 0.1);   // core/BaseQualityHelper.cpp:13 (host glibc)
+  geno_mut_matrix(par->denovo_mut_rate, par->denovo_tstv, E->M_h);
+  static pm_synth_tables syn;
+  pm_synth_build_tables(&syn);
+  std::vector<int32_t> fa(ped->n_person, -1), mo(ped->n_person, -1);
+  if (ped->father && ped->mother)
+    for (int f = 0; f < ped->n_fam; f++)
+      for (int j = ped->fam_start[f]; j < ped->fam_start[f + 1]; j++) {
+        fa[j] = ped->father[j] < 0 ? -1 : ped->father[j] - ped->fam_start[f];
+        mo[j] = ped->mother[j] < 0 ? -1 : ped->mother[j] - ped->fam_start[f];
+      }
+  DALLOC(E->d_fam_start, ped->n_fam + 1);
+  DALLOC(E->d_fam_kind, ped->n_fam);
+  DALLOC(E->d_fa, ped->n_person);
+  DALLOC(E->d_mo, ped->n_person);
+  DALLOC(E->d_sex, ped->n_person);
+  DALLOC(E->d_units, units.size());
+  DALLOC(E->d_lktab, 256);
+  DALLOC(E->d_M, 100);
+  DALLOC(E->d_syn, 1);
+  HIP_TRY(hipMemcpy(E->d_fam_start, ped->fam_start, sizeof(int) * (ped->n_fam + 1), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(E->d_fam_kind, ped->fam_kind, sizeof(int) * ped->n_fam, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(E->d_fa, fa.data(), sizeof(int) * ped->n_person, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(E->d_mo, mo.data(), sizeof(int) * ped->n_person, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(E->d_sex, ped->sex, ped->n_person, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(E->d_units, units.data(), sizeof(int4) * units.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(E->d_lktab, lk, sizeof(lk), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(E->d_M, E->M_h, sizeof(E->M_h), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(E->d_syn, &syn, sizeof(syn), hipMemcpyHostToDevice));
+  // batch buffers
+  const size_t nb = (size_t)max_batch, np = (size_t)ped->n_person;
+  DALLOC(E->d_pl, nb * np * 10);
+  DALLOC(E->d_dm, nb * np);
+  DALLOC(E->d_ref, nb);
+  DALLOC(E->d_res, nb);
+  DALLOC(E->d_calls, nb * np);
+  DALLOC(E->d_raw, nb * 8);
+  DALLOC(E->d_minv, nb * 8);
+  DALLOC(E->d_evals, nb * 8);
+  DALLOC(E->d_mono, nb);
+  DALLOC(E->d_item_sex, nb);
+  for (int l = 0; l < N_LISTS; l++) DALLOC(E->d_items[l], nb * 4);
+  DALLOC(E->d_counts, 16);
+  DALLOC(E->d_eval_total, 1);
+  DALLOC(E->d_row_site, nb);
+  DALLOC(E->d_counters, 16);
+  HIP_TRY(hipMemset(E->d_counters, 0, 16 * sizeof(unsigned long long)));
+  HIP_TRY(hipMemset(E->d_eval_total, 0, sizeof(unsigned long long)));
+  int rc = pm_engine_begin_section(E, PM_CHR_AUTO);
+  if (rc) { pm_engine_destroy(E); return rc; }
+  *out = E;
+  return PM_OK;
+}
+
+int pm_engine_begin_section(pm_engine* E, int32_t chrom) {
+  if (!E || chrom < 0 || chrom > 3) { pm_set_last_error("pm_engine_begin_section: invalid arguments"); return PM_EINVAL; }
+  E->chrom = chrom;
+  // GetPolyPrior (NucFamGenotypeLikelihood.cpp:231-304)
+  int n;
+  if (chrom == PM_CHR_X) n = E->female_founders * 2 + E->male_founders;
+  else if (chrom == PM_CHR_Y) n = E->male_founders;
+  else if (chrom == PM_CHR_MT) n = E->n_founders;
+  else n = 2 * E->n_founders;
+  double p = 0;
+  for (int i = 1; i <= n; i++) p += 1.0 / i;
+  E->prior = p * E->par.theta;
+  HIP_TRY(hipSetDevice(E->device));
+  HIP_TRY(hipMemsetAsync(E->d_counters, 0, 16 * sizeof(unsigned long long), E->stream));
+  HIP_TRY(hipStreamSynchronize(E->stream));
+  return PM_OK;
+}
+
+static DevArgs make_args(pm_engine* E, int n, const uint8_t* pl, const uint32_t* dm, const uint8_t* ref, pm_site_result* res,
+                         pm_geno_call* calls) {
+  DevArgs A;
+  memset(&A, 0, sizeof(A));
+  A.n_fam = E->n_fam; A.n_person = E->n_person; A.n_fam_gt1 = E->n_fam > 1; A.single_nuclear = E->single_nuclear;
+  A.chrom = E->chrom; A.denovo = E->par.denovo;
+  A.fam_start = E->d_fam_start; A.fam_kind = E->d_fam_kind; A.sex = E->d_sex; A.fa_local = E->d_fa; A.mo_local = E->d_mo;
+  A.units = E->d_units; A.T = E->T; A.S = E->S;
+  A.lktab = E->d_lktab; A.M = E->d_M; A.syn = E->d_syn;
+  A.precision = E->par.precision; A.posterior = E->par.posterior; A.theta = E->par.theta;
+  A.min_total_depth = E->par.min_total_depth; A.max_total_depth = E->par.max_total_depth; A.min_map_quality = E->par.min_map_quality;
+  A.min_ps = E->par.min_ps; A.denovo_min_llr = E->par.denovo_min_llr; A.log10_denovo_min_llr = log10(E->par.denovo_min_llr);
+  A.force_call = E->par.force_call; A.all_sites = E->par.all_sites;
+  const double pts = E->par.poly_tstv / (E->par.poly_tstv + 1), ptv = (1 - pts) / 2, prior = E->prior;
+  A.lp_mono = log10(1 - prior);                  // main.cpp:450
+  A.lp_ts = log10(prior * pts);                  // :469
+  A.lp_tv = log10(prior * ptv);                  // :479, :489
+  A.lp_other = log10(prior * 0.001);             // :509-529
+  A.np_ts = log10(prior * 2. / 3.);              // :472
+  A.np_tv = log10(prior * 1. / 6.);              // :482, :492
+  A.n = n; A.pl = pl; A.dm = dm; A.ref = ref; A.res = res; A.calls = calls;
+  A.raw = E->d_raw; A.minv = E->d_minv; A.evals = E->d_evals; A.mono_plain = E->d_mono; A.item_sex = E->d_item_sex;
+  for (int l = 0; l < N_LISTS; l++) A.items[l] = E->d_items[l];
+  A.counts = E->d_counts; A.eval_total = E->d_eval_total; A.row_site = E->d_row_site; A.counters = E->d_counters;
+  A.carry_postprob = E->carry_postprob ? 1 : 0;
+  return A;
+}
+
+typedef void (*BrentFn)(DevArgs, int);
+static BrentFn brent_kernel(int T, int S) {
+#define PMK(t, s) if (T == t && S == s) return k_brent<t, s>;
+  PMK(64, 1) PMK(64, 2) PMK(64, 4) PMK(128, 4) PMK(256, 4) PMK(512, 4) PMK(1024, 4) PMK(1024, 8)
+#undef PMK
+  return nullptr;
+}
+
+static int launch_brent(pm_engine* E, const DevArgs& A, int list) {
+  BrentFn fn = brent_kernel(E->T, E->S);
+  hipEvent_t a, b;
+  HIP_TRY(hipEventCreate(&a));
+  HIP_TRY(hipEventCreate(&b));
+  HIP_TRY(hipEventRecord(a, E->stream));
+  hipLaunchKernelGGL(fn, dim3(E->grid_brent), dim3(E->T), 0, E->stream, A, list);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(b, E->stream));
+  E->brent_events.push_back({a, b});
+  return PM_OK;
+}
+
+static int run_pipeline(pm_engine* E, int n, const uint8_t* pl, const uint32_t* dm, const uint8_t* ref, pm_site_result* res,
+                        pm_geno_call* calls) {
+  DevArgs A = make_args(E, n, pl, dm, ref, res, calls);
+  HIP_TRY(hipMemsetAsync(E->d_counts, 0, 16 * sizeof(int), E->stream));
+  {
+    const int big = 0x7fffffff;   // counts[4] = first emitted site (atomicMin)
+    HIP_TRY(hipMemcpyAsync(E->d_counts + 4, &big, sizeof(int), hipMemcpyHostToDevice, E->stream));
+  }
+  hipLaunchKernelGGL(k_prep, dim3(n), dim3(256), 0, E->stream, A);
+  HIP_TRY(hipGetLastError());
+  int rc;
+  if ((rc = launch_brent(E, A, 0))) return rc;
+  const int tb = 256, gb = (n + tb - 1) / tb;
+  hipLaunchKernelGGL(k_select, dim3(gb), dim3(tb), 0, E->stream, A);
+  HIP_TRY(hipGetLastError());
+  if ((rc = launch_brent(E, A, 1))) return rc;
+  hipLaunchKernelGGL(k_finalize, dim3(gb), dim3(tb), 0, E->stream, A);
+  HIP_TRY(hipGetLastError());
+  if (E->par.denovo) {
+    hipLaunchKernelGGL(k_prepare_items7, dim3(gb), dim3(tb), 0, E->stream, A);
+    if ((rc = launch_brent(E, A, 2))) return rc;
+    hipLaunchKernelGGL(k_final_dn, dim3(gb), dim3(tb), 0, E->stream, A);
+    HIP_TRY(hipGetLastError());
+  }
+  hipLaunchKernelGGL(k_rows, dim3(1), dim3(1024), 0, E->stream, A);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_posterior, dim3(E->n_cu * 4), dim3(256), 0, E->stream, A);
+  HIP_TRY(hipGetLastError());
+  return PM_OK;
+}
+
+static int collect_stats(pm_engine* E) {
+  for (auto& pr : E->brent_events) {
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, pr.first, pr.second));
+    E->stats.kernel_ms += ms;
+    E->stats.launches++;
+    hipEventDestroy(pr.first); hipEventDestroy(pr.second);
+  }
+  E->brent_events.clear();
+  return PM_OK;
+}
+
+int pm_engine_run_device(pm_engine* E, int32_t n, const uint8_t* d_pl, const uint32_t* d_dm, const uint8_t* d_ref, pm_site_result* d_res,
+                         pm_geno_call* d_calls) {
+  if (!E || n < 0 || n > E->max_batch) { pm_set_last_error("pm_engine_run_device: invalid arguments (n > max_batch?)"); return PM_EINVAL; }
+  if (n == 0) return PM_OK;
+  HIP_TRY(hipSetDevice(E->device));
+  return run_pipeline(E, n, d_pl, d_dm, d_ref, d_res ? d_res : E->d_res, d_calls ? d_calls : E->d_calls);
+}
+
+int pm_engine_sync(pm_engine* E) {
+  if (!E) return PM_EINVAL;
+  HIP_TRY(hipSetDevice(E->device));
+  HIP_TRY(hipStreamSynchronize(E->stream));
+  int counts[16];
+  HIP_TRY(hipMemcpy(counts, E->d_counts, sizeof(counts), hipMemcpyDeviceToHost));
+  if (counts[4] != 0x7fffffff) E->carry_postprob = true;
+  int rc = collect_stats(E);
+  if (rc) return rc;
+  if (counts[5]) { pm_set_last_error("ScalarMinimizer::Brent got stuck"); return PM_EBRENT; }
+  return PM_OK;
+}
+
+int pm_engine_run(pm_engine* E, int32_t n, const uint8_t* pl, const uint32_t* dm, const uint8_t* ref, int32_t on_device,
+                  pm_site_result* res, pm_geno_call* calls, int32_t* n_rows) {
+  if (!E || n < 0 || n > E->max_batch || !res || !n_rows) { pm_set_last_error("pm_engine_run: invalid arguments"); return PM_EINVAL; }
+  *n_rows = 0;
+  if (n == 0) return PM_OK;
+  HIP_TRY(hipSetDevice(E->device));
+  const size_t np = E->n_person;
+  const uint8_t* dpl = pl;
+  const uint32_t* ddm = dm;
+  const uint8_t* dref = ref;
+  if (!on_device) {
+    HIP_TRY(hipMemcpyAsync(E->d_pl, pl, (size_t)n * np * 10, hipMemcpyHostToDevice, E->stream));
+    HIP_TRY(hipMemcpyAsync(E->d_dm, dm, (size_t)n * np * 4, hipMemcpyHostToDevice, E->stream));
+    HIP_TRY(hipMemcpyAsync(E->d_ref, ref, (size_t)n, hipMemcpyHostToDevice, E->stream));
+    dpl = E->d_pl; ddm = E->d_dm; dref = E->d_ref;
+  }
+  int rc = run_pipeline(E, n, dpl, ddm, dref, E->d_res, E->d_calls);
+  if (rc) return rc;
+  rc = pm_engine_sync(E);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpy(res, E->d_res, sizeof(pm_site_result) * n, hipMemcpyDeviceToHost));
+  int counts[16];
+  HIP_TRY(hipMemcpy(counts, E->d_counts, sizeof(counts), hipMemcpyDeviceToHost));
+  *n_rows = counts[3];
+  if (calls && counts[3] > 0)
+    HIP_TRY(hipMemcpy(calls, E->d_calls, sizeof(pm_geno_call) * np * counts[3], hipMemcpyDeviceToHost));
+  return PM_OK;
+}
+
+int pm_engine_counters(pm_engine* E, pm_counters* out) {
+  if (!E || !out) return PM_EINVAL;
+  HIP_TRY(hipSetDevice(E->device));
+  unsigned long long c[16];
+  HIP_TRY(hipStreamSynchronize(E->stream));
+  HIP_TRY(hipMemcpy(c, E->d_counters, sizeof(c), hipMemcpyDeviceToHost));
+  memset(out, 0, sizeof(*out));
+  for (int k = 0; k < 5; k++) out->ref_base_counts[k] = (int64_t)c[k];
+  out->min_total_depth_filter = (int64_t)c[5];
+  out->max_total_depth_filter = (int64_t)c[6];
+  out->min_ps_filter = (int64_t)c[7];
+  out->min_map_qual_filter = (int64_t)c[8];
+  out->homo_ref = (int64_t)c[9];
+  out->transitions = (int64_t)c[10];
+  out->transversions = (int64_t)c[11];
+  out->tstvs1 = (int64_t)c[12];
+  out->tstvs2 = (int64_t)c[13];
+  out->tvs1tvs2 = (int64_t)c[14];
+  out->nocall = (int64_t)c[15];
+  return PM_OK;
+}
+
+int pm_engine_synth(pm_engine* E, int32_t n, uint64_t seed, uint64_t off, uint8_t* d_pl, uint32_t* d_dm, uint8_t* d_ref) {
+  if (!E || n <= 0) return PM_EINVAL;
+  HIP_TRY(hipSetDevice(E->device));
+  DevArgs A = make_args(E, 0, nullptr, nullptr, nullptr, nullptr, nullptr);
+  const long long total = (long long)n * E->n_fam;
+  const int tb = 256;
+  hipLaunchKernelGGL(k_synth, dim3((unsigned)((total + tb - 1) / tb)), dim3(tb), 0, E->stream, A, n, seed, off, d_pl, d_dm, d_ref);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(E->stream));
+  return PM_OK;
+}
+
+int pm_device_alloc(pm_engine* E, uint64_t bytes, void** p) {
+  if (!E || !p) return PM_EINVAL;
+  HIP_TRY(hipSetDevice(E->device));
+  HIP_TRY(hipMalloc(p, bytes ? bytes : 1));
+  return PM_OK;
+}
+int pm_device_free(pm_engine* E, void* p) {
+  if (!E) return PM_EINVAL;
+  HIP_TRY(hipSetDevice(E->device));
+  HIP_TRY(hipFree(p));
+  return PM_OK;
+}
+int pm_copy_to_host(pm_engine* E, void* dst, const void* src, uint64_t bytes) {
+  if (!E) return PM_EINVAL;
+  HIP_TRY(hipSetDevice(E->device));
+  HIP_TRY(hipStreamSynchronize(E->stream));
+  HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  return PM_OK;
+}
+
+int pm_engine_kernel_stats(pm_engine* E, pm_kernel_stats* out, int32_t reset) {
+  if (!E || !out) return PM_EINVAL;
+  HIP_TRY(hipSetDevice(E->device));
+  unsigned long long ev = 0;
+  HIP_TRY(hipStreamSynchronize(E->stream));
+  int rc = collect_stats(E);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpy(&ev, E->d_eval_total, sizeof(ev), hipMemcpyDeviceToHost));
+  *out = E->stats;
+  out->evals = (int64_t)ev;
+  out->fam_evals = (int64_t)ev * E->n_fam;
+  if (reset) {
+    E->stats = pm_kernel_stats{};
+    HIP_TRY(hipMemset(E->d_eval_total, 0, sizeof(ev)));
+  }
+  return PM_OK;
+}
+
+}  // extern "C"

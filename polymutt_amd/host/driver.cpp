@@ -74,6 +74,8 @@ Options parse_command_line(int argc, char** argv) {
       throw FatalError(std::string("Unrecognized argument ") + s + "\n");
     }
   }
+  if (!o.positionFile.empty()) { o.force_call = true; o.quick_call = false; o.all_sites = false; }   // main.cpp:151
+  if (o.all_sites) o.quick_call = false;                                                            // main.cpp:153
   return o;
 }
 

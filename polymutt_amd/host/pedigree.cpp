@@ -248,7 +248,7 @@ void Pedigree::buildFamilies() {
 
 void Pedigree::flatten() {
   fam_start.clear(); fam_founders.clear(); fam_kind.clear(); peel_start.clear();
-  sex.clear(); is_founder.clear(); steps.clear(); column_pid.clear(); column_glf.clear();
+  sex.clear(); is_founder.clear(); father.clear(); mother.clear(); steps.clear(); column_pid.clear(); column_glf.clear();
   n_founders = male_founders = female_founders = 0;
   for (auto& F : families) {
     fam_start.push_back((int32_t)sex.size());
@@ -271,6 +271,8 @@ void Pedigree::flatten() {
       lsex.push_back(p.sex);
       lpid.push_back(p.pid);
       lpar.emplace_back(p.founder() ? -1 : persons[p.father].traverse, p.founder() ? -1 : persons[p.mother].traverse);
+      father.push_back(p.founder() ? -1 : fam_start.back() + persons[p.father].traverse);
+      mother.push_back(p.founder() ? -1 : fam_start.back() + persons[p.mother].traverse);
     }
     if (kind == PM_FAM_EXTENDED) {
       F.peel = build_peeling_order(F.count, lsex, lpar, F.famid, lpid);
@@ -290,6 +292,8 @@ pm_pedigree Pedigree::view() const {
   v.fam_kind = fam_kind.data();
   v.sex = sex.data();
   v.is_founder = is_founder.data();
+  v.father = father.data();
+  v.mother = mother.data();
   v.peel_start = peel_start.data();
   v.steps = steps.empty() ? nullptr : steps.data();
   v.n_founders = n_founders;

@@ -44,6 +44,7 @@ class Pedigree {
   // Flattened arrays (VCF column order = families in order, members in path order).
   std::vector<int32_t> fam_start, fam_founders, fam_kind, peel_start;
   std::vector<int8_t> sex, is_founder;
+  std::vector<int32_t> father, mother;   // flattened person index of each parent, -1 for founders
   std::vector<pm_peel_step> steps;
   std::vector<std::string> column_pid;   // pid per flattened person
   std::vector<int> column_glf;           // (int) GLF_Index per flattened person

@@ -1,0 +1,42 @@
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+EXAMPLE = os.path.join(ROOT, "tests", "golden", "example")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
+    config.addinivalue_line("markers", "slow: longer CPU test")
+
+
+def _gpu_available():
+    try:
+        import torch  # noqa: F401
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+def pytest_collection_modifyitems(config, items):
+    if _gpu_available():
+        return
+    skip = pytest.mark.skip(reason="no HIP device in this container")
+    for it in items:
+        if "gpu" in it.keywords:
+            it.add_marker(skip)
+
+
+@pytest.fixture(scope="session")
+def built():
+    """Build native artefacts once per session (no-op when up to date)."""
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "build/libpm_oracle.so"], check=True)
+    lib = os.path.join(ROOT, "polymutt_amd", "lib", "libpolymutt.so")
+    if not os.path.exists(lib):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "polymutt_amd")], check=True)
+    return True

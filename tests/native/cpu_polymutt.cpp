@@ -35,8 +35,6 @@ class OracleEvaluator : public SiteEvaluator {
 int main(int argc, char** argv) {
   try {
     Options opt = parse_command_line(argc, argv);
-    if (!opt.positionFile.empty()) { opt.force_call = true; opt.quick_call = false; opt.all_sites = false; }
-    if (opt.all_sites) opt.quick_call = false;
     Pedigree ped;
     ped.load(opt.datFile, opt.pedFile);
     pm_pedigree v = ped.view();

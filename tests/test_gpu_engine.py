@@ -1,0 +1,111 @@
+"""GPU parity tests: the HIP engine (through the C ABI) against the CPU oracle and the reference's
+golden VCFs.  Marked gpu; run on an MI355X with `pytest -m gpu`."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import polymutt_amd as pm
+from conftest import EXAMPLE, ROOT
+from oracle_binding import Oracle
+from parity import compare_results
+
+pytestmark = pytest.mark.gpu
+
+
+def _read_all(ped, gif_dir, gif="test.gif"):
+    cwd = os.getcwd()
+    os.chdir(gif_dir)
+    try:
+        rd = pm.GlfReader(ped, gif)
+    finally:
+        os.chdir(cwd)
+    out = []
+    for label, _ in rd.sections():
+        pos, ref, pl, dm = rd.read(200000)
+        out.append((label, pos, ref, pl, dm))
+    return out
+
+
+def _run_both(ped, params, sections, batch=4096, chrom_of=lambda lab: pm.PM_CHR_AUTO):
+    eng = pm.Engine(ped.view, params, max_batch=batch)
+    ora = Oracle(ped.view, params)
+    stats = []
+    for label, pos, ref, pl, dm in sections:
+        ch = chrom_of(label)
+        eng.begin_section(ch)
+        ora.begin_section(ch)
+        for s in range(0, len(ref), batch):
+            e, ec = eng.run(pl[s:s + batch], dm[s:s + batch], ref[s:s + batch])
+            o, oc = ora.run(pl[s:s + batch], dm[s:s + batch], ref[s:s + batch])
+            stats.append(compare_results(e, o, ec, oc, label=f"[{label}:{s}] "))
+        ce, co = eng.counters().as_array(), ora.counters().as_array()
+        assert (ce == co).all(), (ce, co)
+    eng.close()
+    return stats
+
+
+@pytest.mark.parametrize("pedfile,kw", [
+    ("test.ped", dict()),
+    ("test.ped", dict(min_total_depth=150, max_total_depth=200, posterior=0.9)),
+    ("test.mix.ped", dict()),
+    ("test.ped", dict(denovo=1, denovo_mut_rate=1.5e-7)),
+    ("test.ped", dict(all_sites=1)),
+])
+def test_example_sites_match_oracle(built, pedfile, kw):
+    ped = pm.Pedigree(os.path.join(EXAMPLE, "test.dat"), os.path.join(EXAMPLE, pedfile))
+    secs = _read_all(ped, EXAMPLE)
+    stats = _run_both(ped, pm.Params.defaults(**kw), secs)
+    assert sum(s["sites"] for s in stats) == 81016
+
+
+def _golden_body(name):
+    import gzip
+    p = os.path.join(EXAMPLE, name)
+    if name.endswith(".gz"):
+        return gzip.open(p, "rt").read().splitlines()
+    return [l for l in open(p).read().splitlines() if not l.startswith("##")]
+
+
+@pytest.mark.parametrize("args,golden", [
+    (["-p", "test.ped", "-d", "test.dat", "-g", "test.gif", "-c", "0.9", "--minDepth", "150", "--maxDepth", "200",
+      "--nthreads", "4"], "test.out.vcf.body.gz"),
+    (["-p", "test.mix.ped", "-d", "test.dat", "-g", "test.gif"], "test.out.vcfa.body.gz"),
+    (["-p", "test.ped", "-d", "test.dat", "-g", "test.gif", "--nthreads", "4", "--denovo", "--rate_denovo", "1.5e-07"],
+     "test.denovo.out.vcf"),
+])
+def test_cli_reproduces_reference_goldens(built, tmp_path, args, golden):
+    out = tmp_path / "out.vcf"
+    r = subprocess.run([pm.BIN_PATH] + args + ["--out_vcf", str(out)], cwd=EXAMPLE, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    got = [l for l in out.read_text().splitlines() if not l.startswith("##")]
+    exp = _golden_body(golden)
+    assert len(got) == len(exp)
+    diff = [i for i, (a, b) in enumerate(zip(got, exp)) if a != b]
+    assert not diff, f"{len(diff)} lines differ; first:\n{got[diff[0]][:300]}\n{exp[diff[0]][:300]}"
+
+
+@pytest.mark.parametrize("shape,nfam,nsites", [("quad", 300, 600), ("trio", 200, 600), ("mixed", 101, 400),
+                                               ("single", 64, 300)])
+def test_synthetic_device_generator_and_parity(built, shape, nfam, nsites, tmp_path):
+    d = str(tmp_path / shape)
+    pm.synth_write_dataset(d, shape, nfam, nsites, 7)
+    ped = pm.Pedigree(os.path.join(d, "test.dat"), os.path.join(d, "test.ped"))
+    secs = _read_all(ped, d)
+    label, pos, ref, pl, dm = secs[0]
+    # device generator == host generator == GLF files
+    hpl, hdm, href = pm.synth_block_host(ped.view, nsites, 7)
+    assert (hpl == pl).all() and (hdm == dm).all() and (href == ref).all()
+    eng = pm.Engine(ped.view, pm.Params.defaults(), max_batch=nsites)
+    d_pl, d_dm, d_ref = eng.alloc(pl.nbytes), eng.alloc(dm.nbytes), eng.alloc(ref.nbytes)
+    eng.synth(nsites, 7, 0, d_pl, d_dm, d_ref)
+    gpl, gdm, gref = np.zeros_like(pl), np.zeros_like(dm), np.zeros_like(ref)
+    eng.to_host(gpl, d_pl, pl.nbytes); eng.to_host(gdm, d_dm, dm.nbytes); eng.to_host(gref, d_ref, ref.nbytes)
+    assert (gpl == pl).all() and (gdm == dm).all() and (gref == ref).all()
+    for p in (d_pl, d_dm, d_ref):
+        eng.free(p)
+    eng.close()
+    stats = _run_both(ped, pm.Params.defaults(), secs, batch=256)
+    assert sum(s["called"] for s in stats) > 0
