@@ -917,6 +917,7 @@ int pmo_site(pmo_ctx *c, const uint8_t *pl, const uint32_t *dm, int32_t refBase,
   }
   if (g_brent_err) return PM_EBRENT;
   R->status = PM_SITE_CALLED; R->n_cfg = ncfg; R->maxidx = maxidx; R->var_post_prob = vpp; R->poly_qual = qual;
+  R->allele1 = c->lk[0].a1; R->allele2 = c->lk[0].a2;   /* set by CalcVarPosterior for every evaluated site */
   for (int k = 0; k < 7; k++) {
     R->varllk[k] = k < ncfg ? varllk[k] : 0.0; R->varfreq[k] = k < ncfg ? varfreq[k] : 0.0;
     R->evals[k] = k < ncfg ? (int32_t)c->lk[k].evals : 0;

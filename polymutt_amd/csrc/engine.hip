@@ -590,12 +590,13 @@ __global__ void __launch_bounds__(256) k_finalize(DevArgs A) {
         // noprior[0] = varllk[0] - log10(1-prior)  (main.cpp:460), lk_mono = MonomorphismLogLikelihood
         const double dlr = (v[0] - A.lp_mono) - A.mono_plain[site];
         R->denovo_lr = dlr;
-        if (dlr <= A.log10_denovo_min_llr && !fa) emit = false;
+        if (dlr <= A.log10_denovo_min_llr && !fa) emit = false;   // main.cpp:563 compares with log10(minLLR)
       }
     }
     R->af = af;
     if (emit) {
-      R->emit = 1;
+      // OutputVCF_denovo (:1868) suppresses the record when denovoLR < minLLR (no log10 there)
+      R->emit = (A.denovo && maxidx == 0 && R->denovo_lr < A.denovo_min_llr) ? 2 : 1;
       R->is_mono = (!A.denovo && maxidx == 0) ? 1 : 0;
       R->denovo_mono = (A.denovo && maxidx == 0) ? 1 : 0;
       atomicMin(&A.counts[4], site);
@@ -640,6 +641,7 @@ __global__ void k_final_dn(DevArgs A) {
   const double noprior = R->varllk[mx] - npc;
   R->denovo_lr = noprior - raw[7];
   if (!A.single_nuclear) R->af = A.minv[site * 8 + 7];
+  R->emit = (R->denovo_lr < A.denovo_min_llr) ? 2 : 1;
 }
 
 // ------------------------------------------------------------------------------------------------
