@@ -188,7 +188,14 @@ int pm_copy_to_host(pm_engine *eng, void *h_dst, const void *d_src, uint64_t byt
 
 /* Timing of the dominant (Brent) kernel over the last run: launches, summed kernel ms (HIP events on the
  * engine stream), total objective evaluations and family-evaluations (for roofline accounting). */
-typedef struct { int64_t launches; double kernel_ms; int64_t evals; int64_t fam_evals; double total_ms; } pm_kernel_stats;
+typedef struct {
+  int64_t launches;      /* k_brent launches */
+  double  kernel_ms;     /* summed k_brent time (HIP events on the engine stream) */
+  int64_t evals;         /* objective evaluations by Brent items */
+  int64_t fam_evals;     /* evals x families */
+  int64_t items;         /* (site, configuration) work items evaluated */
+  int64_t sites;         /* sites processed */
+} pm_kernel_stats;
 int pm_engine_kernel_stats(pm_engine *eng, pm_kernel_stats *out, int32_t reset);
 
 const char *pm_last_error(void);

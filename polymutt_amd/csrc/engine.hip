@@ -446,64 +446,63 @@ __global__ void __launch_bounds__(T) k_brent(DevArgs A, int list) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_prep: one block per site
+// k_prep: one lane per site.  CalcReadStats and MonomorphismLogLikelihood walk the persons serially in
+// the reference's order, so the monomorphism log-likelihood is bit-identical (NucFamGenotypeLikelihood.cpp:502-546).
 __global__ void __launch_bounds__(256) k_prep(DevArgs A) {
-  __shared__ long long s_sum[4][4];
-  __shared__ uint8_t s_hr[4096];
-  const int site = blockIdx.x;
-  if (site >= A.n) return;
-  const int r = A.ref[site];
-  const int np = A.n_person;
-  const uint8_t* pl = A.pl + (size_t)site * np * 10;
-  const uint32_t* dm = A.dm + (size_t)site * np;
-  pm_site_result* R = A.res + site;
-  const bool okref = r >= 1 && r <= 4;
-  const int h = okref ? d_gi(r, r) : 0;
-  long long dsum = 0, mqsum = 0, nsd = 0;
-  for (int p = threadIdx.x; p < np; p += 256) {
-    const uint32_t x = dm[p];
-    const int d = (int)(x & 0xFFFFFF);
-    dsum += d; mqsum += (x >> 24); nsd += d > 0;
+  __shared__ unsigned long long s_c[9];
+  if (threadIdx.x < 9) s_c[threadIdx.x] = 0;
+  __syncthreads();
+  const int site = blockIdx.x * 256 + threadIdx.x;
+  bool valid = false;
+  if (site < A.n) {
+    const int r = A.ref[site];
+    const int np = A.n_person;
+    const uint8_t* pl = A.pl + (size_t)site * np * 10;
+    const uint32_t* dm = A.dm + (size_t)site * np;
+    pm_site_result* R = A.res + site;
+    const bool okref = r >= 1 && r <= 4;
+    const int h = okref ? d_gi(r, r) : 0;
+    int dsum = 0, nsd = 0;
+    double mq = 0.0, mono = 0.0;
+    for (int p = 0; p < np; p++) {
+      const uint32_t x = dm[p];
+      const int d = (int)(x & 0xFFFFFF);
+      dsum += d; mq += (double)(x >> 24); nsd += d > 0;
+      mono += -(double)(pl[(size_t)p * 10 + h]) / 10;
+    }
+    pm_site_result O;
+    memset(&O, 0, sizeof(O));
+    O.maxidx = -2; O.call_row = -1; O.ab = 0.5; O.denovo_lr = -1;
+    A.mono_plain[site] = mono;
+    if (!okref) O.status = PM_SITE_BAD_REF;
+    else {
+      atomicAdd(&s_c[r], 1ull);
+      double avgmq = 0., ps = 0.;
+      if (nsd > 0) { avgmq = mq / (double)nsd; ps = (double)nsd / (double)np; }
+      O.total_depth = dsum; O.num_samp_with_data = nsd; O.avg_map_qual = avgmq; O.perc_samp_with_data = ps;
+      int st = 0;   // filters, main.cpp:345-348
+      if (dsum < A.min_total_depth) st = PM_SITE_MIN_DEPTH;
+      else if (A.max_total_depth > 0 && dsum > A.max_total_depth) st = PM_SITE_MAX_DEPTH;
+      else if (ps * 100 < A.min_ps) st = PM_SITE_MIN_PS;
+      else if (avgmq < A.min_map_quality) st = PM_SITE_MIN_MAPQ;
+      if (st) { O.status = st; atomicAdd(&s_c[4 + st], 1ull); }
+      else { O.status = PM_SITE_CALLED; valid = true; }
+    }
+    *R = O;
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) { dsum += __shfl_xor(dsum, o, 64); mqsum += __shfl_xor(mqsum, o, 64); nsd += __shfl_xor(nsd, o, 64); }
-  if ((threadIdx.x & 63) == 0) { s_sum[0][threadIdx.x >> 6] = dsum; s_sum[1][threadIdx.x >> 6] = mqsum; s_sum[2][threadIdx.x >> 6] = nsd; }
-  // MonomorphismLogLikelihood (:502-517): exact serial sum over persons, staged through LDS
-  double mono = 0.0;
-  for (int base = 0; base < np; base += 4096) {
-    const int cnt = min(4096, np - base);
-    __syncthreads();
-    for (int p = threadIdx.x; p < cnt; p += 256) s_hr[p] = pl[(size_t)(base + p) * 10 + h];
-    __syncthreads();
-    if (threadIdx.x == 0)
-      for (int p = 0; p < cnt; p++) mono += -(double)(s_hr[p]) / 10;
+  // enqueue (site, configuration) Brent items, one atomic per wave
+  const int nit = A.denovo ? 4 : 3;
+  const unsigned long long bal = __ballot(valid);
+  const int lane = threadIdx.x & 63;
+  int base = 0;
+  if (lane == 0 && bal) base = atomicAdd(&A.counts[0], nit * __popcll(bal));
+  base = __shfl(base, 0, 64);
+  if (valid) {
+    const int slot = base + nit * __popcll(bal & ((1ull << lane) - 1ull));
+    for (int k = 0; k < nit; k++) A.items[0][slot + k] = (site << 3) | (A.denovo ? k : k + 1);
   }
   __syncthreads();
-  if (threadIdx.x != 0) return;
-  dsum = s_sum[0][0] + s_sum[0][1] + s_sum[0][2] + s_sum[0][3];
-  mqsum = s_sum[1][0] + s_sum[1][1] + s_sum[1][2] + s_sum[1][3];
-  nsd = s_sum[2][0] + s_sum[2][1] + s_sum[2][2] + s_sum[2][3];
-  memset(R, 0, sizeof(*R));
-  R->maxidx = -2; R->call_row = -1; R->ab = 0.5; R->denovo_lr = -1;
-  A.mono_plain[site] = mono;
-  if (!okref) { R->status = PM_SITE_BAD_REF; return; }
-  atomicAdd(&A.counters[r], 1ull);
-  // CalcReadStats :520-546
-  const int td = (int)dsum, n = (int)nsd;
-  double avgmq = 0., ps = 0.;
-  if (n > 0) { avgmq = (double)mqsum / (double)n; ps = (double)n / (double)np; }
-  R->total_depth = td; R->num_samp_with_data = n; R->avg_map_qual = avgmq; R->perc_samp_with_data = ps;
-  // filters, main.cpp:345-348
-  int st = 0;
-  if (td < A.min_total_depth) st = PM_SITE_MIN_DEPTH;
-  else if (A.max_total_depth > 0 && td > A.max_total_depth) st = PM_SITE_MAX_DEPTH;
-  else if (ps * 100 < A.min_ps) st = PM_SITE_MIN_PS;
-  else if (avgmq < A.min_map_quality) st = PM_SITE_MIN_MAPQ;
-  if (st) { R->status = st; atomicAdd(&A.counters[4 + st], 1ull); return; }
-  R->status = PM_SITE_CALLED;
-  const int nit = A.denovo ? 4 : 3;
-  const int slot = atomicAdd(&A.counts[0], nit);
-  for (int k = 0; k < nit; k++) A.items[0][slot + k] = (site << 3) | (A.denovo ? k : k + 1);
+  if (threadIdx.x < 9 && s_c[threadIdx.x]) atomicAdd(&A.counters[threadIdx.x], s_c[threadIdx.x]);
 }
 
 // CalcVarPosterior (:1693-1749); returns maxidx, sets vpp/qual/alleles
@@ -728,29 +727,31 @@ __device__ void d_kid_geno(int chrom, const uint8_t* pl, const double* lk, int p
   out[0] = G11; out[1] = G12; out[2] = G22;
 }
 
+template <bool DN>
 __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
   __shared__ double s_lk[256];
   __shared__ double s_M[100];
-  __shared__ double s_ab[2][256];
   for (int i = threadIdx.x; i < 256; i += blockDim.x) s_lk[i] = A.lktab[i];
   for (int i = threadIdx.x; i < 100; i += blockDim.x) s_M[i] = A.M[i];
   __syncthreads();
-  const int rows = A.counts[3];
-  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+  const long long work = (long long)A.counts[3] * A.n_fam;
+  for (long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x; gid < work; gid += (long long)gridDim.x * blockDim.x) {
+    const int row = (int)(gid / A.n_fam);
+    const int f = (int)(gid % A.n_fam);
     const int site = A.row_site[row];
     const pm_site_result* R = A.res + site;
     const int np = A.n_person;
     const uint8_t* pl = A.pl + (size_t)site * np * 10;
-    const uint32_t* dm = A.dm + (size_t)site * np;
     pm_geno_call* out = A.calls + (size_t)row * np;
     const int a1 = R->allele1, a2 = R->allele2;
     const int g11 = d_gi(a1, a1), g12 = d_gi(a1, a2), g22 = d_gi(a2, a2);
-    const int chrom = A.chrom, dn = A.denovo;
+    const int chrom = A.chrom;
+    constexpr int dn = DN ? 1 : 0;
     // CalcPostProb freq (main.cpp:576-587)
     const double freq = (R->maxidx == 0) ? (dn ? 1.0 : 1 - A.theta) : R->af;
     const int is_mono = (R->maxidx == 0 && !dn) ? 1 : 0;
     const int sex_carry = d_member_sex_before(A, site);
-    for (int f = threadIdx.x; f < A.n_fam; f += blockDim.x) {
+    {
       const int p0 = A.fam_start[f], n = A.fam_start[f + 1] - p0, kind = A.fam_kind[f];
       // member sex when family f's CalcParentMarginal runs: last member of family f-1 (non-de-novo)
       const int msex = dn ? 0 : (f == 0 ? sex_carry : A.sex[p0 - 1]);
@@ -875,7 +876,26 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
         }
       }
     }
-    // CalculateAB (:1006-1039), autosomes only, exact serial sums staged through LDS
+  }
+}
+
+// CalculateAB (:1006-1039) for emitted autosomal non-de-novo sites: per-person terms in parallel,
+// the two sums accumulated serially in person order (bit-identical to the reference).
+__global__ void __launch_bounds__(256) k_ab(DevArgs A) {
+  __shared__ double s_lk[256];
+  __shared__ double s_ab[2][256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) s_lk[i] = A.lktab[i];
+  __syncthreads();
+  const int rows = A.counts[3];
+  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+    const int site = A.row_site[row];
+    const pm_site_result* R = A.res + site;
+    const int np = A.n_person;
+    const uint8_t* pl = A.pl + (size_t)site * np * 10;
+    const uint32_t* dm = A.dm + (size_t)site * np;
+    const int a1 = R->allele1, a2 = R->allele2;
+    const int g11 = d_gi(a1, a1), g12 = d_gi(a1, a2), g22 = d_gi(a2, a2);
+    const int dn = A.denovo, chrom = A.chrom;
     if (!dn && chrom == PM_CHR_AUTO) {
       const double fr = R->af;
       const double p11 = fr * fr, p12 = 2 * fr * (1 - fr), p22 = (1 - fr) * (1 - fr);
@@ -965,6 +985,7 @@ struct pm_engine {
   int chrom = PM_CHR_AUTO;
   int T = 64, S = 1;
   int grid_brent = 1024;
+  int last_n = 0;
   int n_cu = 256;
   bool carry_postprob = false;
   std::vector<int> fam_start_h;
@@ -1249,12 +1270,13 @@ static int launch_brent(pm_engine* E, const DevArgs& A, int list) {
 static int run_pipeline(pm_engine* E, int n, const uint8_t* pl, const uint32_t* dm, const uint8_t* ref, pm_site_result* res,
                         pm_geno_call* calls) {
   DevArgs A = make_args(E, n, pl, dm, ref, res, calls);
+  E->last_n = n;
   HIP_TRY(hipMemsetAsync(E->d_counts, 0, 16 * sizeof(int), E->stream));
   {
     const int big = 0x7fffffff;   // counts[4] = first emitted site (atomicMin)
     HIP_TRY(hipMemcpyAsync(E->d_counts + 4, &big, sizeof(int), hipMemcpyHostToDevice, E->stream));
   }
-  hipLaunchKernelGGL(k_prep, dim3(n), dim3(256), 0, E->stream, A);
+  hipLaunchKernelGGL(k_prep, dim3((n + 255) / 256), dim3(256), 0, E->stream, A);
   HIP_TRY(hipGetLastError());
   int rc;
   if ((rc = launch_brent(E, A, 0))) return rc;
@@ -1272,8 +1294,13 @@ static int run_pipeline(pm_engine* E, int n, const uint8_t* pl, const uint32_t* 
   }
   hipLaunchKernelGGL(k_rows, dim3(1), dim3(1024), 0, E->stream, A);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_posterior, dim3(E->n_cu * 4), dim3(256), 0, E->stream, A);
+  if (E->par.denovo) hipLaunchKernelGGL(k_posterior<true>, dim3(E->n_cu * 8), dim3(256), 0, E->stream, A);
+  else hipLaunchKernelGGL(k_posterior<false>, dim3(E->n_cu * 8), dim3(256), 0, E->stream, A);
   HIP_TRY(hipGetLastError());
+  if (!E->par.denovo && E->chrom == PM_CHR_AUTO) {
+    hipLaunchKernelGGL(k_ab, dim3(E->n_cu * 8), dim3(256), 0, E->stream, A);
+    HIP_TRY(hipGetLastError());
+  }
   return PM_OK;
 }
 
@@ -1304,6 +1331,8 @@ int pm_engine_sync(pm_engine* E) {
   int counts[16];
   HIP_TRY(hipMemcpy(counts, E->d_counts, sizeof(counts), hipMemcpyDeviceToHost));
   if (counts[4] != 0x7fffffff) E->carry_postprob = true;
+  E->stats.items += (int64_t)counts[0] + counts[1] + counts[2];
+  E->stats.sites += E->last_n;
   int rc = collect_stats(E);
   if (rc) return rc;
   if (counts[5]) { pm_set_last_error("ScalarMinimizer::Brent got stuck"); return PM_EBRENT; }
