@@ -90,6 +90,8 @@ typedef struct {
   int32_t force_call;          /* set by --pos */
   int32_t all_sites;           /* --all_sites */
   int32_t quick_call;          /* --quick_call */
+  int32_t exact_log10;         /* engine numerics: 1 = one log10 per family, summed (the reference's form);
+                                  0 = normalised product of family likelihoods, one log10 per evaluation */
 } pm_params;
 
 /* Site status codes (which `continue` of main.cpp:300-594 was taken). */

@@ -211,13 +211,14 @@ struct ItemCtx {
   int chrom;
 };
 
+template <bool GEN>
 __device__ __forceinline__ void hoist_nuc(const DevArgs& A, const ItemCtx& I, const uint8_t* pl, const double* lk, const double* M,
                                           int p0, int n, double* cond) {
   const uint8_t* F = pl + (size_t)p0 * 10;
   const uint8_t* Mo = F + 10;
   double F11 = lk[F[I.g11]], F12 = lk[F[I.g12]], F22 = lk[F[I.g22]];
   double M11 = lk[Mo[I.g11]], M12 = lk[Mo[I.g12]], M22 = lk[Mo[I.g22]];
-  if (!I.denovo) {   // CalcParentMarginal :1049-1051
+  if (GEN && !I.denovo) {   // CalcParentMarginal :1049-1051
     if (I.chrom == PM_CHR_X) F12 = 0.0;
     if (I.chrom == PM_CHR_Y) { M11 = M12 = M22 = 1.0; F12 = 0.0; }
     if (I.chrom == PM_CHR_MT) F12 = M12 = 0.0;
@@ -227,10 +228,10 @@ __device__ __forceinline__ void hoist_nuc(const DevArgs& A, const ItemCtx& I, co
   for (int k = 0; k < 9; k++) kids[k] = 1.0;
   for (int j = 2; j < n; j++) {
     const uint8_t* K = pl + (size_t)(p0 + j) * 10;
-    if (!I.denovo) {
+    if (!GEN || !I.denovo) {
       const double l11 = lk[K[I.g11]], l12 = lk[K[I.g12]], l22 = lk[K[I.g22]];
 #pragma unroll
-      for (int k = 0; k < 9; k++) kids[k] *= d_one_kid(k, I.chrom, I.sex, l11, l12, l22);
+      for (int k = 0; k < 9; k++) kids[k] *= d_one_kid(k, GEN ? I.chrom : (int)PM_CHR_AUTO, I.sex, l11, l12, l22);
     } else {
       double D11 = 0.0, D12 = 0.0, D22 = 0.0;
 #pragma unroll
@@ -306,7 +307,7 @@ __device__ __forceinline__ void block_sum3(double& x, double& y, double& z, doub
 }
 
 // per-lane partial of CalcAllFamLogLikelihood(freq) over the lane's units
-template <int S>
+template <int S, bool GEN>
 __device__ __forceinline__ double lane_loglik(double f, const int4* unit, const double (*cond)[9], const int* fl, int pmode) {
   double pp[9];
   d_parent_prior(pmode, f, pp);
@@ -321,7 +322,7 @@ __device__ __forceinline__ double lane_loglik(double f, const int4* unit, const 
 #pragma unroll
       for (int k = 0; k < 9; k++) v += cond[s][k] * pp[k];
       part += log10(v);
-    } else if (ty == U_FP) {
+    } else if (GEN && ty == U_FP) {
       if (unit[s].w & UF_FIRST) prod = 1.0;
 #pragma unroll
       for (int j = 0; j < 3; j++) {
@@ -338,11 +339,91 @@ __device__ __forceinline__ double lane_loglik(double f, const int4* unit, const 
   return part;
 }
 
-template <int T, int S>
+// Product-mode objective: instead of summing log10 of every family likelihood (one log10 per family),
+// each lane multiplies its families' likelihoods into a normalised (mantissa, exponent) pair, the block
+// reduces the pairs by multiplication, and one log10 per evaluation turns the product into
+// CalcAllFamLogLikelihood.  Sum-of-logs == log-of-product exactly in real arithmetic; the floating-point
+// result is at least as accurate as the reference's serial sum (DESIGN.md "Numerics").
+#define PM_LOG10_2_HI 0x1.3441350800000p-2
+#define PM_LOG10_2_LO 0x1.f79fef311f12bp-34
+
+template <int S, bool GEN>
+__device__ __forceinline__ void lane_prod(double f, const int4* unit, const double (*cond)[9], const int* fl, int pmode, double& m,
+                                          int& e) {
+  double pp[9];
+  d_parent_prior(pmode, f, pp);
+  const double g = 1 - f;
+  const double P0 = f * f, P1 = f * g * 2, P2 = g * g;
+  // every slot's likelihood is normalised independently (no serial chain), then the mantissas
+  // (each in [0.5, 1)) are multiplied as a tree and the exponents summed.
+  double mv[S];
+  int ev[S];
+#pragma unroll
+  for (int s = 0; s < S; s++) {
+    const int ty = unit[s].x;
+    double v = 1.0;
+    if (ty == U_NUC) {
+      v = 0.0;
+#pragma unroll
+      for (int k = 0; k < 9; k++) v += cond[s][k] * pp[k];
+    } else if (GEN && ty == U_FP) {
+#pragma unroll
+      for (int j = 0; j < 3; j++) {
+        const int b = (fl[s] >> (2 * j)) & 3;
+        if (b & 2) continue;
+        double sp = 0.0;
+        if (b & 1) sp = sp + cond[s][3 * j] * f + cond[s][3 * j + 1] * 0 + cond[s][3 * j + 2] * g;
+        else sp = sp + cond[s][3 * j] * P0 + cond[s][3 * j + 1] * P1 + cond[s][3 * j + 2] * P2;
+        v *= sp;   // <= 3 persons: no underflow before normalisation
+      }
+    }
+    mv[s] = frexp(v, &ev[s]);
+  }
+#pragma unroll
+  for (int w = 1; w < S; w *= 2)
+#pragma unroll
+    for (int s = 0; s + w < S; s += 2 * w) {
+      int x;
+      mv[s] = frexp(mv[s] * mv[s + w], &x);
+      ev[s] += ev[s + w] + x;
+    }
+  m = mv[0];
+  e = ev[0];
+}
+
+template <int T>
+__device__ __forceinline__ double block_logprod(double m, int e, double* red, int* rede, int& par) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {   // commutative butterfly: identical (m, e) in every lane
+    const double mo = __shfl_xor(m, o, 64);
+    const int eo = __shfl_xor(e, o, 64);
+    int ev;
+    m = frexp(m * mo, &ev);
+    e += eo + ev;
+  }
+  if (T > 64) {
+    constexpr int W = T / 64;
+    if ((threadIdx.x & 63) == 0) { red[par * 16 + (threadIdx.x >> 6)] = m; rede[par * 16 + (threadIdx.x >> 6)] = e; }
+    __syncthreads();
+    m = red[par * 16]; e = rede[par * 16];
+#pragma unroll
+    for (int i = 1; i < W; i++) {
+      int ev;
+      m = frexp(m * red[par * 16 + i], &ev);
+      e += rede[par * 16 + i] + ev;
+    }
+    par ^= 1;
+  }
+  const double de = (double)e;
+  return log10(m) + (de * PM_LOG10_2_HI + de * PM_LOG10_2_LO);
+}
+
+template <int T, int S, bool PROD, bool GEN>
 __global__ void __launch_bounds__(T) k_brent(DevArgs A, int list) {
   __shared__ double s_lk[256];
   __shared__ double s_M[100];
   __shared__ double s_red[96];
+  __shared__ int s_rede[32];
   for (int i = threadIdx.x; i < 256; i += T) s_lk[i] = A.lktab[i];
   for (int i = threadIdx.x; i < 100; i += T) s_M[i] = A.M[i];
   __syncthreads();
@@ -360,12 +441,13 @@ __global__ void __launch_bounds__(T) k_brent(DevArgs A, int list) {
     if (cfg == 7) { I.a1 = A.res[site].allele1; I.a2 = A.res[site].allele2; }
     else cfg_alleles(cfg, r, &I.a1, &I.a2);
     I.g11 = d_gi(I.a1, I.a1); I.g12 = d_gi(I.a1, I.a2); I.g22 = d_gi(I.a2, I.a2);
-    I.denovo = A.denovo && cfg != 7;
-    I.sex = (cfg == 7) ? A.item_sex[site] : 0;
-    I.chrom = A.chrom;
+    I.denovo = GEN ? (A.denovo && cfg != 7) : 0;
+    I.sex = (GEN && cfg == 7) ? A.item_sex[site] : 0;
+    I.chrom = GEN ? A.chrom : PM_CHR_AUTO;
     int pmode;
     if (I.denovo) pmode = A.n_fam_gt1 ? PR_AUTO : PR_DN_SINGLE;
     else if (!A.n_fam_gt1) pmode = PR_TRIO;   // isMono is never set on the evaluating objects
+    else if (!GEN) pmode = PR_AUTO;
     else pmode = A.chrom == PM_CHR_X ? PR_X : A.chrom == PM_CHR_Y ? PR_Y : A.chrom == PM_CHR_MT ? PR_MT : PR_AUTO;
 
     const uint8_t* pl = A.pl + (size_t)site * A.n_person * 10;
@@ -374,8 +456,8 @@ __global__ void __launch_bounds__(T) k_brent(DevArgs A, int list) {
 #pragma unroll
     for (int s = 0; s < S; s++) {
       fl[s] = 0;
-      if (unit[s].x == U_NUC) hoist_nuc(A, I, pl, s_lk, s_M, unit[s].z, unit[s].w, cond[s]);
-      else if (unit[s].x == U_FP) fl[s] = hoist_fp(A, I, pl, s_lk, unit[s].z, unit[s].w & 0xFF, cond[s]);
+      if (unit[s].x == U_NUC) hoist_nuc<GEN>(A, I, pl, s_lk, s_M, unit[s].z, unit[s].w, cond[s]);
+      else if (GEN && unit[s].x == U_FP) fl[s] = hoist_fp(A, I, pl, s_lk, unit[s].z, unit[s].w & 0xFF, cond[s]);
     }
     double* raw = A.raw + (size_t)site * 8;
     const bool single = (cfg == 0) || A.single_nuclear;
@@ -388,7 +470,14 @@ __global__ void __launch_bounds__(T) k_brent(DevArgs A, int list) {
     int phase = 0, iter = 0, nev = 0;
     bool ok = false;
     for (;;) {
-      const double tot = block_sum<T>(lane_loglik<S>(x, unit, cond, fl, pmode), s_red, par);
+      double tot;
+      if (PROD) {
+        double m; int e;
+        lane_prod<S, GEN>(x, unit, cond, fl, pmode, m, e);
+        tot = block_logprod<T>(m, e, s_red, s_rede, par);
+      } else {
+        tot = block_sum<T>(lane_loglik<S, GEN>(x, unit, cond, fl, pmode), s_red, par);
+      }
       nev++;
       if (single) { mn = 0.0; fmin = -tot; ok = true; break; }
       const double fx = -tot;
@@ -446,60 +535,77 @@ __global__ void __launch_bounds__(T) k_brent(DevArgs A, int list) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_prep: one lane per site.  CalcReadStats and MonomorphismLogLikelihood walk the persons serially in
-// the reference's order, so the monomorphism log-likelihood is bit-identical (NucFamGenotypeLikelihood.cpp:502-546).
+// In-order accumulation of one wave's 64 per-lane terms into a running sum held by every lane:
+// s = (((s + t_0) + t_1) + ... + t_63), lanes in ascending order -- the reference's serial loop order.
+// Lanes whose term is an exact zero are skipped: adding +-0.0 never changes a running sum that is not
+// -0.0 (the sums here start at +0.0), so the result is bit-identical to the full serial loop.
+__device__ __forceinline__ double wave_serial_add(double s, double t, bool nz) {
+  unsigned long long m = __ballot(nz);
+  while (m) {
+    const int l = __ffsll((long long)m) - 1;
+    m &= m - 1;
+    s += __shfl(t, l, 64);
+  }
+  return s;
+}
+
+// k_prep: one wave per site.  CalcReadStats (integer sums, order-free) and MonomorphismLogLikelihood
+// (serial double sum, kept in the reference's person order) -- NucFamGenotypeLikelihood.cpp:502-546.
 __global__ void __launch_bounds__(256) k_prep(DevArgs A) {
   __shared__ unsigned long long s_c[9];
   if (threadIdx.x < 9) s_c[threadIdx.x] = 0;
   __syncthreads();
-  const int site = blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int site = wave;
   bool valid = false;
   if (site < A.n) {
     const int r = A.ref[site];
     const int np = A.n_person;
     const uint8_t* pl = A.pl + (size_t)site * np * 10;
     const uint32_t* dm = A.dm + (size_t)site * np;
-    pm_site_result* R = A.res + site;
     const bool okref = r >= 1 && r <= 4;
     const int h = okref ? d_gi(r, r) : 0;
-    int dsum = 0, nsd = 0;
-    double mq = 0.0, mono = 0.0;
-    for (int p = 0; p < np; p++) {
-      const uint32_t x = dm[p];
+    long long dsum = 0, mqsum = 0, nsd = 0;
+    double mono = 0.0;
+    for (int base = 0; base < np; base += 64) {
+      const int p = base + lane;
+      uint32_t x = 0;
+      int hr = 0;
+      if (p < np) { x = dm[p]; hr = pl[(size_t)p * 10 + h]; }
       const int d = (int)(x & 0xFFFFFF);
-      dsum += d; mq += (double)(x >> 24); nsd += d > 0;
-      mono += -(double)(pl[(size_t)p * 10 + h]) / 10;
+      dsum += d; mqsum += (x >> 24); nsd += d > 0;
+      mono = wave_serial_add(mono, -(double)hr / 10, hr != 0);
     }
-    pm_site_result O;
-    memset(&O, 0, sizeof(O));
-    O.maxidx = -2; O.call_row = -1; O.ab = 0.5; O.denovo_lr = -1;
-    A.mono_plain[site] = mono;
-    if (!okref) O.status = PM_SITE_BAD_REF;
-    else {
-      atomicAdd(&s_c[r], 1ull);
-      double avgmq = 0., ps = 0.;
-      if (nsd > 0) { avgmq = mq / (double)nsd; ps = (double)nsd / (double)np; }
-      O.total_depth = dsum; O.num_samp_with_data = nsd; O.avg_map_qual = avgmq; O.perc_samp_with_data = ps;
-      int st = 0;   // filters, main.cpp:345-348
-      if (dsum < A.min_total_depth) st = PM_SITE_MIN_DEPTH;
-      else if (A.max_total_depth > 0 && dsum > A.max_total_depth) st = PM_SITE_MAX_DEPTH;
-      else if (ps * 100 < A.min_ps) st = PM_SITE_MIN_PS;
-      else if (avgmq < A.min_map_quality) st = PM_SITE_MIN_MAPQ;
-      if (st) { O.status = st; atomicAdd(&s_c[4 + st], 1ull); }
-      else { O.status = PM_SITE_CALLED; valid = true; }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { dsum += __shfl_xor(dsum, o, 64); mqsum += __shfl_xor(mqsum, o, 64); nsd += __shfl_xor(nsd, o, 64); }
+    if (lane == 0) {
+      pm_site_result O;
+      memset(&O, 0, sizeof(O));
+      O.maxidx = -2; O.call_row = -1; O.ab = 0.5; O.denovo_lr = -1;
+      A.mono_plain[site] = mono;
+      if (!okref) O.status = PM_SITE_BAD_REF;
+      else {
+        atomicAdd(&s_c[r], 1ull);
+        const int td = (int)dsum, n = (int)nsd;
+        double avgmq = 0., ps = 0.;
+        if (n > 0) { avgmq = (double)mqsum / (double)n; ps = (double)n / (double)np; }
+        O.total_depth = td; O.num_samp_with_data = n; O.avg_map_qual = avgmq; O.perc_samp_with_data = ps;
+        int st = 0;   // filters, main.cpp:345-348
+        if (td < A.min_total_depth) st = PM_SITE_MIN_DEPTH;
+        else if (A.max_total_depth > 0 && td > A.max_total_depth) st = PM_SITE_MAX_DEPTH;
+        else if (ps * 100 < A.min_ps) st = PM_SITE_MIN_PS;
+        else if (avgmq < A.min_map_quality) st = PM_SITE_MIN_MAPQ;
+        if (st) { O.status = st; atomicAdd(&s_c[4 + st], 1ull); }
+        else { O.status = PM_SITE_CALLED; valid = true; }
+      }
+      A.res[site] = O;
+      if (valid) {
+        const int nit = A.denovo ? 4 : 3;
+        const int slot = atomicAdd(&A.counts[0], nit);
+        for (int k = 0; k < nit; k++) A.items[0][slot + k] = (site << 3) | (A.denovo ? k : k + 1);
+      }
     }
-    *R = O;
-  }
-  // enqueue (site, configuration) Brent items, one atomic per wave
-  const int nit = A.denovo ? 4 : 3;
-  const unsigned long long bal = __ballot(valid);
-  const int lane = threadIdx.x & 63;
-  int base = 0;
-  if (lane == 0 && bal) base = atomicAdd(&A.counts[0], nit * __popcll(bal));
-  base = __shfl(base, 0, 64);
-  if (valid) {
-    const int slot = base + nit * __popcll(bal & ((1ull << lane) - 1ull));
-    for (int k = 0; k < nit; k++) A.items[0][slot + k] = (site << 3) | (A.denovo ? k : k + 1);
   }
   __syncthreads();
   if (threadIdx.x < 9 && s_c[threadIdx.x]) atomicAdd(&A.counters[threadIdx.x], s_c[threadIdx.x]);
@@ -783,7 +889,7 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
       ItemCtx I;
       I.a1 = a1; I.a2 = a2; I.g11 = g11; I.g12 = g12; I.g22 = g22; I.denovo = dn; I.sex = msex; I.chrom = chrom;
       double cond[9], pp[9], pg[9];
-      hoist_nuc(A, I, pl, s_lk, s_M, p0, n, cond);
+      hoist_nuc<true>(A, I, pl, s_lk, s_M, p0, n, cond);
       int pmode;
       if (dn) pmode = A.n_fam_gt1 ? PR_AUTO : PR_DN_SINGLE;
       else if (!A.n_fam_gt1 && !is_mono) pmode = PR_TRIO;
@@ -883,11 +989,11 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
 // the two sums accumulated serially in person order (bit-identical to the reference).
 __global__ void __launch_bounds__(256) k_ab(DevArgs A) {
   __shared__ double s_lk[256];
-  __shared__ double s_ab[2][256];
   for (int i = threadIdx.x; i < 256; i += blockDim.x) s_lk[i] = A.lktab[i];
   __syncthreads();
+  const int lane = threadIdx.x & 63;
   const int rows = A.counts[3];
-  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += gridDim.x * 4) {
     const int site = A.row_site[row];
     const pm_site_result* R = A.res + site;
     const int np = A.n_person;
@@ -895,41 +1001,38 @@ __global__ void __launch_bounds__(256) k_ab(DevArgs A) {
     const uint32_t* dm = A.dm + (size_t)site * np;
     const int a1 = R->allele1, a2 = R->allele2;
     const int g11 = d_gi(a1, a1), g12 = d_gi(a1, a2), g22 = d_gi(a2, a2);
-    const int dn = A.denovo, chrom = A.chrom;
-    if (!dn && chrom == PM_CHR_AUTO) {
-      const double fr = R->af;
-      const double p11 = fr * fr, p12 = 2 * fr * (1 - fr), p22 = (1 - fr) * (1 - fr);
-      double Asum = 0.0, Bsum = 0.0;
-      for (int base = 0; base < np; base += 256) {
-        const int p = base + threadIdx.x;
-        double ta = 0.0, tb = 0.0;
-        bool use = false;
-        if (p < np) {
-          const int depth = (int)(dm[p] & 0xFFFFFF);
-          const uint8_t* Rr = pl + (size_t)p * 10;
-          const double l11 = s_lk[Rr[g11]], l12 = s_lk[Rr[g12]], l22 = s_lk[Rr[g22]];
-          const int k11 = Rr[g11], k12 = Rr[g12], k22 = Rr[g22];
-          const double PHet = (p12 * l12) / (p11 * l11 + p12 * l12 + p22 * l22);
-          if (PHet > 1e-05 && depth > 0) {
-            int scale = k22 + k11 - 2 * k12 + 6 * depth;
-            const int minimum = abs(k22 - k11);
-            if (scale < 4) scale = 4;
-            if (scale < minimum) scale = minimum;
-            const int nRef = (int)(0.5 * depth * (1 + (k22 - k11) / (scale + 1e-30)));
-            ta = PHet * nRef; tb = PHet * depth; use = true;
-          }
+    const double fr = R->af;
+    const double p11 = fr * fr, p12 = 2 * fr * (1 - fr), p22 = (1 - fr) * (1 - fr);
+    double Asum = 0.0, Bsum = 0.0;
+    for (int base = 0; base < np; base += 64) {
+      const int p = base + lane;
+      double ta = 0.0, tb = 0.0;
+      bool use = false;
+      if (p < np) {
+        const int depth = (int)(dm[p] & 0xFFFFFF);
+        const uint8_t* Rr = pl + (size_t)p * 10;
+        const int k11 = Rr[g11], k12 = Rr[g12], k22 = Rr[g22];
+        const double l11 = s_lk[k11], l12 = s_lk[k12], l22 = s_lk[k22];
+        const double PHet = (p12 * l12) / (p11 * l11 + p12 * l12 + p22 * l22);
+        if (PHet > 1e-05 && depth > 0) {
+          int scale = k22 + k11 - 2 * k12 + 6 * depth;
+          const int minimum = abs(k22 - k11);
+          if (scale < 4) scale = 4;
+          if (scale < minimum) scale = minimum;
+          const int nRef = (int)(0.5 * depth * (1 + (k22 - k11) / (scale + 1e-30)));
+          ta = PHet * nRef; tb = PHet * depth; use = true;
         }
-        s_ab[0][threadIdx.x] = use ? ta : 0.0;
-        s_ab[1][threadIdx.x] = use ? tb : -1.0;   // -1 marks "no contribution"
-        __syncthreads();
-        if (threadIdx.x == 0) {
-          const int cnt = min(256, np - base);
-          for (int i = 0; i < cnt; i++) if (s_ab[1][i] >= 0.0) { Asum += s_ab[0][i]; Bsum += s_ab[1][i]; }
-        }
-        __syncthreads();
       }
-      if (threadIdx.x == 0) A.res[site].ab = (0.05 + Asum) / (0.1 + Bsum);
+      // A += PHet*nRef; B += PHet*depth in person order (only contributing persons change the sums)
+      unsigned long long m = __ballot(use);
+      while (m) {
+        const int l = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        Asum += __shfl(ta, l, 64);
+        Bsum += __shfl(tb, l, 64);
+      }
     }
+    if (lane == 0) A.res[site].ab = (0.05 + Asum) / (0.1 + Bsum);
   }
 }
 
@@ -985,6 +1088,7 @@ struct pm_engine {
   int chrom = PM_CHR_AUTO;
   int T = 64, S = 1;
   int grid_brent = 1024;
+  bool has_fp = false;
   int last_n = 0;
   int n_cu = 256;
   bool carry_postprob = false;
@@ -1049,7 +1153,8 @@ static int dalloc(X** p, size_t count) {
 }
 #define DALLOC(p, n) do { int _r = dalloc(&(p), (n)); if (_r) { pm_engine_destroy(E); return _r; } } while (0)
 
-static const struct { int T, S; } kVariants[] = {{64, 1}, {64, 2}, {64, 4}, {128, 4}, {256, 4}, {512, 4}, {1024, 4}, {1024, 8}};
+static const struct { int T, S; } kVariants[] = {{64, 1}, {64, 2}, {64, 4}, {128, 4}, {256, 4}, {512, 2}, {512, 4},
+                                                 {1024, 1}, {1024, 2}, {1024, 4}, {1024, 8}, {128, 8}, {64, 8}, {64, 16}};
 
 // Deal families to lanes: family-major round robin; founders-only families are split into <=3-person chunks
 // kept on one lane.  Returns false if the plan does not fit T x S.
@@ -1126,6 +1231,7 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
   E->max_batch = max_batch;
   E->n_founders = ped->n_founders; E->male_founders = ped->male_founders; E->female_founders = ped->female_founders;
   E->single_nuclear = (ped->n_fam == 1 && ped->fam_kind[0] == PM_FAM_NUCLEAR) ? 1 : 0;
+  for (int f = 0; f < ped->n_fam; f++) if (ped->fam_kind[f] != PM_FAM_NUCLEAR) E->has_fp = true;
   E->fam_start_h.assign(ped->fam_start, ped->fam_start + ped->n_fam + 1);
   E->sex_h.assign(ped->sex, ped->sex + ped->n_person);
   HIP_TRY(hipSetDevice(device));
@@ -1135,8 +1241,25 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
   // plan
   std::vector<int4> units;
   bool planned = false;
-  for (auto v : kVariants) {
-    if (plan_units(ped, v.T, v.S, units)) { E->T = v.T; E->S = v.S; planned = true; break; }
+  // optional override for geometry experiments: PM_BRENT_TS="T,S"
+  if (const char* ov = getenv("PM_BRENT_TS")) {
+    int t = 0, sl = 0;
+    if (sscanf(ov, "%d,%d", &t, &sl) == 2)
+      for (auto v : kVariants)
+        if (v.T == t && v.S == sl && plan_units(ped, t, sl, units)) { E->T = t; E->S = sl; planned = true; }
+  }
+  // default: the first geometry (in preference order) that holds every family.  One wave per item
+  // (T=64, no barrier) wins while its slots fit the register file without scratch: up to S=16 for the
+  // lean autosomal kernel, S=8 for the generic one (de novo / founders-only units); beyond that the item
+  // is spread over 2-8 waves (one barrier per evaluation).  Sections on chrX/Y/MT run the generic
+  // kernel on the same plan.
+  {
+    const bool gen = par->denovo || E->has_fp;
+    static const int2 lean[] = {{64, 1}, {64, 2}, {64, 4}, {64, 8}, {64, 16}, {512, 4}, {1024, 4}, {1024, 8}};
+    static const int2 generic[] = {{64, 1}, {64, 2}, {64, 4}, {64, 8}, {256, 4}, {512, 4}, {1024, 4}, {1024, 8}};
+    const int2* pref = gen ? generic : lean;
+    for (int i = 0; i < 8 && !planned; i++)
+      if (plan_units(ped, pref[i].x, pref[i].y, units)) { E->T = pref[i].x; E->S = pref[i].y; planned = true; }
   }
   if (!planned) { pm_engine_destroy(E); pm_set_last_error("pm_engine_create: pedigree too large for the lane plan"); return PM_EPED; }
   hipDeviceProp_t prop;
@@ -1247,15 +1370,22 @@ static DevArgs make_args(pm_engine* E, int n, const uint8_t* pl, const uint32_t*
 }
 
 typedef void (*BrentFn)(DevArgs, int);
-static BrentFn brent_kernel(int T, int S) {
-#define PMK(t, s) if (T == t && S == s) return k_brent<t, s>;
-  PMK(64, 1) PMK(64, 2) PMK(64, 4) PMK(128, 4) PMK(256, 4) PMK(512, 4) PMK(1024, 4) PMK(1024, 8)
+static BrentFn brent_kernel(int T, int S, bool prod, bool gen) {
+#define PMK(t, s)                                                                     \
+  if (T == t && S == s) {                                                             \
+    if (gen) return prod ? k_brent<t, s, true, true> : k_brent<t, s, false, true>;    \
+    return prod ? k_brent<t, s, true, false> : k_brent<t, s, false, false>;           \
+  }
+  PMK(64, 1) PMK(64, 2) PMK(64, 4) PMK(128, 4) PMK(256, 4) PMK(512, 2) PMK(512, 4) PMK(1024, 1) PMK(1024, 2)
+  PMK(1024, 4) PMK(1024, 8) PMK(128, 8) PMK(64, 8) PMK(64, 16)
 #undef PMK
   return nullptr;
 }
 
 static int launch_brent(pm_engine* E, const DevArgs& A, int list) {
-  BrentFn fn = brent_kernel(E->T, E->S);
+  // lean kernel: autosome, no de novo model, nuclear families only (the common case)
+  const bool gen = E->chrom != PM_CHR_AUTO || E->par.denovo || E->has_fp;
+  BrentFn fn = brent_kernel(E->T, E->S, !E->par.exact_log10, gen);
   hipEvent_t a, b;
   HIP_TRY(hipEventCreate(&a));
   HIP_TRY(hipEventCreate(&b));
@@ -1276,7 +1406,7 @@ static int run_pipeline(pm_engine* E, int n, const uint8_t* pl, const uint32_t* 
     const int big = 0x7fffffff;   // counts[4] = first emitted site (atomicMin)
     HIP_TRY(hipMemcpyAsync(E->d_counts + 4, &big, sizeof(int), hipMemcpyHostToDevice, E->stream));
   }
-  hipLaunchKernelGGL(k_prep, dim3((n + 255) / 256), dim3(256), 0, E->stream, A);
+  hipLaunchKernelGGL(k_prep, dim3((n + 3) / 4), dim3(256), 0, E->stream, A);
   HIP_TRY(hipGetLastError());
   int rc;
   if ((rc = launch_brent(E, A, 0))) return rc;

@@ -15,7 +15,7 @@ struct Options {
   double posterior = 0.5, theta = 0.001, theta_indel = 0.0001, tstv = 2.0, precision = 0.0001;
   int minTotalDepth = 0, maxTotalDepth = 0, minMapQuality = 0, nthreads = 1;
   double minPS = 0;
-  bool denovo = false, gl_off = false, quick_call = false, all_sites = false, force_call = false;
+  bool denovo = false, gl_off = false, quick_call = false, all_sites = false, force_call = false, exact_log10 = false;
   double denovo_rate = 1.5e-08, denovo_tstv = 2.0, denovo_llr = 0.01;
   int device = 0, batch = 4096;
   std::string cmd;
