@@ -68,7 +68,14 @@ bool synth_shape(const std::string& shape, int fam, std::vector<SynthMember>& ou
   return false;
 }
 
-int synth_write_dataset(const std::string& dir, const std::string& shape, int nfam, int nsites, uint64_t seed, std::string& err) {
+// shape "<template>+dn": additionally plants a de novo het call (ref/transition) in one non-founder
+// of one family at ~3% of sites, so the --denovo output path has records to check.  Files only:
+// the device generator (bench) never plants.
+int synth_write_dataset(const std::string& dir, const std::string& shape_arg, int nfam, int nsites, uint64_t seed,
+                        std::string& err) {
+  std::string shape = shape_arg;
+  bool plant = false;
+  if (shape.size() > 3 && shape.compare(shape.size() - 3, 3, "+dn") == 0) { plant = true; shape.resize(shape.size() - 3); }
   mkdir(dir.c_str(), 0755);
   static pm_synth_tables T;
   static bool built = false;
@@ -124,6 +131,21 @@ int synth_write_dataset(const std::string& dir, const std::string& shape, int nf
       fa.resize(n); mo.resize(n); pl.resize((size_t)n * 10); dm.resize(n); hap.resize(n);
       for (int j = 0; j < n; j++) { fa[j] = F[j].fa; mo[j] = F[j].mo; }
       pm_syn_family(&T, seed, (uint64_t)s, ref, af, n, fa.data(), mo.data(), gbase[f], pl.data(), dm.data(), hap.data());
+      if (plant && pm_u01(seed, (uint64_t)s, 0, 901) < 0.03 &&
+          (int)(pm_u01(seed, (uint64_t)s, 0, 902) * nfam) == f) {
+        int kids[64], nk = 0;
+        for (int j = 0; j < n && nk < 64; j++) if (fa[j] >= 0) kids[nk++] = j;
+        if (nk > 0) {
+          const int j = kids[(int)(pm_u01(seed, (uint64_t)s, 0, 903) * nk) % nk];
+          static const int gidx[4][4] = {{0, 1, 2, 3}, {1, 4, 5, 6}, {2, 5, 7, 8}, {3, 6, 8, 9}};
+          const int alt = ref == 1 ? 3 : ref == 3 ? 1 : ref == 2 ? 4 : 2;
+          uint8_t* q = pl.data() + (size_t)j * 10;
+          for (int g = 0; g < 10; g++) q[g] = 255;
+          q[gidx[ref - 1][ref - 1]] = 45;
+          q[gidx[ref - 1][alt - 1]] = 0;
+          q[gidx[alt - 1][alt - 1]] = 90;
+        }
+      }
       for (int j = 0; j < n; j++) {
         uint8_t rec[20];
         rec[0] = (uint8_t)(0x10 | iupac[ref]);

@@ -40,3 +40,15 @@ def built():
     if not os.path.exists(lib):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "polymutt_amd")], check=True)
     return True
+
+
+@pytest.fixture(scope="session")
+def cpu_driver():
+    """tests/native/build/cpu_polymutt: the product host driver with the CPU oracle as evaluator."""
+    exe = os.path.join(ROOT, "tests", "native", "build", "cpu_polymutt")
+    import __graft_entry__
+    srcs = [os.path.join(ROOT, "tests", "native", "cpu_polymutt.cpp"), os.path.join(ROOT, "oracle", "pm_oracle.c")] + \
+        [os.path.join(ROOT, "polymutt_amd", "host", f) for f in os.listdir(os.path.join(ROOT, "polymutt_amd", "host"))]
+    if not os.path.exists(exe) or max(os.path.getmtime(s) for s in srcs) > os.path.getmtime(exe):
+        __graft_entry__.build_cpu_driver()
+    return exe

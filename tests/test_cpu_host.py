@@ -1,0 +1,178 @@
+"""CPU tests of the drop-in boundary and the host side: the C-ABI library loads and exports every
+entry point include/*.h declares, the product fails loudly without a HIP device, the pedigree loader
+and Elston-Stewart schedule builder reproduce the reference's ordering, the
+synthetic generator is identical between its host and GLF-file forms, and site sharding plus the
+single counter all-reduce equals the unsharded section (gloo, world_size 2)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import polymutt_amd as pm
+from conftest import EXAMPLE, ROOT
+from polymutt_amd.shard import shard_range
+
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("polymutt_engine.h", "polymutt_host.h")]
+
+
+def _declared_functions():
+    names = set()
+    for h in HEADERS:
+        text = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        for m in re.finditer(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b(pmh?_\w+)\s*\(", text, flags=re.M):
+            names.add(m.group(1))
+    return names
+
+
+def _gpu():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+def test_library_exports_every_declared_entry_point():
+    declared = _declared_functions()
+    assert len(declared) >= 25, declared
+    lib = C.CDLL(pm.LIB_PATH)
+    missing = [n for n in sorted(declared) if not hasattr(lib, n)]
+    assert not missing, missing
+    # the Python binding declares exactly the header's surface
+    assert declared == set(pm.engine.EXPORTS), declared ^ set(pm.engine.EXPORTS)
+    nm = subprocess.run(["nm", "-D", "--defined-only", pm.LIB_PATH], capture_output=True, text=True).stdout
+    exported = {l.split()[-1] for l in nm.splitlines() if " T " in l}
+    assert declared <= exported
+
+
+def test_abi_version_and_struct_layout():
+    lib = pm.load_library()
+    src = open(HEADERS[0]).read()
+    ver = int(re.search(r"#define PM_ABI_VERSION (\d+)", src).group(1))
+    assert lib.pm_abi_version() == ver
+    assert C.sizeof(pm.SiteResult) == 240 and C.sizeof(pm.GenoCall) == 16
+    assert C.sizeof(pm.Counters) == 16 * 8
+
+
+@pytest.mark.skipif(_gpu(), reason="checks the no-device failure path")
+def test_engine_fails_loudly_without_device():
+    ped = pm.Pedigree(os.path.join(EXAMPLE, "test.dat"), os.path.join(EXAMPLE, "test.ped"))
+    with pytest.raises(RuntimeError, match="no HIP device"):
+        pm.Engine(ped.view, pm.Params.defaults())
+
+
+@pytest.mark.skipif(_gpu(), reason="checks the no-device failure path")
+def test_cli_fails_loudly_without_device(tmp_path):
+    r = subprocess.run([pm.BIN_PATH, "-p", "test.ped", "-d", "test.dat", "-g", "test.gif", "--out_vcf",
+                        str(tmp_path / "o.vcf")], cwd=EXAMPLE, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    assert "FATAL ERROR" in r.stdout and "HIP device" in r.stdout
+    assert not (tmp_path / "o.vcf").exists() or "#CHROM" not in (tmp_path / "o.vcf").read_text()
+
+
+def test_cli_rejects_unknown_option():
+    r = subprocess.run([pm.BIN_PATH, "--no_such_flag"], capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0 and "FATAL ERROR" in r.stdout
+
+
+def test_example_pedigree_layout():
+    ped = pm.Pedigree(os.path.join(EXAMPLE, "test.dat"), os.path.join(EXAMPLE, "test.ped"))
+    assert ped.n_fam == 3 and ped.n_person == 12
+    assert list(ped.fam_start()) == [0, 4, 8, 12]
+    assert list(ped.fam_kind()) == [pm.FAM_NUCLEAR] * 3
+    assert list(ped.sex()[:4]) == [1, 2, 1, 2] or set(ped.sex()) <= {1, 2}
+    mix = pm.Pedigree(os.path.join(EXAMPLE, "test.dat"), os.path.join(EXAMPLE, "test.mix.ped"))
+    kinds = list(mix.fam_kind())
+    assert kinds.count(pm.FAM_NUCLEAR) == 2 and kinds.count(pm.FAM_FOUNDERS) == 4
+
+
+def _steps(ped, f):
+    v = ped.view
+    ps = np.ctypeslib.as_array(v.peel_start, shape=(v.n_fam + 1,))
+    return [(v.steps[i].type, v.steps[i].from0, v.steps[i].from1, v.steps[i].to0, v.steps[i].to1)
+            for i in range(ps[f], ps[f + 1])]
+
+
+@pytest.mark.parametrize("shape,expected", [
+    # SURVEY.md Appendix C, observed with the reference's own ES_Peeling
+    ("ext10", [(1, 6, -1, 4, 2), (1, 7, -1, 4, 2), (1, 8, -1, 3, 5), (1, 9, -1, 3, 5), (2, 2, -1, 4, -1),
+               (2, 3, -1, 5, -1), (1, 4, -1, 0, 1), (1, 5, -1, 0, 1), (2, 0, -1, 1, -1)]),
+    ("roof", [(1, 6, -1, 4, 5), (1, 7, -1, 4, 5), (3, 0, 1, 4, -1), (3, 2, 3, 5, -1), (2, 4, -1, 5, -1)]),
+])
+def test_peeling_schedule_matches_reference(tmp_path, shape, expected):
+    pm.synth_write_dataset(str(tmp_path), shape, 2, 1, 1)
+    ped = pm.Pedigree(str(tmp_path / "test.dat"), str(tmp_path / "test.ped"))
+    assert list(ped.fam_kind()) == [pm.FAM_EXTENDED] * 2
+    for f in range(2):
+        assert _steps(ped, f) == expected
+
+
+def test_synthetic_host_block_equals_glf_files(tmp_path):
+    from fixtures import read_dataset
+    for shape, nfam in [("quad", 13), ("mixed", 9), ("ext10", 3), ("single", 5)]:
+        d = tmp_path / shape
+        pm.synth_write_dataset(str(d), shape, nfam, 97, 5)
+        ped, secs, _ = read_dataset(str(d))
+        (label, pos, ref, pl, dm), = secs
+        assert label == "1" and (np.diff(pos) == 1).all()
+        hpl, hdm, href = pm.synth_block_host(ped.view, 97, 5)
+        assert (hpl == pl).all() and (hdm == dm).all() and (href == ref).all()
+        # depth U{8..29}, mapQ 60, PL 255 outside the 3 biallelic genotypes
+        depth, mq = dm & 0xFFFFFF, dm >> 24
+        assert depth.min() >= 8 and depth.max() <= 29 and (mq == 60).all()
+        assert ((pl == 255).sum(axis=-1) >= 7).all() and (pl.min(axis=-1) == 0).all()
+
+
+def test_shard_range_partitions():
+    for n in (0, 1, 7, 1000, 1001):
+        for w in (1, 2, 3, 8):
+            rs = [shard_range(n, r, w) for r in range(w)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+            assert max(h - l for l, h in rs) - min(h - l for l, h in rs) <= 1
+
+
+def _sharded_worker(rank, world, port, d, out):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from fixtures import read_dataset
+    from oracle_binding import Oracle
+    from polymutt_amd.shard import allreduce_counters
+    ped, secs, _ = read_dataset(d)
+    (label, pos, ref, pl, dm), = secs
+    lo, hi = shard_range(len(ref), rank, world)
+    ora = Oracle(ped.view, pm.Params.defaults())
+    ora.begin_section(pm.PM_CHR_AUTO)
+    ora.run(pl[lo:hi], dm[lo:hi], ref[lo:hi])
+    total = allreduce_counters(ora.counters().as_array())
+    if rank == 0:
+        np.save(out, total)
+    dist.destroy_process_group()
+
+
+def test_sharded_counters_allreduce_gloo(tmp_path):
+    import socket
+    import torch.multiprocessing as mp
+    from fixtures import read_dataset
+    from oracle_binding import Oracle
+    d = str(tmp_path / "ds")
+    pm.synth_write_dataset(d, "quad", 20, 301, 9)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = str(tmp_path / "total.npy")
+    mp.start_processes(_sharded_worker, args=(2, port, d, out), nprocs=2, join=True, start_method="spawn")
+    ped, secs, _ = read_dataset(d)
+    (label, pos, ref, pl, dm), = secs
+    ora = Oracle(ped.view, pm.Params.defaults())
+    ora.begin_section(pm.PM_CHR_AUTO)
+    ora.run(pl, dm, ref)
+    whole = ora.counters().as_array()
+    assert (np.load(out) == whole).all()
+    assert whole[:5].sum() == 301

@@ -1,0 +1,68 @@
+"""CPU tests: the oracle (oracle/pm_oracle.c) and the product host driver (GLF reader, pedigree
+loader, VCF writer, CLI) pinned against the reference -- its committed example goldens and the
+per-site dumps / VCFs of its own objects on synthetic datasets (tests/golden/synth)."""
+import gzip
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import polymutt_amd as pm
+from conftest import EXAMPLE
+from fixtures import CASES, compare_to_dump, golden_dump, golden_vcf_body, make_dataset, params_and_chrom, read_dataset
+from oracle_binding import Oracle
+
+
+def _body(path):
+    return [l for l in open(path).read().splitlines() if not l.startswith("##")]
+
+
+EXAMPLE_RUNS = [
+    (["-p", "test.ped", "-d", "test.dat", "-g", "test.gif", "-c", "0.9", "--minDepth", "150", "--maxDepth", "200",
+      "--nthreads", "4"], "test.out.vcf.body.gz"),
+    (["-p", "test.mix.ped", "-d", "test.dat", "-g", "test.gif"], "test.out.vcfa.body.gz"),
+    (["-p", "test.ped", "-d", "test.dat", "-g", "test.gif", "--nthreads", "4", "--denovo", "--rate_denovo", "1.5e-07"],
+     "test.denovo.out.vcf"),
+]
+
+
+@pytest.mark.parametrize("args,golden", EXAMPLE_RUNS, ids=["default_filters", "mix_ped", "denovo"])
+def test_cpu_driver_reproduces_example_goldens(cpu_driver, tmp_path, args, golden):
+    out = tmp_path / "out.vcf"
+    r = subprocess.run([cpu_driver] + args + ["--out_vcf", str(out)], cwd=EXAMPLE, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:]
+    p = os.path.join(EXAMPLE, golden)
+    exp = gzip.open(p, "rt").read().splitlines() if p.endswith(".gz") else _body(p)
+    got = _body(out)
+    assert got == exp
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_oracle_matches_reference_dump(built, tmp_path, name):
+    case = make_dataset(name, str(tmp_path))
+    ped, secs, sha = read_dataset(str(tmp_path))
+    assert sha == case["block_sha256"], "synthetic generator no longer reproduces the reference's inputs"
+    par, chrom = params_and_chrom(case["flags"])
+    ora = Oracle(ped.view, par)
+    ora.begin_section(chrom)
+    (label, pos, ref, pl, dm), = secs
+    res, _ = ora.run(pl, dm, ref)
+    st = compare_to_dump(res, golden_dump(name), label=name + " ")
+    assert st["sites"] == case["dumped_sites"]
+    # same Brent in the same arithmetic order: identical evaluation counts and minimisers
+    assert st["eval_path_mismatch"] == 0 and st["flat_divergence"] == 0, st
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_cpu_driver_matches_reference_vcf(cpu_driver, tmp_path, name):
+    case = make_dataset(name, str(tmp_path))
+    r = subprocess.run([cpu_driver, "-p", "test.ped", "-d", "test.dat", "-g", "test.gif", "--out_vcf", "out.vcf"]
+                       + case["flags"], cwd=tmp_path, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:]
+    exp = [l for l in golden_vcf_body(name) if l]
+    got = _body(tmp_path / "out.vcf") if os.path.exists(tmp_path / "out.vcf") else []
+    assert len(got) == len(exp)
+    diff = [i for i, (a, b) in enumerate(zip(got, exp)) if a != b]
+    assert not diff, f"{len(diff)} lines differ; first:\n{got[diff[0]][:300]}\n{exp[diff[0]][:300]}"
