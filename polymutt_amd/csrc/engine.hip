@@ -74,6 +74,18 @@ struct DevArgs {
   const int32_t* mo_local;
   const int4* units;       // [S][T]
   int T, S;
+  // Elston-Stewart (extended families): per-lane family lists, packed schedules, workspace
+  const int* fam_founders;
+  const int8_t* is_founder;
+  const int* peel_start;   // [n_fam+1] into steps
+  const int2* steps;       // packed pm_peel_step + marriage-partial slot (see pack_steps)
+  const int* ext_count;    // [T] ES families per lane
+  const int* ext_fam;      // [max_ext][T]
+  const double* T10;       // FamilyLikelihoodES::transmission        [10][10][10]
+  const double* T10dn;     // FamilyLikelihoodES::transmission_denovo [10][10][10]
+  double* ws;              // peeling workspace, lane-interleaved
+  int ws_per_lane;         // doubles per lane (max over ES families of n*ns + couples*ns*ns)
+  int unrelated;           // --quick_call MakeUnrelated(): every family is all-founder
   // tables
   const double* lktab;     // [256]
   const double* M;         // [100] genotype mutation matrix
@@ -272,6 +284,128 @@ __device__ __forceinline__ int hoist_fp(const DevArgs& A, const ItemCtx& I, cons
 }
 
 // ------------------------------------------------------------------------------------------------
+// Elston-Stewart peeling of one extended family (FamilyLikelihoodES.cpp), one lane per family.
+// Restates CalcSingleFamLikelihood_BA / _denovo (FamilyLikelihoodSeq.cpp:256-279) with FillZeroPenetrance
+// (:327-356) for the posteriors: SetFounderPriors(_BA) :643-687, InitializePartials(_BA) :1434-1465,
+// peelOffspring2Parents :1105-1130/:1289-1310, peelSpouse2Spouse :1182-1230/:1312-1356,
+// peelParents2Offspring :1260-1286/:1358-1395, CalculateLikelihood_BA :1013-1032.  Operation order is
+// the reference's, so every family likelihood is bit-identical to it.  partials[n][ns] and the marriage
+// partials [couples][ns][ns] live in a per-lane HBM workspace interleaved across lanes (coalesced, L2-hot).
+//
+// packed step: x = type | from0 << 8 | from1 << 16 | to0 << 24, y = to1 | slot << 8 | create << 16 | fa2mo << 17
+// (255 = none); slot = marriage-partial index resolved on the host (created by the first type-1 step of a couple).
+__constant__ double c_TBA[5][27];   // transmission_BA, _CHRX_2Female, _CHRX_2Male, _CHRY, _MITO (:812-924)
+
+__device__ __forceinline__ double d_tba(int i, int j, int k, int chrom, int child_sex) {   // GetTransmissionProb_BA :1059-1075
+  const int o = i * 9 + j * 3 + k;
+  double t = c_TBA[0][o];
+  if (chrom == PM_CHR_X) t = (child_sex == MALE) ? c_TBA[2][o] : c_TBA[1][o];
+  if (chrom == PM_CHR_Y) t = (child_sex == MALE) ? c_TBA[3][o] : 1.0;
+  if (chrom == PM_CHR_MT) t = c_TBA[4][o];
+  return t;
+}
+
+template <int NS>
+__device__ __forceinline__ double d_es_lk(const DevArgs& A, int f, const uint8_t* pl, const double* lk, int g11, int g12, int g22, int chrom,
+                          double freq, int zp, int zg, double* ws, size_t st) {
+  const int p0 = A.fam_start[f], n = A.fam_start[f + 1] - p0, nf = A.fam_founders[f];
+  const bool X = chrom == PM_CHR_X, Y = chrom == PM_CHR_Y, MT = chrom == PM_CHR_MT;
+  const int gidx[3] = {g11, g12, g22};
+#define PP(i, j) ws[((size_t)(i) * NS + (j)) * st]
+#define MPP(sl, x, y) ws[((size_t)n * NS + (size_t)(sl) * NS * NS + (x) * NS + (y)) * st]
+  for (int i = 0; i < n; i++) {
+    const int sx = A.sex[p0 + i];
+    const bool fo = A.is_founder[p0 + i] != 0;
+    const uint8_t* R = pl + (size_t)(p0 + i) * 10;
+    if (NS == 3) {
+      double pr[3] = {0.0, 0.0, 0.0};
+      if (i < nf) {
+        pr[0] = freq * freq; pr[1] = 2 * freq * (1 - freq); pr[2] = (1 - freq) * (1 - freq);
+        if (X) if (sx == MALE) { pr[0] = freq; pr[1] = 0; pr[2] = 1 - freq; }
+        if (Y) { if (sx == MALE) { pr[0] = freq; pr[1] = 0; pr[2] = 1 - freq; } else { pr[0] = 1; pr[1] = 1; pr[2] = 1; } }
+        if (MT) { pr[0] = freq; pr[1] = 0; pr[2] = 1 - freq; }
+      }
+#pragma unroll
+      for (int j = 0; j < 3; j++) {
+        const double pen = (zp == i && gidx[j] != zg) ? 0.0 : lk[R[gidx[j]]];
+        PP(i, j) = (Y && sx == FEMALE) ? 1.0 : (fo ? pr[j] * pen : pen);
+      }
+    } else {
+      double pr[10];
+#pragma unroll
+      for (int j = 0; j < 10; j++) pr[j] = 0.0;
+      if (i < nf) {
+        double q0 = freq * freq, q1 = 2 * freq * (1 - freq), q2 = (1 - freq) * (1 - freq);
+        if (X) if (sx == MALE) { q0 = freq; q1 = 0; q2 = 1 - freq; }
+        if (Y) { if (sx == MALE) { q0 = freq; q1 = 0; q2 = 1 - freq; } else { q0 = 1; q1 = 1; q2 = 1; } }
+        if (MT) { q0 = freq; q1 = 0; q2 = 1 - freq; }
+        // pr[gidx[0]] = q0; pr[gidx[1]] = q1; pr[gidx[2]] = q2 (static indexing keeps pr in registers)
+#pragma unroll
+        for (int j = 0; j < 10; j++) pr[j] = (j == g22) ? q2 : (j == g12) ? q1 : (j == g11) ? q0 : 0.0;
+      }
+#pragma unroll
+      for (int j = 0; j < 10; j++) {
+        const double pen = (zp == i && j != zg) ? 0.0 : lk[R[j]];
+        PP(i, j) = fo ? pr[j] * pen : pen;
+      }
+    }
+  }
+  const int s0 = A.peel_start[f], s1 = A.peel_start[f + 1];
+  for (int s = s0; s < s1; s++) {
+    const int2 S = A.steps[s];
+    const int type = S.x & 255, from0 = (S.x >> 8) & 255, from1 = (S.x >> 16) & 255, to0 = (S.x >> 24) & 255;
+    const int to1 = S.y & 255, slot = (S.y >> 8) & 255, create = (S.y >> 16) & 1, fa2mo = (S.y >> 17) & 1;
+    (void)to1;
+    if (type == 1) {   // offspring -> parents
+      const int off = from0;
+      if (create)
+        for (int x = 0; x < NS; x++)
+          for (int y = 0; y < NS; y++) MPP(slot, x, y) = 1.0;
+      const int csex = A.sex[p0 + off];
+      for (int i = 0; i < NS; i++)
+        for (int j = 0; j < NS; j++) {
+          double sum = 0;
+          for (int k = 0; k < NS; k++) {
+            const double t = (NS == 3) ? d_tba(i, j, k, chrom, csex) : A.T10dn[(i * 10 + j) * 10 + k];
+            sum += t * PP(off, k);
+          }
+          MPP(slot, i, j) *= sum;
+        }
+    } else if (type == 2) {   // spouse -> spouse
+      const int sf = from0, stt = to0;
+      for (int i = 0; i < NS; i++) {
+        double sum = 0.0;
+        if (slot == 255) for (int j = 0; j < NS; j++) sum += PP(sf, j);
+        else if (fa2mo) for (int j = 0; j < NS; j++) sum += PP(sf, j) * MPP(slot, j, i);
+        else for (int j = 0; j < NS; j++) sum += PP(sf, j) * MPP(slot, i, j);
+        PP(stt, i) *= sum;
+      }
+    } else {   // parents -> only offspring
+      const int fa = from0, mo = from1, off = to0;
+      const int csex = A.sex[p0 + off];
+      for (int k = 0; k < NS; k++) {
+        double sum = 0.0;
+        for (int i = 0; i < NS; i++)
+          for (int j = 0; j < NS; j++) {
+            double t;
+            if (NS == 3) t = d_tba(i, j, k, chrom, csex);
+            else t = (slot == 255) ? A.T10dn[(i * 10 + j) * 10 + k] : A.T10[(i * 10 + j) * 10 + k];   // quirk :1391
+            if (slot == 255) sum += PP(fa, i) * PP(mo, j) * t;
+            else sum += PP(fa, i) * MPP(slot, i, j) * PP(mo, j) * t;
+          }
+        PP(off, k) *= sum;
+      }
+    }
+  }
+  const int fin = (A.steps[s1 - 1].x >> 24) & 255;
+  double L = 0.0;
+  for (int i = 0; i < NS; i++) L += PP(fin, i);
+  return L;
+#undef PP
+#undef MPP
+}
+
+// ------------------------------------------------------------------------------------------------
 template <int T>
 __device__ __forceinline__ double block_sum(double x, double* red, int& par) {
 #pragma unroll
@@ -418,7 +552,9 @@ __device__ __forceinline__ double block_logprod(double m, int e, double* red, in
   return log10(m) + (de * PM_LOG10_2_HI + de * PM_LOG10_2_LO);
 }
 
-template <int T, int S, bool PROD, bool GEN>
+// GEN=false: lean autosomal nuclear-only kernel; GEN=true: chrX/Y/MT, de novo, founder-only units;
+// ES=true additionally peels the lane's extended families (instantiated only for pedigrees that have them).
+template <int T, int S, bool PROD, bool GEN, bool ES>
 __global__ void __launch_bounds__(T) k_brent(DevArgs A, int list) {
   __shared__ double s_lk[256];
   __shared__ double s_M[100];
@@ -460,7 +596,8 @@ __global__ void __launch_bounds__(T) k_brent(DevArgs A, int list) {
       else if (GEN && unit[s].x == U_FP) fl[s] = hoist_fp(A, I, pl, s_lk, unit[s].z, unit[s].w & 0xFF, cond[s]);
     }
     double* raw = A.raw + (size_t)site * 8;
-    const bool single = (cfg == 0) || A.single_nuclear;
+    double* wsl = ES ? A.ws + (size_t)blockIdx.x * A.ws_per_lane * T + threadIdx.x : nullptr;
+    const bool single = (cfg == 0) || (A.single_nuclear && !A.unrelated);
     // One evaluation site for the objective: the three bracketing evaluations of OptimizeFrequency
     // (:432-444) and every Brent step (core/MathGold.cpp:81-177) run through the same loop body.
     const double tol = A.precision;
@@ -474,9 +611,26 @@ __global__ void __launch_bounds__(T) k_brent(DevArgs A, int list) {
       if (PROD) {
         double m; int e;
         lane_prod<S, GEN>(x, unit, cond, fl, pmode, m, e);
+        if (ES && A.ext_count)   // extended families of this lane: Elston-Stewart peeling per evaluation
+          for (int q = 0; q < A.ext_count[threadIdx.x]; q++) {
+            const int f = A.ext_fam[q * T + threadIdx.x];
+            const double v = I.denovo ? d_es_lk<10>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, x, -1, -1, wsl, T)
+                                      : d_es_lk<3>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, x, -1, -1, wsl, T);
+            int e1, e2;
+            const double mv = frexp(v, &e1);
+            m = frexp(m * mv, &e2);
+            e += e1 + e2;
+          }
         tot = block_logprod<T>(m, e, s_red, s_rede, par);
       } else {
-        tot = block_sum<T>(lane_loglik<S, GEN>(x, unit, cond, fl, pmode), s_red, par);
+        double part = lane_loglik<S, GEN>(x, unit, cond, fl, pmode);
+        if (ES && A.ext_count)
+          for (int q = 0; q < A.ext_count[threadIdx.x]; q++) {
+            const int f = A.ext_fam[q * T + threadIdx.x];
+            part += log10(I.denovo ? d_es_lk<10>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, x, -1, -1, wsl, T)
+                                   : d_es_lk<3>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, x, -1, -1, wsl, T));
+          }
+        tot = block_sum<T>(part, s_red, par);
       }
       nev++;
       if (single) { mn = 0.0; fmin = -tot; ok = true; break; }
@@ -600,7 +754,10 @@ __global__ void __launch_bounds__(256) k_prep(DevArgs A) {
         else { O.status = PM_SITE_CALLED; valid = true; }
       }
       A.res[site] = O;
-      if (valid) {
+      if (valid && A.unrelated) {   // --quick_call pre-filter first (main.cpp:354-437)
+        const int slot = atomicAdd(&A.counts[1], 3);
+        for (int k = 0; k < 3; k++) A.items[1][slot + k] = (site << 3) | (k + 1);
+      } else if (valid) {
         const int nit = A.denovo ? 4 : 3;
         const int slot = atomicAdd(&A.counts[0], nit);
         for (int k = 0; k < nit; k++) A.items[0][slot + k] = (site << 3) | (A.denovo ? k : k + 1);
@@ -655,6 +812,47 @@ __global__ void k_select(DevArgs A) {
     for (int k = 0; k < 3; k++) A.items[1][slot + k] = (site << 3) | (4 + k);
     R->n_cfg = 7;
   } else R->n_cfg = 4;
+}
+
+// --quick_call (main.cpp:354-437): the unrelated model's varllk -- MonomorphismLogLikelihood (plain, even
+// under --denovo) and the all-founder Brent results of the quick pass.
+__device__ __forceinline__ void fill_varllk_quick(const DevArgs& A, int site, int n, double* v) {
+  const double* raw = A.raw + (size_t)site * 8;
+  v[0] = A.lp_mono + A.mono_plain[site];
+  v[1] = A.lp_ts + raw[1];
+  v[2] = A.lp_tv + raw[2];
+  v[3] = A.lp_tv + raw[3];
+  for (int k = 4; k < n; k++) v[k] = A.lp_other + raw[k];
+}
+
+__global__ void k_quick_select(DevArgs A) {   // CalcVarPosterior(4) of the quick pass -> 3 more quick items
+  const int site = blockIdx.x * blockDim.x + threadIdx.x;
+  if (site >= A.n || A.res[site].status != PM_SITE_CALLED) return;
+  double v[7], vpp, q; int a1, a2;
+  fill_varllk_quick(A, site, 4, v);
+  d_var_posterior(v, 4, A.ref[site], &vpp, &q, &a1, &a2);
+  A.res[site].n_cfg = 4;
+  if (vpp < 0.99) {
+    const int slot = atomicAdd(&A.counts[2], 3);
+    for (int k = 0; k < 3; k++) A.items[2][slot + k] = (site << 3) | (4 + k);
+    A.res[site].n_cfg = 7;
+  }
+}
+
+__global__ void k_quick_final(DevArgs A) {   // quick decision; survivors enter the pedigree model
+  const int site = blockIdx.x * blockDim.x + threadIdx.x;
+  if (site >= A.n) return;
+  pm_site_result* R = A.res + site;
+  if (R->status != PM_SITE_CALLED) return;
+  double v[7], vpp, q; int a1, a2;
+  const int n = R->n_cfg;
+  fill_varllk_quick(A, site, n, v);
+  const int maxidx = d_var_posterior(v, n, A.ref[site], &vpp, &q, &a1, &a2);
+  R->n_cfg = 0;
+  if (vpp < A.posterior || maxidx == 0) { R->status = PM_SITE_QUICK_SKIP; return; }
+  const int nit = A.denovo ? 4 : 3;
+  const int slot = atomicAdd(&A.counts[0], nit);
+  for (int k = 0; k < nit; k++) A.items[0][slot + k] = (site << 3) | (A.denovo ? k : k + 1);
 }
 
 // main.cpp:539-574 per site; counters aggregated per block
@@ -833,7 +1031,7 @@ __device__ void d_kid_geno(int chrom, const uint8_t* pl, const double* lk, int p
   out[0] = G11; out[1] = G12; out[2] = G22;
 }
 
-template <bool DN>
+template <bool DN, bool ES>
 __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
   __shared__ double s_lk[256];
   __shared__ double s_M[100];
@@ -841,7 +1039,8 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
   for (int i = threadIdx.x; i < 100; i += blockDim.x) s_M[i] = A.M[i];
   __syncthreads();
   const long long work = (long long)A.counts[3] * A.n_fam;
-  for (long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x; gid < work; gid += (long long)gridDim.x * blockDim.x) {
+  const size_t gid_base = (size_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (size_t)gridDim.x * blockDim.x;
+  for (long long gid = (long long)gid_base; gid < work; gid += (long long)stride) {
     const int row = (int)(gid / A.n_fam);
     const int f = (int)(gid % A.n_fam);
     const int site = A.row_site[row];
@@ -884,7 +1083,38 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
         }
         continue;
       }
-      if (kind != PM_FAM_NUCLEAR) continue;   // extended pedigrees: k_posterior_ext
+      if (ES && kind == PM_FAM_EXTENDED) {   // CalcPostProb_SingleExtendedPed_BA :171-216 / _denovo :140-169
+        double* wsl = A.ws + gid_base;
+        const size_t st = stride;
+        for (int j = 0; j < n; j++) {
+          const int p = p0 + j, sx = A.sex[p];
+          if (!dn) {
+            if (chrom == PM_CHR_Y && sx == FEMALE) {
+              const double z[3] = {0, 0, 0};
+              d_emit_call(out + p, z, 0, PM_LBL_DOT, 0.0);
+              continue;
+            }
+            const double l11 = d_es_lk<3>(A, f, pl, s_lk, g11, g12, g22, chrom, freq, j, g11, wsl, st);
+            const double l12 = d_es_lk<3>(A, f, pl, s_lk, g11, g12, g22, chrom, freq, j, g12, wsl, st);
+            const double l22 = d_es_lk<3>(A, f, pl, s_lk, g11, g12, g22, chrom, freq, j, g22, wsl, st);
+            const double sum = l11 + l12 + l22;
+            double post[3] = {0, 0, 0};
+            if (sum != 0) { post[0] = l11 / sum; post[1] = l12 / sum; post[2] = l22 / sum; }
+            d_emit_call(out + p, post, d_best3(l11, l12, l22), d_vcf_label(chrom, sx), post[1] + post[2] * 2);
+          } else {
+            double lkv[10], sum = 0.0;
+            for (int k = 0; k < 10; k++) lkv[k] = d_es_lk<10>(A, f, pl, s_lk, g11, g12, g22, chrom, freq, j, k, wsl, st);
+            for (int k = 0; k < 10; k++) sum += lkv[k];
+            double post[10];
+            for (int k = 0; k < 10; k++) post[k] = (sum == 0) ? 0 : lkv[k] / sum;
+            int b = 0; double mx = 0.0;
+            for (int k = 0; k < 10; k++) if (mx < lkv[k]) { mx = lkv[k]; b = k; }
+            d_emit_call(out + p, post, b, PM_LBL_GENO10, 0.0);
+          }
+        }
+        continue;
+      }
+      if (kind != PM_FAM_NUCLEAR) continue;
       // CalcParentMarginal(_denovo) at freq
       ItemCtx I;
       I.a1 = a1; I.a2 = a2; I.g11 = g11; I.g12 = g12; I.g22 = g22; I.denovo = dn; I.sex = msex; I.chrom = chrom;
@@ -1110,6 +1340,15 @@ struct pm_engine {
   double *d_raw = nullptr, *d_minv = nullptr, *d_mono = nullptr;
   int* d_evals = nullptr;
   int8_t* d_item_sex = nullptr;
+  // extended families (Elston-Stewart)
+  int n_ext = 0, max_ext = 0, ws_per_lane = 0, grid_post = 0;
+  int *d_fam_founders = nullptr, *d_peel_start = nullptr, *d_ext_count = nullptr, *d_ext_fam = nullptr;
+  int8_t* d_is_founder = nullptr;
+  int2* d_steps = nullptr;
+  double *d_T10 = nullptr, *d_T10dn = nullptr, *d_ws = nullptr;
+  // --quick_call: the MakeUnrelated() plan (every family an all-founder product) with its own geometry
+  int Tq = 0, Sq = 0, grid_q = 0;
+  int4* d_units_q = nullptr;
   int* d_items[N_LISTS] = {nullptr, nullptr, nullptr};
   int* d_counts = nullptr;
   unsigned long long* d_eval_total = nullptr;
@@ -1158,13 +1397,16 @@ static const struct { int T, S; } kVariants[] = {{64, 1}, {64, 2}, {64, 4}, {128
 
 // Deal families to lanes: family-major round robin; founders-only families are split into <=3-person chunks
 // kept on one lane.  Returns false if the plan does not fit T x S.
-static bool plan_units(const pm_pedigree* ped, int T, int S, std::vector<int4>& units) {
+// Extended families are not units: they go to per-lane lists (plan_ext).  unrelated = the --quick_call
+// MakeUnrelated() view (FamilyLikelihoodSeq.cpp:54-59): every family is an all-founder product.
+static bool plan_units(const pm_pedigree* ped, int T, int S, std::vector<int4>& units, bool unrelated = false) {
   units.assign((size_t)T * S, make_int4(U_NONE, -1, 0, 0));
   std::vector<int> used(T, 0);
   int lane = 0;
   for (int f = 0; f < ped->n_fam; f++) {
-    const int p0 = ped->fam_start[f], n = ped->fam_start[f + 1] - p0, kind = ped->fam_kind[f];
+    const int p0 = ped->fam_start[f], n = ped->fam_start[f + 1] - p0, kind = unrelated ? PM_FAM_FOUNDERS : ped->fam_kind[f];
     std::vector<int4> us;
+    if (kind == PM_FAM_EXTENDED) continue;
     if (kind == PM_FAM_NUCLEAR) us.push_back(make_int4(U_NUC, f, p0, n));
     else if (kind == PM_FAM_FOUNDERS) {
       for (int j = 0; j < n; j += 3) {
@@ -1173,7 +1415,7 @@ static bool plan_units(const pm_pedigree* ped, int T, int S, std::vector<int4>& 
         if (j + 3 >= n) fl |= UF_LAST;
         us.push_back(make_int4(U_FP, f, p0 + j, fl));
       }
-    } else return false;   // extended pedigrees are not planned here
+    }
     // choose the lane: next in round-robin order with enough room
     int tries = 0;
     while (used[lane] + (int)us.size() > S && tries < T) { lane = (lane + 1) % T; tries++; }
@@ -1184,12 +1426,84 @@ static bool plan_units(const pm_pedigree* ped, int T, int S, std::vector<int4>& 
   return true;
 }
 
+// Packs one extended family's ES_Peeling schedule for d_es_lk: marriage-partial slots are resolved the
+// way the reference's partial map behaves (created by the first type-1 step of a couple, looked up by
+// later type-2/3 steps, absent before that).  Returns the workspace doubles the family needs, -1 if it
+// cannot be packed (family larger than 255 members).
+static int pack_steps(const pm_pedigree* ped, int f, int ns, std::vector<int2>& out) {
+  const int p0 = ped->fam_start[f], n = ped->fam_start[f + 1] - p0;
+  if (n > 255 || !ped->peel_start || !ped->steps) return -1;
+  std::vector<std::pair<int, int>> keys;
+  auto find = [&](int a, int b) {
+    for (size_t i = 0; i < keys.size(); i++) if (keys[i].first == a && keys[i].second == b) return (int)i;
+    return -1;
+  };
+  for (int k = ped->peel_start[f]; k < ped->peel_start[f + 1]; k++) {
+    const pm_peel_step& S = ped->steps[k];
+    int slot = 255, create = 0, fa2mo = 0;
+    if (S.type == 1) {
+      int i = find(S.to0, S.to1);
+      if (i < 0) { i = (int)keys.size(); keys.push_back({S.to0, S.to1}); create = 1; }
+      slot = i;
+    } else if (S.type == 2) {
+      int a, b;
+      if (ped->sex[p0 + S.from0] == FEMALE) { a = S.to0; b = S.from0; fa2mo = 0; } else { a = S.from0; b = S.to0; fa2mo = 1; }
+      const int i = find(a, b);
+      slot = i < 0 ? 255 : i;
+    } else if (S.type == 3) {
+      const int i = find(S.from0, S.from1);
+      slot = i < 0 ? 255 : i;
+    } else return -1;
+    if (keys.size() > 254) return -1;
+    int2 e;
+    e.x = (S.type & 255) | ((S.from0 & 255) << 8) | ((S.from1 & 255) << 16) | ((S.to0 & 255) << 24);
+    e.y = (S.to1 & 255) | (slot << 8) | (create << 16) | (fa2mo << 17);
+    out.push_back(e);
+  }
+  if (ped->peel_start[f + 1] == ped->peel_start[f]) return -1;
+  return n * ns + (int)keys.size() * ns * ns;
+}
+
+static int gi_h(int b1, int b2) { return b1 < b2 ? (b1 - 1) * (10 - b1) / 2 + (b2 - b1) : (b2 - 1) * (10 - b2) / 2 + (b1 - b2); }
+
+// FamilyLikelihoodES::SetTransmissionMatrix (:752-785) and SetTransmissionMatrix_denovo (:787-810)
+static void transmission_tables(const double* M, std::vector<double>& T10, std::vector<double>& T10dn) {
+  T10.assign(1000, 0.0);
+  T10dn.assign(1000, 0.0);
+  for (int i = 1; i <= 4; i++)
+    for (int j = i; j <= 4; j++) {
+      const int x = gi_h(i, j);
+      for (int k = 1; k <= 4; k++)
+        for (int m = k; m <= 4; m++) {
+          const int y = gi_h(k, m), g[4] = {gi_h(i, k), gi_h(i, m), gi_h(j, k), gi_h(j, m)};
+          for (int t = 0; t < 4; t++) T10[(x * 10 + y) * 10 + g[t]] += 0.25;
+        }
+    }
+  for (int i = 0; i < 10; i++)
+    for (int j = 0; j < 10; j++)
+      for (int k = 0; k < 10; k++) {
+        double s = .0;
+        for (int m = 0; m < 10; m++) s += T10[(i * 10 + j) * 10 + m] * M[m * 10 + k];
+        T10dn[(i * 10 + j) * 10 + k] = s;
+      }
+}
+
+// SetTransmissionMatrix_BA, _CHRX_2Female, _CHRX_2Male, _CHRY, _MITO (:812-924), [parent1][parent2][child]
+static const double kTBA[5][27] = {
+    {1, 0, 0, .5, .5, 0, 0, 1, 0, .5, .5, 0, .25, .5, .25, 0, .5, .5, 0, 1, 0, 0, .5, .5, 0, 0, 1},
+    {1, 0, 0, .5, .5, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, .5, .5, 0, 0, 1},
+    {1, 0, 0, .5, 0, .5, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, .5, 0, .5, 0, 0, 1},
+    {1, 0, 0, 1, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 1, 0, 0, 1},
+    {1, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 1}};
+
 extern "C" {
 
 void pm_engine_destroy(pm_engine* E) {
   if (!E) return;
   hipSetDevice(E->device);
-  void* bufs[] = {E->d_fam_start, E->d_fam_kind, E->d_fa, E->d_mo, E->d_sex, E->d_units, E->d_lktab, E->d_M, E->d_syn,
+  void* bufs[] = {E->d_fam_founders, E->d_peel_start, E->d_ext_count, E->d_ext_fam, E->d_is_founder, E->d_steps, E->d_T10,
+                  E->d_T10dn, E->d_ws, E->d_units_q,
+                  E->d_fam_start, E->d_fam_kind, E->d_fa, E->d_mo, E->d_sex, E->d_units, E->d_lktab, E->d_M, E->d_syn,
                   E->d_pl, E->d_ref, E->d_dm, E->d_res, E->d_calls, E->d_raw, E->d_minv, E->d_mono, E->d_evals,
                   E->d_item_sex, E->d_items[0], E->d_items[1], E->d_items[2], E->d_counts, E->d_eval_total, E->d_row_site,
                   E->d_counters};
@@ -1213,16 +1527,6 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
     return PM_EHIP;
   }
   if (device < 0 || device >= ndev) { pm_set_last_error("pm_engine_create: device index out of range"); return PM_EINVAL; }
-  for (int f = 0; f < ped->n_fam; f++) {
-    if (ped->fam_kind[f] == PM_FAM_EXTENDED) {
-      pm_set_last_error("pm_engine_create: extended pedigrees (Elston-Stewart peeling) are not supported by this engine build yet");
-      return PM_EPED;
-    }
-    if (ped->fam_start[f + 1] - ped->fam_start[f] > 32 && ped->fam_kind[f] == PM_FAM_NUCLEAR) {
-      // fine: nuclear families of any size are supported
-    }
-  }
-  if (par->quick_call) { pm_set_last_error("pm_engine_create: --quick_call is not supported by this engine build yet"); return PM_EINVAL; }
   pm_engine* E = new pm_engine;
   E->device = device;
   E->par = *par;
@@ -1231,7 +1535,10 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
   E->max_batch = max_batch;
   E->n_founders = ped->n_founders; E->male_founders = ped->male_founders; E->female_founders = ped->female_founders;
   E->single_nuclear = (ped->n_fam == 1 && ped->fam_kind[0] == PM_FAM_NUCLEAR) ? 1 : 0;
-  for (int f = 0; f < ped->n_fam; f++) if (ped->fam_kind[f] != PM_FAM_NUCLEAR) E->has_fp = true;
+  for (int f = 0; f < ped->n_fam; f++) {
+    if (ped->fam_kind[f] != PM_FAM_NUCLEAR) E->has_fp = true;
+    if (ped->fam_kind[f] == PM_FAM_EXTENDED) E->n_ext++;
+  }
   E->fam_start_h.assign(ped->fam_start, ped->fam_start + ped->n_fam + 1);
   E->sex_h.assign(ped->sex, ped->sex + ped->n_person);
   HIP_TRY(hipSetDevice(device));
@@ -1258,8 +1565,11 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
     static const int2 lean[] = {{64, 1}, {64, 2}, {64, 4}, {64, 8}, {64, 16}, {512, 4}, {1024, 4}, {1024, 8}};
     static const int2 generic[] = {{64, 1}, {64, 2}, {64, 4}, {64, 8}, {256, 4}, {512, 4}, {1024, 4}, {1024, 8}};
     const int2* pref = gen ? generic : lean;
+    // extended families are the expensive terms: spread them one per lane up to 256 lanes
+    int tmin = 1;
+    while (tmin < std::min(E->n_ext, 256)) tmin *= 2;
     for (int i = 0; i < 8 && !planned; i++)
-      if (plan_units(ped, pref[i].x, pref[i].y, units)) { E->T = pref[i].x; E->S = pref[i].y; planned = true; }
+      if (pref[i].x >= tmin && plan_units(ped, pref[i].x, pref[i].y, units)) { E->T = pref[i].x; E->S = pref[i].y; planned = true; }
   }
   if (!planned) { pm_engine_destroy(E); pm_set_last_error("pm_engine_create: pedigree too large for the lane plan"); return PM_EPED; }
   hipDeviceProp_t prop;
@@ -1298,6 +1608,72 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
   HIP_TRY(hipMemcpy(E->d_lktab, lk, sizeof(lk), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(E->d_M, E->M_h, sizeof(E->M_h), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(E->d_syn, &syn, sizeof(syn), hipMemcpyHostToDevice));
+  // --- Elston-Stewart data: packed schedules, per-lane family lists, transmission tables, workspace
+  {
+    const int ns = par->denovo ? 10 : 3;
+    std::vector<int> peel_start(ped->n_fam + 1, 0);
+    std::vector<int2> steps;
+    std::vector<int> founders(ped->fam_founders, ped->fam_founders + ped->n_fam);
+    int wsmax = 0;
+    for (int f = 0; f < ped->n_fam; f++) {
+      peel_start[f] = (int)steps.size();
+      if (ped->fam_kind[f] != PM_FAM_EXTENDED) continue;
+      const int w = pack_steps(ped, f, ns, steps);
+      if (w < 0) {
+        pm_engine_destroy(E);
+        pm_set_last_error("pm_engine_create: extended family without a usable peeling schedule (or > 255 members)");
+        return PM_EPED;
+      }
+      wsmax = std::max(wsmax, w);
+    }
+    peel_start[ped->n_fam] = (int)steps.size();
+    E->ws_per_lane = wsmax;
+    const int T = E->T;
+    E->max_ext = (E->n_ext + T - 1) / T;
+    std::vector<int> ext_count(T, 0), ext_fam((size_t)std::max(1, E->max_ext) * T, -1);
+    int q = 0;
+    for (int f = 0; f < ped->n_fam; f++)
+      if (ped->fam_kind[f] == PM_FAM_EXTENDED) { const int lane = q % T; ext_fam[(size_t)ext_count[lane]++ * T + lane] = f; q++; }
+    std::vector<double> T10, T10dn;
+    transmission_tables(E->M_h, T10, T10dn);
+    DALLOC(E->d_fam_founders, ped->n_fam);
+    DALLOC(E->d_is_founder, ped->n_person);
+    DALLOC(E->d_peel_start, ped->n_fam + 1);
+    DALLOC(E->d_steps, std::max<size_t>(1, steps.size()));
+    DALLOC(E->d_ext_count, T);
+    DALLOC(E->d_ext_fam, ext_fam.size());
+    DALLOC(E->d_T10, 1000);
+    DALLOC(E->d_T10dn, 1000);
+    HIP_TRY(hipMemcpy(E->d_fam_founders, founders.data(), sizeof(int) * ped->n_fam, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(E->d_is_founder, ped->is_founder, ped->n_person, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(E->d_peel_start, peel_start.data(), sizeof(int) * peel_start.size(), hipMemcpyHostToDevice));
+    if (!steps.empty()) HIP_TRY(hipMemcpy(E->d_steps, steps.data(), sizeof(int2) * steps.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(E->d_ext_count, ext_count.data(), sizeof(int) * T, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(E->d_ext_fam, ext_fam.data(), sizeof(int) * ext_fam.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(E->d_T10, T10.data(), sizeof(double) * 1000, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(E->d_T10dn, T10dn.data(), sizeof(double) * 1000, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_TBA), kTBA, sizeof(kTBA)));
+    // workspace: the Brent grid and the posterior grid are capped so each needs <= 1 GiB
+    E->grid_post = E->n_cu * 8;
+    if (wsmax > 0) {
+      const size_t cap = (size_t)1 << 30, per_lane = (size_t)wsmax * sizeof(double);
+      E->grid_brent = (int)std::max<size_t>(E->n_cu, std::min<size_t>(E->grid_brent, cap / (per_lane * T)));
+      E->grid_post = (int)std::max<size_t>(E->n_cu, std::min<size_t>(E->grid_post, cap / (per_lane * 256)));
+      const size_t lanes = std::max((size_t)E->grid_brent * T, (size_t)E->grid_post * 256);
+      DALLOC(E->d_ws, lanes * wsmax);
+    }
+  }
+  // --- --quick_call: the unrelated plan (all persons in <=3-person founder chunks)
+  if (par->quick_call) {
+    static const int2 gq[] = {{64, 1}, {64, 2}, {64, 4}, {64, 8}, {256, 4}, {512, 4}, {1024, 4}, {1024, 8}};
+    std::vector<int4> uq;
+    for (auto g : gq)
+      if (plan_units(ped, g.x, g.y, uq, true)) { E->Tq = g.x; E->Sq = g.y; break; }
+    if (!E->Tq) { pm_engine_destroy(E); pm_set_last_error("pm_engine_create: pedigree too large for the --quick_call lane plan"); return PM_EPED; }
+    E->grid_q = E->n_cu * std::max(1, 1024 / E->Tq);
+    DALLOC(E->d_units_q, uq.size());
+    HIP_TRY(hipMemcpy(E->d_units_q, uq.data(), sizeof(int4) * uq.size(), hipMemcpyHostToDevice));
+  }
   // batch buffers
   const size_t nb = (size_t)max_batch, np = (size_t)ped->n_person;
   DALLOC(E->d_pl, nb * np * 10);
@@ -1349,6 +1725,10 @@ static DevArgs make_args(pm_engine* E, int n, const uint8_t* pl, const uint32_t*
   A.chrom = E->chrom; A.denovo = E->par.denovo;
   A.fam_start = E->d_fam_start; A.fam_kind = E->d_fam_kind; A.sex = E->d_sex; A.fa_local = E->d_fa; A.mo_local = E->d_mo;
   A.units = E->d_units; A.T = E->T; A.S = E->S;
+  A.fam_founders = E->d_fam_founders; A.is_founder = E->d_is_founder; A.peel_start = E->d_peel_start; A.steps = E->d_steps;
+  A.ext_count = E->n_ext ? E->d_ext_count : nullptr; A.ext_fam = E->d_ext_fam;
+  A.T10 = E->d_T10; A.T10dn = E->d_T10dn; A.ws = E->d_ws; A.ws_per_lane = E->ws_per_lane;
+  A.unrelated = E->par.quick_call ? 1 : 0;   // k_prep: route sites through the quick pre-filter first
   A.lktab = E->d_lktab; A.M = E->d_M; A.syn = E->d_syn;
   A.precision = E->par.precision; A.posterior = E->par.posterior; A.theta = E->par.theta;
   A.min_total_depth = E->par.min_total_depth; A.max_total_depth = E->par.max_total_depth; A.min_map_quality = E->par.min_map_quality;
@@ -1370,27 +1750,41 @@ static DevArgs make_args(pm_engine* E, int n, const uint8_t* pl, const uint32_t*
 }
 
 typedef void (*BrentFn)(DevArgs, int);
-static BrentFn brent_kernel(int T, int S, bool prod, bool gen) {
-#define PMK(t, s)                                                                     \
-  if (T == t && S == s) {                                                             \
-    if (gen) return prod ? k_brent<t, s, true, true> : k_brent<t, s, false, true>;    \
-    return prod ? k_brent<t, s, true, false> : k_brent<t, s, false, false>;           \
+static BrentFn brent_kernel(int T, int S, bool prod, bool gen, bool es) {
+#define PMK(t, s)                                                                              \
+  if (T == t && S == s) {                                                                      \
+    if (gen) return prod ? k_brent<t, s, true, true, false> : k_brent<t, s, false, true, false>; \
+    return prod ? k_brent<t, s, true, false, false> : k_brent<t, s, false, false, false>;        \
+  }
+#define PMKE(t, s) \
+  if (T == t && S == s) return prod ? k_brent<t, s, true, true, true> : k_brent<t, s, false, true, true>;
+  if (es) {
+    PMKE(64, 1) PMKE(64, 2) PMKE(64, 4) PMKE(64, 8) PMKE(256, 4) PMKE(512, 4) PMKE(1024, 4) PMKE(1024, 8)
+    return nullptr;
   }
   PMK(64, 1) PMK(64, 2) PMK(64, 4) PMK(128, 4) PMK(256, 4) PMK(512, 2) PMK(512, 4) PMK(1024, 1) PMK(1024, 2)
   PMK(1024, 4) PMK(1024, 8) PMK(128, 8) PMK(64, 8) PMK(64, 16)
 #undef PMK
+#undef PMKE
   return nullptr;
 }
 
-static int launch_brent(pm_engine* E, const DevArgs& A, int list) {
+static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelated = false) {
+  DevArgs A = A0;
+  int T = E->T, S = E->S, grid = E->grid_brent;
   // lean kernel: autosome, no de novo model, nuclear families only (the common case)
-  const bool gen = E->chrom != PM_CHR_AUTO || E->par.denovo || E->has_fp;
-  BrentFn fn = brent_kernel(E->T, E->S, !E->par.exact_log10, gen);
+  bool gen = E->chrom != PM_CHR_AUTO || E->par.denovo || E->has_fp;
+  if (unrelated) {   // MakeUnrelated(): all-founder products over the quick plan, no ES, no de novo model
+    A.units = E->d_units_q; A.T = T = E->Tq; A.S = S = E->Sq; grid = E->grid_q;
+    A.ext_count = nullptr; A.unrelated = 1; A.denovo = 0; gen = true;
+  } else A.unrelated = 0;
+  BrentFn fn = brent_kernel(T, S, !E->par.exact_log10, gen, !unrelated && E->n_ext > 0);
+  if (!fn) { pm_set_last_error("launch_brent: no kernel variant for the lane plan"); return PM_EINVAL; }
   hipEvent_t a, b;
   HIP_TRY(hipEventCreate(&a));
   HIP_TRY(hipEventCreate(&b));
   HIP_TRY(hipEventRecord(a, E->stream));
-  hipLaunchKernelGGL(fn, dim3(E->grid_brent), dim3(E->T), 0, E->stream, A, list);
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(T), 0, E->stream, A, list);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(b, E->stream));
   E->brent_events.push_back({a, b});
@@ -1409,8 +1803,17 @@ static int run_pipeline(pm_engine* E, int n, const uint8_t* pl, const uint32_t* 
   hipLaunchKernelGGL(k_prep, dim3((n + 3) / 4), dim3(256), 0, E->stream, A);
   HIP_TRY(hipGetLastError());
   int rc;
-  if ((rc = launch_brent(E, A, 0))) return rc;
   const int tb = 256, gb = (n + tb - 1) / tb;
+  if (E->par.quick_call) {   // main.cpp:354-437 on lists 1 and 2, survivors -> list 0
+    if ((rc = launch_brent(E, A, 1, true))) return rc;
+    hipLaunchKernelGGL(k_quick_select, dim3(gb), dim3(tb), 0, E->stream, A);
+    HIP_TRY(hipGetLastError());
+    if ((rc = launch_brent(E, A, 2, true))) return rc;
+    hipLaunchKernelGGL(k_quick_final, dim3(gb), dim3(tb), 0, E->stream, A);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemsetAsync(E->d_counts + 1, 0, 2 * sizeof(int), E->stream));
+  }
+  if ((rc = launch_brent(E, A, 0))) return rc;
   hipLaunchKernelGGL(k_select, dim3(gb), dim3(tb), 0, E->stream, A);
   HIP_TRY(hipGetLastError());
   if ((rc = launch_brent(E, A, 1))) return rc;
@@ -1424,8 +1827,11 @@ static int run_pipeline(pm_engine* E, int n, const uint8_t* pl, const uint32_t* 
   }
   hipLaunchKernelGGL(k_rows, dim3(1), dim3(1024), 0, E->stream, A);
   HIP_TRY(hipGetLastError());
-  if (E->par.denovo) hipLaunchKernelGGL(k_posterior<true>, dim3(E->n_cu * 8), dim3(256), 0, E->stream, A);
-  else hipLaunchKernelGGL(k_posterior<false>, dim3(E->n_cu * 8), dim3(256), 0, E->stream, A);
+  {
+    void (*post)(DevArgs) = E->par.denovo ? (E->n_ext ? k_posterior<true, true> : k_posterior<true, false>)
+                                          : (E->n_ext ? k_posterior<false, true> : k_posterior<false, false>);
+    hipLaunchKernelGGL(post, dim3(E->grid_post), dim3(256), 0, E->stream, A);
+  }
   HIP_TRY(hipGetLastError());
   if (!E->par.denovo && E->chrom == PM_CHR_AUTO) {
     hipLaunchKernelGGL(k_ab, dim3(E->n_cu * 8), dim3(256), 0, E->stream, A);
