@@ -1,20 +1,27 @@
 #!/usr/bin/env python3
 """bench.py -- headline benchmark of the MI355X polyMutt engine.
 
-Metric (BASELINE.json): sites/s for the whole node, 1000 nuclear quad families, synthetic GLF sites
-(SURVEY.md 8(d) recipe, generated on the device), plus achieved HBM GB/s and the FP64 roofline of the
-dominant kernel (k_brent).  A "step" = one pass of the full per-site path (read stats, filters,
-monomorphism, 3(+3) Brent-optimised allele configurations, model selection, genotype posteriors)
-over one batch of sites already resident in HBM.
+Metric (BASELINE.json): sites/s for the whole node, 1000 nuclear quad families, synthetic GLF-shaped sites
+(SURVEY.md 8(d) recipe, generated on the device), plus achieved HBM GB/s.  A "step" = one pass of the
+full per-site path (read stats, filters, monomorphism, 3(+3) Brent-optimised allele configurations, model
+selection, de novo LR with --denovo, genotype posteriors, allele balance) over one batch of sites already
+resident in HBM.
+
+Roofline: the dominant kernel is k_brent (the Brent allele-frequency maximisation).  `roofline` reports it
+against HBM as the contract and BASELINE.json ask (algorithmic bytes = each launch reads the PL block of
+every site it touches once); the kernel is in fact FP64-VALU bound, so `roofline_fp64` reports the
+SURVEY 8(d) algorithmic op count against the measured FP64 issue rate (tools/fp64_peak.hip).  `traffic`
+is the PMC-measured HBM bytes per k_brent dispatch from the committed rocprofv3 passes under profiles/.
 
 Multi-GPU: one process per GPU (torchrun); sites are sharded (weak scaling, no data-path collective);
-the section summary counters are combined with one RCCL all-reduce, as the north star prescribes.
+the section summary counters are combined with one RCCL all-reduce (polymutt_amd/shard.py).
 
-cpu_baseline: the reference itself (oracle/_ref/pm_ref, built from /root/reference sources; it travels
-to the GPU box as a prebuilt binary) on a bounded sample of the same synthetic workload written as GLF
-files, timed on the host cores -- rank 0, N=1 only.
+cpu_baseline: the reference itself (oracle/_ref/pm_ref, built from /root/reference sources by
+oracle/ref/Makefile; it travels to the GPU box as a built binary) on a bounded GLF sample of the same
+workload, timed on the host cores -- rank 0, N=1 only.
 """
 import argparse
+import glob
 import json
 import os
 import shutil
@@ -28,28 +35,32 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-FP64_PEAK_TFLOPS = 78.6       # MI355X FP64 vector (FMA counted as 2), datasheet
-FP64_NONFMA_TFLOPS = 39.3     # issue rate of non-fused FP64 mul/add (the engine issues no FMA: parity)
-HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md (spec)
+FP64_PEAK_TFLOPS = 78.6       # MI355X FP64 vector, FMA counted as 2 (spec)
+FP64_NONFMA_TOPS = 39.3       # mul/add issue rate = half the FMA-counted peak (profiles/*_fp64_peak.json measures it)
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--families", type=int, default=1000)
-    ap.add_argument("--kids", type=int, default=2)
+    ap.add_argument("--shape", choices=["quad", "trio"], default="quad")
+    ap.add_argument("--denovo", action="store_true", help="BASELINE config 3: --denovo MutationModel")
     ap.add_argument("--batch", type=int, default=65536, help="sites per step per GPU")
     ap.add_argument("--pool", type=int, default=2, help="distinct resident batches cycled by the steps")
     ap.add_argument("--seed", type=int, default=7)
-    ap.add_argument("--cpu-sites", type=int, default=2000)
+    ap.add_argument("--cpu-sites", type=int, default=500)
     ap.add_argument("--cpu-threads", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-inputs", action="store_true",
+                    help="PCIe-inclusive variant: blocks start in host memory and results return to the host "
+                         "(pm_engine_run); never the headline value")
     return ap.parse_args()
 
 
-def quad_pedigree(pm, nfam, kids):
+def nuclear_pedigree(pm, nfam, kids):
     size = 2 + kids
     n = nfam * size
     sex = np.zeros(n, np.int8)
@@ -67,6 +78,9 @@ def quad_pedigree(pm, nfam, kids):
     return pm.pedigree_from_arrays(np.full(nfam, size), np.full(nfam, 2), kind, sex, isf, fa, mo)
 
 
+quad_pedigree = nuclear_pedigree   # used by __graft_entry__.smoke()
+
+
 def cpu_baseline(args):
     """Reference binary (or the CPU port) on a bounded GLF sample of the same workload."""
     import polymutt_amd as pm
@@ -80,21 +94,42 @@ def cpu_baseline(args):
         return None
     tmp = tempfile.mkdtemp(prefix="pm_cpu_", dir=os.environ.get("TMPDIR", "/tmp"))
     try:
-        shape = "quad" if args.kids == 2 else "trio"
-        pm.synth_write_dataset(tmp, shape, args.families, args.cpu_sites, args.seed)
+        pm.synth_write_dataset(tmp, args.shape, args.families, args.cpu_sites, args.seed)
         cmd = [exe, "-p", "test.ped", "-d", "test.dat", "-g", "test.gif", "--out_vcf", "out.vcf",
-               "--nthreads", str(args.cpu_threads)]
+               "--nthreads", str(args.cpu_threads)] + (["--denovo"] if args.denovo else [])
         t0 = time.perf_counter()
-        r = subprocess.run(cmd, cwd=tmp, capture_output=True, text=True, timeout=600)
+        r = subprocess.run(cmd, cwd=tmp, capture_output=True, text=True, timeout=900)
         dt = time.perf_counter() - t0
         if r.returncode != 0:
             return {"error": r.stdout[-500:]}
         return {"value": args.cpu_sites / dt, "unit": "sites/s", "cores": args.cpu_threads, "kind": kind,
-                "sample": f"{args.families} synthetic {shape} families x {args.cpu_sites} sites written as GLF (seed "
-                          f"{args.seed}), end-to-end wall time incl. GLF ingest, --nthreads {args.cpu_threads}",
+                "sample": f"{args.families} synthetic {args.shape} families x {args.cpu_sites} sites (seed {args.seed}) "
+                          f"written as GLF, end-to-end wall time incl. GLF ingest, --nthreads {args.cpu_threads}"
+                          + (", --denovo" if args.denovo else ""),
                 "seconds": dt}
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
+
+
+def pmc_traffic():
+    """HBM bytes per k_brent dispatch from the newest committed PMC summary (profiles/rNN_pmc.json)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    for k, v in d.items():
+        if k.startswith("k_brent") and "hbm_read_bytes_per_dispatch" in v:
+            return v["hbm_read_bytes_per_dispatch"] + v.get("hbm_write_bytes_per_dispatch", 0.0), os.path.basename(files[-1])
+    return None, os.path.basename(files[-1])
+
+
+def measured_fp64_peak():
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_fp64_peak.json")))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    rates = [d[k] for k in ("v_mul_f64_Tops", "v_add_f64_Tops") if k in d]
+    return max(rates) if rates else None   # the faster of mul/add: the conservative (larger) peak
 
 
 def main():
@@ -102,31 +137,47 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
+    dev = None
     if world > 1:
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
+        dev = torch.device("cuda", local)
     import polymutt_amd as pm
+    from polymutt_amd.shard import allreduce_counters, max_over_ranks
 
-    ped = quad_pedigree(pm, args.families, args.kids)
+    kids = 2 if args.shape == "quad" else 1
+    ped = nuclear_pedigree(pm, args.families, kids)
     B, P = args.batch, args.pool
-    eng = pm.Engine(ped, pm.Params.defaults(), device=local, max_batch=B)
+    params = pm.Params.defaults(denovo=1 if args.denovo else 0)
+    eng = pm.Engine(ped, params, device=local, max_batch=B)
     npers = ped.n_person
     bufs = []
-    for p in range(P):
+    for p in range(P):   # this rank's shard of the synthetic site stream (weak scaling)
         d_pl, d_dm, d_ref = eng.alloc(B * npers * 10), eng.alloc(B * npers * 4), eng.alloc(B)
         eng.synth(B, args.seed, (rank * P + p) * B, d_pl, d_dm, d_ref)
         bufs.append((d_pl, d_dm, d_ref))
 
+    host = None
+    if args.host_inputs:   # copy the resident batches to (pageable) host arrays once
+        host = []
+        for d_pl, d_dm, d_ref in bufs:
+            hpl, hdm, href = np.empty(B * npers * 10, np.uint8), np.empty(B * npers, np.uint32), np.empty(B, np.uint8)
+            eng.to_host(hpl, d_pl, hpl.nbytes); eng.to_host(hdm, d_dm, hdm.nbytes); eng.to_host(href, d_ref, href.nbytes)
+            host.append((hpl, hdm, href))
+
     def step(i):
+        if host is not None:
+            eng.run(*host[i % P])   # H2D inputs, pipeline, D2H results + genotype rows
+            return
         d_pl, d_dm, d_ref = bufs[i % P]
         eng.run_device(B, d_pl, d_dm, d_ref)
         eng.sync()
 
     def barrier():
-        if dist is not None:
+        if world > 1:
+            import torch.distributed as dist
             dist.barrier()
 
     for i in range(args.warmup):
@@ -140,25 +191,25 @@ def main():
         step(i)
     eng.sync()
     barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = max_over_ranks(time.perf_counter() - t0, dev)
     ks = eng.kernel_stats()
-    counters = eng.counters().as_array()
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        c = torch.tensor(counters, dtype=torch.int64, device="cuda")
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)   # the single RCCL all-reduce of the section counters
-        counters = c.cpu().numpy()
+    counters = allreduce_counters(eng.counters().as_array(), dev)   # the single RCCL all-reduce
 
     total_sites = B * args.steps * world
     value = total_sites / elapsed
-    # dominant kernel roofline (SURVEY 8(d) algorithmic op count, log10 counted as 1 op)
-    nf, K = args.families, args.kids
-    ops = ks.evals * (19 * nf + 17) + ks.items * nf * (18 + 36 * K)
+    nf, K = args.families, kids
     kern_s = ks.kernel_ms * 1e-3
-    achieved = ops / kern_s / 1e12 if kern_s > 0 else 0.0
+    launches = max(1, ks.launches)
+    avg_launch_s = kern_s / launches
+    # k_brent algorithmic bytes: every launch reads the PL block (nPerson x 10 B) of each site it touches once
+    alg_bytes_launch = ks.site_visits * npers * 10 / launches
+    achieved_gbs = alg_bytes_launch / avg_launch_s / 1e9 if kern_s > 0 else 0.0
+    traffic, pmc_file = pmc_traffic()
+    # SURVEY 8(d) algorithmic FP64 op count (log10 counted as 1 op)
+    ops = ks.evals * (19 * nf + 17) + ks.items * nf * (18 + 36 * K)
+    achieved_tops = ops / kern_s / 1e12 if kern_s > 0 else 0.0
+    peak_meas = measured_fp64_peak()
+    peak_tops = peak_meas or FP64_NONFMA_TOPS
     b_site = 14 * npers + 1
     if rank == 0:
         out = {
@@ -166,16 +217,21 @@ def main():
             "value": value, "unit": "sites/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": f"{nf} nuclear families (2 parents + {K} kids), synthetic GLF sites per SURVEY 8(d), "
-                                   f"dense blocks resident in HBM", "families": nf, "persons": npers,
-                       "sites_per_step_per_gpu": B, "distinct_sites_per_gpu": B * P, "parallelism": f"site-shard x{world}"},
-            "roofline": {"bound": "fp64-valu", "kernel": "k_brent", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
-                         "frac_of_nonfma_issue_peak": achieved / FP64_NONFMA_TFLOPS, "traffic": None,
-                         "launches": ks.launches, "kernel_ms_total": ks.kernel_ms,
-                         "avg_launch_ms": ks.kernel_ms / max(1, ks.launches), "evals": ks.evals, "items": ks.items,
-                         "log10_per_s": ks.evals * nf / kern_s if kern_s > 0 else 0.0,
-                         "ops_per_site": ops / max(1, ks.sites)},
+            "config": {"workload": f"{nf} nuclear {args.shape} families (2 parents + {K} kids), synthetic GLF-shaped "
+                                   f"sites per SURVEY 8(d) generated in HBM" + (", --denovo" if args.denovo else ""),
+                       "families": nf, "persons": npers, "sites_per_step_per_gpu": B,
+                       "distinct_sites_per_gpu": B * P, "parallelism": f"site-shard x{world}",
+                       "inputs": "host (PCIe-inclusive)" if args.host_inputs else "HBM-resident"},
+            "roofline": {"bound": "hbm", "kernel": "k_brent", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS,
+                         "traffic": traffic, "traffic_source": pmc_file,
+                         "algorithmic_bytes_per_launch": alg_bytes_launch, "avg_launch_ms": avg_launch_s * 1e3,
+                         "launches": ks.launches, "note": "k_brent is FP64-VALU bound; see roofline_fp64"},
+            "roofline_fp64": {"bound": "fp64-valu", "kernel": "k_brent", "achieved": achieved_tops, "peak": peak_tops,
+                              "unit": "Tops/s (mul/add, non-FMA)", "frac": achieved_tops / peak_tops,
+                              "peak_source": "measured max(v_mul_f64, v_add_f64) issue rate" if peak_meas else "spec/2",
+                              "evals": ks.evals, "items": ks.items, "ops_per_site": ops / max(1, ks.sites),
+                              "log10_per_s": ks.evals * nf / kern_s if kern_s > 0 else 0.0},
             "hbm": {"algorithmic_bytes_per_site": b_site, "achieved_GBs": value * b_site / 1e9 / world,
                     "peak_GBs": HBM_PEAK_GBS, "frac": value * b_site / 1e9 / world / HBM_PEAK_GBS},
             "counters": {"sites": int(counters[:5].sum()), "homo_ref": int(counters[9]),
@@ -194,7 +250,8 @@ def main():
         for p in d:
             eng.free(p)
     eng.close()
-    if dist is not None:
+    if world > 1:
+        import torch.distributed as dist
         dist.destroy_process_group()
 
 

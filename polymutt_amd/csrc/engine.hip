@@ -109,7 +109,7 @@ struct DevArgs {
   double* mono_plain;      // [n] MonomorphismLogLikelihood
   int8_t* item_sex;        // [n] member `sex` of famlk[0] for the cfg-7 item
   int* items[N_LISTS];
-  int* counts;             // [N_LISTS] + [3] rows + [4] first_emit + [5] err + [6] evals_total(lo)
+  int* counts;             // [0..2] list sizes, [3] rows, [4] first emitted site, [5] Brent stuck, [8]/[9] quick items/site visits
   unsigned long long* eval_total;
   int* row_site;           // [n] emitted row -> site
   unsigned long long* counters;   // pm_counters as 16 x u64
@@ -569,7 +569,10 @@ __global__ void __launch_bounds__(T) k_brent(DevArgs A, int list) {
   const int nItems = A.counts[list];
   const int* items = A.items[list];
   int par = 0;
-  for (int it = blockIdx.x; it < nItems; it += gridDim.x) {
+  // XCD-aware item order: blocks are dealt round-robin to the 8 XCDs (separate L2s), so consecutive
+  // items -- the 2-4 configurations of one site, which read the same PL block -- go to blocks of one XCD.
+  const int vb = (gridDim.x % 8 == 0) ? (blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8 : blockIdx.x;
+  for (int it = vb; it < nItems; it += gridDim.x) {
     const int item = items[it];
     const int site = item >> 3, cfg = item & 7;
     const int r = A.ref[site];
@@ -853,6 +856,11 @@ __global__ void k_quick_final(DevArgs A) {   // quick decision; survivors enter 
   const int nit = A.denovo ? 4 : 3;
   const int slot = atomicAdd(&A.counts[0], nit);
   for (int k = 0; k < nit; k++) A.items[0][slot + k] = (site << 3) | (A.denovo ? k : k + 1);
+}
+
+__global__ void k_quick_stats(DevArgs A) {   // the quick lists are recycled for the main stage: keep their sizes
+  A.counts[8] = A.counts[1] + A.counts[2];
+  A.counts[9] = A.counts[1] / 3 + A.counts[2] / 3;
 }
 
 // main.cpp:539-574 per site; counters aggregated per block
@@ -1658,6 +1666,7 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
     if (wsmax > 0) {
       const size_t cap = (size_t)1 << 30, per_lane = (size_t)wsmax * sizeof(double);
       E->grid_brent = (int)std::max<size_t>(E->n_cu, std::min<size_t>(E->grid_brent, cap / (per_lane * T)));
+      E->grid_brent -= E->grid_brent % 8;   // keep the XCD-aware item order exact
       E->grid_post = (int)std::max<size_t>(E->n_cu, std::min<size_t>(E->grid_post, cap / (per_lane * 256)));
       const size_t lanes = std::max((size_t)E->grid_brent * T, (size_t)E->grid_post * 256);
       DALLOC(E->d_ws, lanes * wsmax);
@@ -1811,6 +1820,7 @@ static int run_pipeline(pm_engine* E, int n, const uint8_t* pl, const uint32_t* 
     if ((rc = launch_brent(E, A, 2, true))) return rc;
     hipLaunchKernelGGL(k_quick_final, dim3(gb), dim3(tb), 0, E->stream, A);
     HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_quick_stats, dim3(1), dim3(1), 0, E->stream, A);
     HIP_TRY(hipMemsetAsync(E->d_counts + 1, 0, 2 * sizeof(int), E->stream));
   }
   if ((rc = launch_brent(E, A, 0))) return rc;
@@ -1867,7 +1877,8 @@ int pm_engine_sync(pm_engine* E) {
   int counts[16];
   HIP_TRY(hipMemcpy(counts, E->d_counts, sizeof(counts), hipMemcpyDeviceToHost));
   if (counts[4] != 0x7fffffff) E->carry_postprob = true;
-  E->stats.items += (int64_t)counts[0] + counts[1] + counts[2];
+  E->stats.items += (int64_t)counts[0] + counts[1] + counts[2] + counts[8];
+  E->stats.site_visits += (int64_t)counts[0] / (E->par.denovo ? 4 : 3) + counts[1] / 3 + counts[2] + counts[9];
   E->stats.sites += E->last_n;
   int rc = collect_stats(E);
   if (rc) return rc;

@@ -72,7 +72,7 @@ class Counters(C.Structure):
 
 class KernelStats(C.Structure):
     _fields_ = [("launches", i64), ("kernel_ms", f64), ("evals", i64), ("fam_evals", i64), ("items", i64),
-                ("sites", i64)]
+                ("sites", i64), ("site_visits", i64)]
 
 
 SITE_DTYPE = np.dtype([

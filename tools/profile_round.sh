@@ -1,0 +1,27 @@
+#!/bin/bash
+# tools/profile_round.sh ROUND -- run on the GPU box (via gpurun) to collect the round's profiles:
+#   1. rocprofv3 --kernel-trace --stats of the default bench command (kernel time summary)
+#   2. separate PMC passes (FETCH_SIZE, WRITE_SIZE, SQ busy/stall counters) -- never combined with
+#      any other trace domain
+#   3. the FP64 issue-rate microbenchmark (tools/fp64_peak)
+# Outputs land in gpurun_out/prof_$ROUND/; tools/summarize_profile.py turns them into profiles/.
+set -u
+ROUND=${1:-r01}
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+OUT=$R/gpurun_out/prof_$ROUND
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+BENCH="python3 $R/bench.py --no-cpu-baseline"
+step() {   # step NAME SECONDS CMD...
+  local name=$1 secs=$2; shift 2
+  echo "[$(date +%T)] $name" >&2
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
+  local rc=$?
+  if [ $rc -ne 0 ]; then echo "step $name failed rc=$rc" >&2; tail -20 "$OUT/$name.err" >&2; exit $rc; fi
+}
+step fp64_peak 120 "$R/tools/fp64_peak"
+step trace 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- $BENCH
+step pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- $BENCH --steps 4 --warmup 1
+step pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- $BENCH --steps 4 --warmup 1
+step pmc_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmc_sq" -o run -- $BENCH --steps 4 --warmup 1
+echo done >&2

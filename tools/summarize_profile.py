@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile_round.sh run (gpurun_out/prof_ROUND) into committed files under profiles/:
+
+  profiles/ROUND_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary of the default bench command
+  profiles/ROUND_bench.json         the bench JSON line printed under that profiler run
+  profiles/ROUND_pmc.json           per kernel: dispatches and mean FETCH_SIZE / WRITE_SIZE / SQ counters per
+                                    dispatch, plus HBM bytes per dispatch with the gfx950 correction
+                                    (MI355X_MICROARCH.md "HBM": FETCH_SIZE counts 1/2 of the bytes -> x2)
+  profiles/ROUND_fp64_peak.json     measured FP64 issue rates (tools/fp64_peak.hip)
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def short(name):
+    n = name.split("(")[0].replace("void ", "")
+    return n
+
+
+def main():
+    rnd = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{rnd}")
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, f"{rnd}_kernel_stats.csv"))
+    bench = [l for l in open(os.path.join(src, "trace.out")).read().splitlines() if l.startswith("{")]
+    if bench:
+        with open(os.path.join(dst, f"{rnd}_bench.json"), "w") as fh:
+            fh.write(bench[-1] + "\n")
+    peak = [l for l in open(os.path.join(src, "fp64_peak.out")).read().splitlines() if l.startswith("{")]
+    if peak:
+        with open(os.path.join(dst, f"{rnd}_fp64_peak.json"), "w") as fh:
+            fh.write(peak[-1] + "\n")
+    acc = defaultdict(lambda: defaultdict(float))
+    disp = defaultdict(set)
+    for sub in ("pmc_fetch", "pmc_write", "pmc_sq"):
+        path = os.path.join(src, sub, "run_counter_collection.csv")
+        if not os.path.exists(path):
+            continue
+        for row in csv.DictReader(open(path)):
+            k = short(row["Kernel_Name"])
+            acc[k][row["Counter_Name"]] += float(row["Counter_Value"])
+            disp[(k, sub)].add(row["Dispatch_Id"])
+    out = {}
+    for k, counters in acc.items():
+        d = {}
+        for c, v in counters.items():
+            sub = "pmc_fetch" if c == "FETCH_SIZE" else "pmc_write" if c == "WRITE_SIZE" else "pmc_sq"
+            n = max(1, len(disp[(k, sub)]))
+            d[c + "_per_dispatch"] = v / n
+            d["dispatches_" + sub] = n
+        if "FETCH_SIZE_per_dispatch" in d:
+            # FETCH_SIZE / WRITE_SIZE are reported in KiB
+            d["hbm_read_bytes_per_dispatch"] = 2 * d["FETCH_SIZE_per_dispatch"] * 1024
+        if "WRITE_SIZE_per_dispatch" in d:
+            d["hbm_write_bytes_per_dispatch"] = d["WRITE_SIZE_per_dispatch"] * 1024
+        out[k] = d
+    with open(os.path.join(dst, f"{rnd}_pmc.json"), "w") as fh:
+        json.dump(out, fh, indent=1, sort_keys=True)
+    print(json.dumps({k: {kk: round(vv, 1) for kk, vv in v.items()} for k, v in out.items()}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
