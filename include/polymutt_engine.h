@@ -90,9 +90,18 @@ typedef struct {
   int32_t force_call;          /* set by --pos */
   int32_t all_sites;           /* --all_sites */
   int32_t quick_call;          /* --quick_call */
-  int32_t exact_log10;         /* engine numerics: 1 = one log10 per family, summed (the reference's form);
-                                  0 = normalised product of family likelihoods, one log10 per evaluation */
+  int32_t numerics;            /* pm_numerics: how the engine evaluates the Brent objective */
 } pm_params;
+
+/* Objective-evaluation numerics.  All three compute CalcAllFamLogLikelihood; they differ in rounding only.
+ *   PM_NUM_PRODUCT: each family's likelihood exactly as the reference forms it (same operations, same order),
+ *                   families combined as a normalised product, one log10 per evaluation;
+ *   PM_NUM_EXACT:   one log10 per family, summed (the reference's form; ~2x slower);
+ *   PM_NUM_POLY:    (default) nuclear families as a 4-FMA Horner quartic in min(f,1-f)/max(f,1-f) on the lean
+ *                   autosomal kernel (>1 family); every other kernel flavour uses PRODUCT.  Objective values
+ *                   differ from the reference by ~1e-14 relative, so on objectives flat to rounding noise Brent
+ *                   may stop at another point of equal likelihood (never visible in the VCF). */
+typedef enum { PM_NUM_PRODUCT = 0, PM_NUM_EXACT = 1, PM_NUM_POLY = 2 } pm_numerics;
 
 /* Site status codes (which `continue` of main.cpp:300-594 was taken). */
 typedef enum {

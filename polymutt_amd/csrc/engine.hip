@@ -33,6 +33,12 @@
 
 #define MALE 1
 #define FEMALE 2
+#ifndef PM_HOIST_CHUNK
+#define PM_HOIST_CHUNK 4
+#endif
+#ifndef PM_POLY_WAVES
+#define PM_POLY_WAVES 2
+#endif
 
 // ------------------------------------------------------------------------------------------------
 // error reporting (thread-local, C ABI)
@@ -66,6 +72,7 @@ enum UnitType { U_NONE = 0, U_NUC = 1, U_FP = 2 /* founders-only chunk of <=3 pe
 struct DevArgs {
   // pedigree
   int n_fam, n_person, n_fam_gt1, single_nuclear;
+  int max_nuc;             // largest nuclear family (persons)
   int chrom, denovo;
   const int* fam_start;
   const int* fam_kind;
@@ -86,6 +93,7 @@ struct DevArgs {
   double* ws;              // peeling workspace, lane-interleaved
   int ws_per_lane;         // doubles per lane (max over ES families of n*ns + couples*ns*ns)
   int unrelated;           // --quick_call MakeUnrelated(): every family is all-founder
+  double theta_one;        // 1.0 (opaque to the compiler; timing experiments only)
   // tables
   const double* lktab;     // [256]
   const double* M;         // [100] genotype mutation matrix
@@ -525,6 +533,105 @@ __device__ __forceinline__ void lane_prod(double f, const int4* unit, const doub
   e = ev[0];
 }
 
+// Lean product mode (autosomal HWE parent prior, nuclear families only): a family's likelihood
+// Sum_k cond[k] * SetParentPrior(f)[k] is the quartic f^4 a0 + f^3 g a1 + f^2 g^2 a2 + f g^3 a3 + g^4 a4
+// (a0 = c0, a1 = 2(c1+c3), a2 = c2+4c4+c6, a3 = 2(c5+c7), a4 = c8; SetParentPrior :323-331).  With
+// M = max(f, g) and t = min(f, g)/M <= 1 it is M^4 h(t), h a 4-FMA Horner polynomial with non-negative
+// coefficients (no cancellation: relative error <= ~8 ulp); M^(4 nFam) leaves the product as one log10.
+__device__ __forceinline__ void fold_poly(const double* c, double* a) {
+  a[0] = c[0];
+  a[1] = 2 * (c[1] + c[3]);
+  a[2] = c[2] + 4 * c[4] + c[6];
+  a[3] = 2 * (c[5] + c[7]);
+  a[4] = c[8];
+}
+
+// Chunked hoisting for the lean polynomial kernel when every nuclear family has <= 4 persons: the PL
+// bytes of 4 slots (4 x 12 loads) are issued before any of them is used, so the HBM round trips of a
+// chunk overlap instead of running slot after slot.  Arithmetic is hoist_nuc's, in the same order.
+template <int S, int T>
+__device__ __forceinline__ void hoist_poly4(const DevArgs& A, const ItemCtx& I, const uint8_t* pl, const double* lk,
+                                            double (*a)[5], unsigned& live) {
+  constexpr int C = S < PM_HOIST_CHUNK ? S : PM_HOIST_CHUNK;
+#pragma unroll
+  for (int c0 = 0; c0 < S; c0 += C) {
+    uint32_t by[C][12];
+    int nn[C];
+#pragma unroll
+    for (int j = 0; j < C; j++) {
+      const int4 u = A.units[(c0 + j) * T + threadIdx.x];
+      const bool nuc = u.x == U_NUC;
+      nn[j] = nuc ? u.w : 0;
+      const uint8_t* F = pl + (size_t)u.z * 10;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const bool ok = q < nn[j];
+        const uint8_t* R = F + (ok ? q * 10 : 0);
+        by[j][3 * q + 0] = ok ? R[I.g11] : 0;
+        by[j][3 * q + 1] = ok ? R[I.g12] : 0;
+        by[j][3 * q + 2] = ok ? R[I.g22] : 0;
+      }
+      if (nuc) live |= 1u << (c0 + j);
+    }
+#pragma unroll
+    for (int j = 0; j < C; j++) {
+      double c9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+      if (nn[j] >= 2) {
+        double kids[9];
+#pragma unroll
+        for (int k = 0; k < 9; k++) kids[k] = 1.0;
+#pragma unroll
+        for (int q = 2; q < 4; q++)
+          if (q < nn[j]) {
+            const double l11 = lk[by[j][3 * q]], l12 = lk[by[j][3 * q + 1]], l22 = lk[by[j][3 * q + 2]];
+#pragma unroll
+            for (int k = 0; k < 9; k++) kids[k] *= d_one_kid(k, PM_CHR_AUTO, 0, l11, l12, l22);
+          }
+        const double lF[3] = {lk[by[j][0]], lk[by[j][1]], lk[by[j][2]]};
+        const double lM[3] = {lk[by[j][3]], lk[by[j][4]], lk[by[j][5]]};
+#pragma unroll
+        for (int x = 0; x < 3; x++)
+#pragma unroll
+          for (int y = 0; y < 3; y++) c9[3 * x + y] = kids[3 * x + y] * (lF[x] * lM[y]);
+      }
+      fold_poly(c9, a[c0 + j]);
+    }
+  }
+}
+
+// Four interleaved (mantissa, exponent) accumulators: short dependency chains, few live registers.
+// Slots below `full` are occupied on every lane (families are dealt round-robin); only the slot rows at
+// or above it can be empty and are masked (h = 1).
+template <int S>
+__device__ __forceinline__ void lane_poly(bool lo, double t, int full, unsigned live, const double (*a)[5], double& m,
+                                          int& e) {
+  constexpr int NA = S < 4 ? S : 4;
+  double am[NA];
+  int ae[NA];
+#pragma unroll
+  for (int j = 0; j < NA; j++) { am[j] = 1.0; ae[j] = 0; }
+#pragma unroll
+  for (int s = 0; s < S; s++) {
+    double h;
+    if (lo) h = fma(t, fma(t, fma(t, fma(t, a[s][0], a[s][1]), a[s][2]), a[s][3]), a[s][4]);
+    else h = fma(t, fma(t, fma(t, fma(t, a[s][4], a[s][3]), a[s][2]), a[s][1]), a[s][0]);
+    if (s >= full) h = ((live >> s) & 1) ? h : 1.0;
+    int x;
+    am[s % NA] = frexp(am[s % NA] * h, &x);   // |am| in [0.5, 1), h >= ~1e-128 for nuclear families: no underflow
+    ae[s % NA] += x;
+  }
+#pragma unroll
+  for (int w = 1; w < NA; w *= 2)
+#pragma unroll
+    for (int j = 0; j + w < NA; j += 2 * w) {
+      int x;
+      am[j] = frexp(am[j] * am[j + w], &x);
+      ae[j] += ae[j + w] + x;
+    }
+  m = am[0];
+  e = ae[0];
+}
+
 template <int T>
 __device__ __forceinline__ double block_logprod(double m, int e, double* red, int* rede, int& par) {
 #pragma unroll
@@ -554,8 +661,14 @@ __device__ __forceinline__ double block_logprod(double m, int e, double* red, in
 
 // GEN=false: lean autosomal nuclear-only kernel; GEN=true: chrX/Y/MT, de novo, founder-only units;
 // ES=true additionally peels the lane's extended families (instantiated only for pedigrees that have them).
-template <int T, int S, bool PROD, bool GEN, bool ES>
-__global__ void __launch_bounds__(T) k_brent(DevArgs A, int list) {
+// Occupancy target (waves per SIMD) of a Brent flavour: the lean polynomial kernel keeps 5 doubles per
+// family, so even at S=16 two items fit on a SIMD if the hoisting phase is kept from spreading out.
+template <int T, int S, int NUM, bool GEN>
+constexpr int brent_waves() { return (NUM == PM_NUM_POLY && !GEN && T == 64 && S >= 8) ? PM_POLY_WAVES : 1; }
+
+template <int T, int S, int NUM, bool GEN, bool ES>
+__global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(DevArgs A, int list) {
+  constexpr bool PROD = NUM != PM_NUM_EXACT;
   __shared__ double s_lk[256];
   __shared__ double s_M[100];
   __shared__ double s_red[96];
@@ -564,8 +677,12 @@ __global__ void __launch_bounds__(T) k_brent(DevArgs A, int list) {
   for (int i = threadIdx.x; i < 100; i += T) s_M[i] = A.M[i];
   __syncthreads();
   int4 unit[S];
+  constexpr bool POLYK = NUM == PM_NUM_POLY && !GEN;
+  if constexpr (!POLYK) {
 #pragma unroll
-  for (int s = 0; s < S; s++) unit[s] = A.units[s * T + threadIdx.x];
+    for (int s = 0; s < S; s++) unit[s] = A.units[s * T + threadIdx.x];
+  }
+  const int full = A.n_fam / T;   // POLY: slot rows below this are occupied on every lane
   const int nItems = A.counts[list];
   const int* items = A.items[list];
   int par = 0;
@@ -590,12 +707,26 @@ __global__ void __launch_bounds__(T) k_brent(DevArgs A, int list) {
     else pmode = A.chrom == PM_CHR_X ? PR_X : A.chrom == PM_CHR_Y ? PR_Y : A.chrom == PM_CHR_MT ? PR_MT : PR_AUTO;
 
     const uint8_t* pl = A.pl + (size_t)site * A.n_person * 10;
-    double cond[S][9];
+    // POLY (lean product kernel, always the autosomal HWE prior with > 1 family): 5 coefficients per family
+    constexpr bool POLY = NUM == PM_NUM_POLY && !GEN;
+    constexpr int NC = POLY ? 5 : 9;
+    double cond[S][NC];
     int fl[S];
+    unsigned live = 0;
+    bool hoisted = false;
+    if constexpr (POLY) {
+      if (A.max_nuc <= 4) { hoist_poly4<S, T>(A, I, pl, s_lk, cond, live); hoisted = true; }
+    }
 #pragma unroll
     for (int s = 0; s < S; s++) {
       fl[s] = 0;
-      if (unit[s].x == U_NUC) hoist_nuc<GEN>(A, I, pl, s_lk, s_M, unit[s].z, unit[s].w, cond[s]);
+      if (hoisted) continue;
+      if constexpr (POLY) {
+        const int4 u = A.units[s * T + threadIdx.x];   // L1/L2-resident; not kept in registers
+        double c9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        if (u.x == U_NUC) { hoist_nuc<GEN>(A, I, pl, s_lk, s_M, u.z, u.w, c9); live |= 1u << s; }
+        fold_poly(c9, cond[s]);
+      } else if (unit[s].x == U_NUC) hoist_nuc<GEN>(A, I, pl, s_lk, s_M, unit[s].z, unit[s].w, cond[s]);
       else if (GEN && unit[s].x == U_FP) fl[s] = hoist_fp(A, I, pl, s_lk, unit[s].z, unit[s].w & 0xFF, cond[s]);
     }
     double* raw = A.raw + (size_t)site * 8;
@@ -611,9 +742,27 @@ __global__ void __launch_bounds__(T) k_brent(DevArgs A, int list) {
     bool ok = false;
     for (;;) {
       double tot;
-      if (PROD) {
+      if constexpr (POLY) {
+        const double g = 1 - x;
+        const bool lo = x <= g;
+        const double M = lo ? g : x;
         double m; int e;
-        lane_prod<S, GEN>(x, unit, cond, fl, pmode, m, e);
+        lane_poly<S>(lo, (lo ? x : g) / M, full, live, (const double(*)[5])cond, m, e);
+        tot = block_logprod<T>(m, e, s_red, s_rede, par) + (4.0 * A.n_fam) * log10(M);
+#ifdef PM_EXP_EVAL_TWICE   // timing experiment only: a second, identical evaluation the compiler cannot merge
+        {
+          const double x2 = x * A.theta_one;
+          const double g2 = 1 - x2;
+          const bool lo2 = x2 <= g2;
+          const double M2 = lo2 ? g2 : x2;
+          double m2; int e2;
+          lane_poly<S>(lo2, (lo2 ? x2 : g2) / M2, full, live, (const double(*)[5])cond, m2, e2);
+          tot = 0.5 * (tot + block_logprod<T>(m2, e2, s_red, s_rede, par) + (4.0 * A.n_fam) * log10(M2));
+        }
+#endif
+      } else if (PROD) {
+        double m; int e;
+        lane_prod<S, GEN>(x, unit, (const double(*)[9])cond, fl, pmode, m, e);
         if (ES && A.ext_count)   // extended families of this lane: Elston-Stewart peeling per evaluation
           for (int q = 0; q < A.ext_count[threadIdx.x]; q++) {
             const int f = A.ext_fam[q * T + threadIdx.x];
@@ -626,7 +775,7 @@ __global__ void __launch_bounds__(T) k_brent(DevArgs A, int list) {
           }
         tot = block_logprod<T>(m, e, s_red, s_rede, par);
       } else {
-        double part = lane_loglik<S, GEN>(x, unit, cond, fl, pmode);
+        double part = lane_loglik<S, GEN>(x, unit, (const double(*)[9])cond, fl, pmode);
         if (ES && A.ext_count)
           for (int q = 0; q < A.ext_count[threadIdx.x]; q++) {
             const int f = A.ext_fam[q * T + threadIdx.x];
@@ -1332,7 +1481,7 @@ struct pm_engine {
   bool carry_postprob = false;
   std::vector<int> fam_start_h;
   std::vector<int8_t> sex_h;
-  int single_nuclear = 0;
+  int single_nuclear = 0, max_nuc = 0;
   double prior = 0;
   int n_founders = 0, male_founders = 0, female_founders = 0;
   // device buffers
@@ -1535,6 +1684,10 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
     return PM_EHIP;
   }
   if (device < 0 || device >= ndev) { pm_set_last_error("pm_engine_create: device index out of range"); return PM_EINVAL; }
+  if (par->numerics < PM_NUM_PRODUCT || par->numerics > PM_NUM_POLY) {
+    pm_set_last_error("pm_engine_create: unknown numerics mode");
+    return PM_EINVAL;
+  }
   pm_engine* E = new pm_engine;
   E->device = device;
   E->par = *par;
@@ -1543,6 +1696,8 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
   E->max_batch = max_batch;
   E->n_founders = ped->n_founders; E->male_founders = ped->male_founders; E->female_founders = ped->female_founders;
   E->single_nuclear = (ped->n_fam == 1 && ped->fam_kind[0] == PM_FAM_NUCLEAR) ? 1 : 0;
+  for (int f = 0; f < ped->n_fam; f++)
+    if (ped->fam_kind[f] == PM_FAM_NUCLEAR) E->max_nuc = std::max(E->max_nuc, ped->fam_start[f + 1] - ped->fam_start[f]);
   for (int f = 0; f < ped->n_fam; f++) {
     if (ped->fam_kind[f] != PM_FAM_NUCLEAR) E->has_fp = true;
     if (ped->fam_kind[f] == PM_FAM_EXTENDED) E->n_ext++;
@@ -1569,7 +1724,7 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
   // is spread over 2-8 waves (one barrier per evaluation).  Sections on chrX/Y/MT run the generic
   // kernel on the same plan.
   {
-    const bool gen = par->denovo || E->has_fp;
+    const bool gen = par->denovo || E->has_fp || ped->n_fam == 1;
     static const int2 lean[] = {{64, 1}, {64, 2}, {64, 4}, {64, 8}, {64, 16}, {512, 4}, {1024, 4}, {1024, 8}};
     static const int2 generic[] = {{64, 1}, {64, 2}, {64, 4}, {64, 8}, {256, 4}, {512, 4}, {1024, 4}, {1024, 8}};
     const int2* pref = gen ? generic : lean;
@@ -1731,12 +1886,14 @@ static DevArgs make_args(pm_engine* E, int n, const uint8_t* pl, const uint32_t*
   DevArgs A;
   memset(&A, 0, sizeof(A));
   A.n_fam = E->n_fam; A.n_person = E->n_person; A.n_fam_gt1 = E->n_fam > 1; A.single_nuclear = E->single_nuclear;
+  A.max_nuc = E->max_nuc;
   A.chrom = E->chrom; A.denovo = E->par.denovo;
   A.fam_start = E->d_fam_start; A.fam_kind = E->d_fam_kind; A.sex = E->d_sex; A.fa_local = E->d_fa; A.mo_local = E->d_mo;
   A.units = E->d_units; A.T = E->T; A.S = E->S;
   A.fam_founders = E->d_fam_founders; A.is_founder = E->d_is_founder; A.peel_start = E->d_peel_start; A.steps = E->d_steps;
   A.ext_count = E->n_ext ? E->d_ext_count : nullptr; A.ext_fam = E->d_ext_fam;
   A.T10 = E->d_T10; A.T10dn = E->d_T10dn; A.ws = E->d_ws; A.ws_per_lane = E->ws_per_lane;
+  A.theta_one = 1.0;
   A.unrelated = E->par.quick_call ? 1 : 0;   // k_prep: route sites through the quick pre-filter first
   A.lktab = E->d_lktab; A.M = E->d_M; A.syn = E->d_syn;
   A.precision = E->par.precision; A.posterior = E->par.posterior; A.theta = E->par.theta;
@@ -1759,14 +1916,18 @@ static DevArgs make_args(pm_engine* E, int n, const uint8_t* pl, const uint32_t*
 }
 
 typedef void (*BrentFn)(DevArgs, int);
-static BrentFn brent_kernel(int T, int S, bool prod, bool gen, bool es) {
-#define PMK(t, s)                                                                              \
-  if (T == t && S == s) {                                                                      \
-    if (gen) return prod ? k_brent<t, s, true, true, false> : k_brent<t, s, false, true, false>; \
-    return prod ? k_brent<t, s, true, false, false> : k_brent<t, s, false, false, false>;        \
+// numerics: PM_NUM_PRODUCT / PM_NUM_EXACT for every flavour; PM_NUM_POLY only for the lean kernel
+// (the generic and ES flavours fall back to PRODUCT numerics).
+static BrentFn brent_kernel(int T, int S, int num, bool gen, bool es) {
+  const int n = (num == PM_NUM_POLY && gen) ? PM_NUM_PRODUCT : num;
+#define PMK(t, s)                                                                                             \
+  if (T == t && S == s) {                                                                                     \
+    if (gen) return n == PM_NUM_EXACT ? k_brent<t, s, PM_NUM_EXACT, true, false> : k_brent<t, s, PM_NUM_PRODUCT, true, false>; \
+    return n == PM_NUM_EXACT ? k_brent<t, s, PM_NUM_EXACT, false, false>                                      \
+         : n == PM_NUM_POLY ? k_brent<t, s, PM_NUM_POLY, false, false> : k_brent<t, s, PM_NUM_PRODUCT, false, false>; \
   }
 #define PMKE(t, s) \
-  if (T == t && S == s) return prod ? k_brent<t, s, true, true, true> : k_brent<t, s, false, true, true>;
+  if (T == t && S == s) return n == PM_NUM_EXACT ? k_brent<t, s, PM_NUM_EXACT, true, true> : k_brent<t, s, PM_NUM_PRODUCT, true, true>;
   if (es) {
     PMKE(64, 1) PMKE(64, 2) PMKE(64, 4) PMKE(64, 8) PMKE(256, 4) PMKE(512, 4) PMKE(1024, 4) PMKE(1024, 8)
     return nullptr;
@@ -1782,12 +1943,12 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
   DevArgs A = A0;
   int T = E->T, S = E->S, grid = E->grid_brent;
   // lean kernel: autosome, no de novo model, nuclear families only (the common case)
-  bool gen = E->chrom != PM_CHR_AUTO || E->par.denovo || E->has_fp;
+  bool gen = E->chrom != PM_CHR_AUTO || E->par.denovo || E->has_fp || E->n_fam == 1;
   if (unrelated) {   // MakeUnrelated(): all-founder products over the quick plan, no ES, no de novo model
     A.units = E->d_units_q; A.T = T = E->Tq; A.S = S = E->Sq; grid = E->grid_q;
     A.ext_count = nullptr; A.unrelated = 1; A.denovo = 0; gen = true;
   } else A.unrelated = 0;
-  BrentFn fn = brent_kernel(T, S, !E->par.exact_log10, gen, !unrelated && E->n_ext > 0);
+  BrentFn fn = brent_kernel(T, S, E->par.numerics, gen, !unrelated && E->n_ext > 0);
   if (!fn) { pm_set_last_error("launch_brent: no kernel variant for the lane plan"); return PM_EINVAL; }
   hipEvent_t a, b;
   HIP_TRY(hipEventCreate(&a));

@@ -15,7 +15,7 @@ pm_params Options::params() const {
   p.theta = theta; p.poly_tstv = tstv; p.precision = precision; p.posterior = posterior;
   p.min_total_depth = minTotalDepth; p.max_total_depth = maxTotalDepth; p.min_ps = minPS; p.min_map_quality = minMapQuality;
   p.denovo = denovo; p.denovo_mut_rate = denovo_rate; p.denovo_tstv = denovo_tstv; p.denovo_min_llr = denovo_llr;
-  p.force_call = force_call; p.all_sites = all_sites; p.quick_call = quick_call; p.exact_log10 = exact_log10;
+  p.force_call = force_call; p.all_sites = all_sites; p.quick_call = quick_call; p.numerics = exact_log10 ? PM_NUM_EXACT : numerics == "exact" ? PM_NUM_EXACT : numerics == "poly" ? PM_NUM_POLY : PM_NUM_PRODUCT;
   return p;
 }
 
@@ -33,7 +33,7 @@ Options parse_command_line(int argc, char** argv) {
       {"pos", 's', &o.positionFile}, {"all_sites", 'b', &o.all_sites}, {"gl_off", 'b', &o.gl_off},
       {"quick_call", 'b', &o.quick_call},
       // engine options (not in the reference)
-      {"gpu", 'i', &o.device}, {"batch", 'i', &o.batch}, {"exact_log10", 'b', &o.exact_log10},
+      {"gpu", 'i', &o.device}, {"batch", 'i', &o.batch}, {"exact_log10", 'b', &o.exact_log10}, {"numerics", 's', &o.numerics},
   };
   auto assign = [](Flag& f, const char* v) {
     switch (f.kind) {

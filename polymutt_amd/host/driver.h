@@ -16,6 +16,7 @@ struct Options {
   int minTotalDepth = 0, maxTotalDepth = 0, minMapQuality = 0, nthreads = 1;
   double minPS = 0;
   bool denovo = false, gl_off = false, quick_call = false, all_sites = false, force_call = false, exact_log10 = false;
+  std::string numerics = "poly";
   double denovo_rate = 1.5e-08, denovo_tstv = 2.0, denovo_llr = 0.01;
   int device = 0, batch = 4096;
   std::string cmd;

@@ -16,6 +16,7 @@ CASES = json.load(open(os.path.join(SYNTH, "cases.json")))
 
 LLK_RTOL = 1e-9
 FREQ_ATOL = 1e-6
+FLAT_RTOL = 1e-12
 
 
 def make_dataset(name, directory):
@@ -111,7 +112,7 @@ def compare_to_dump(res, dump, label=""):
         if (res[f][called] != dump[f][called]).any():
             i = int(np.nonzero((res[f] != dump[f]) & called)[0][0])
             problems.append(f"{label}{f} differs at site {i}: {res[f][i]} vs reference {dump[f][i]}")
-    flat = runs = 0
+    flat = nonflat = runs = 0
     for k in range(7):
         m = called & (dump["n_cfg"] > k)
         if not m.any():
@@ -121,12 +122,13 @@ def compare_to_dump(res, dump, label=""):
         if (rel > LLK_RTOL).any():
             i = int(np.argmax(rel))
             problems.append(f"{label}varllk[{k}] rel err {rel[i]:.3g} ({e[i]!r} vs reference {o[i]!r})")
-        if k > 0:
-            d = np.abs(res["varfreq"][m, k] - dump["varfreq"][m, k])
-            flat += int((d > FREQ_ATOL).sum())
+        if k > 0:   # see tests/parity.py: divergences on flat objectives are allowed, others bounded
+            d = np.abs(res["varfreq"][m, k] - dump["varfreq"][m, k]) > FREQ_ATOL
+            flat += int((d & (rel <= FLAT_RTOL)).sum())
+            nonflat += int((d & (rel > FLAT_RTOL)).sum())
             runs += int(m.sum())
-    if flat > max(2, 1e-3 * runs):
-        problems.append(f"{label}{flat} minimiser divergences in {runs} Brent runs")
+    if nonflat > max(2, 1e-3 * runs):
+        problems.append(f"{label}{nonflat} minimiser divergences on non-flat objectives in {runs} Brent runs")
     d = np.abs(res["var_post_prob"][called] - dump["var_post_prob"][called])
     if d.size and d.max() > 1e-9:
         problems.append(f"{label}var_post_prob max abs err {d.max():.3g}")
@@ -151,4 +153,4 @@ def compare_to_dump(res, dump, label=""):
     eval_path = int((diff & called[:, None]).any(axis=1).sum())
     assert not problems, "\n".join(problems)
     return {"sites": n, "called": int(called.sum()), "emitted": int(em.sum()), "flat_divergence": flat,
-            "brent_runs": runs, "eval_path_mismatch": eval_path}
+            "nonflat_divergence": nonflat, "brent_runs": runs, "eval_path_mismatch": eval_path}

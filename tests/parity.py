@@ -7,6 +7,7 @@ EXACT = ["status", "n_cfg", "maxidx", "emit", "total_depth", "num_samp_with_data
 LLK_RTOL = 1e-9      # log10-likelihoods: OCML log10 (<=1 ulp) + reduction order, ~1e-13 observed
 FREQ_ATOL = 1e-6     # Brent minimiser / AF
 QUAL_ATOL = 1e-6
+FLAT_RTOL = 1e-12    # |llk_engine - llk_oracle| / |llk| at which an objective counts as flat
 DOSE_ATOL = 1e-9
 
 
@@ -21,7 +22,7 @@ def compare_results(eng, ora, ecalls, ocalls, label=""):
             problems.append(f"{label}{f}: {len(bad)} sites differ, first site {i}: engine {eng[f][i]} oracle {ora[f][i]}")
     called = ora["status"] == 0
     ncfg = ora["n_cfg"]
-    flat_div = runs = 0
+    flat_div = nonflat_div = runs = 0
     for k in range(7):
         m = called & (ncfg > k)
         if not m.any():
@@ -32,17 +33,22 @@ def compare_results(eng, ora, ecalls, ocalls, label=""):
             i = np.argmax(rel)
             problems.append(f"{label}varllk[{k}] rel err {rel[i]:.3g} (engine {e[i]!r} oracle {o[i]!r})")
         if k > 0:
-            # A Brent minimiser may legitimately differ only where the objective is flat to rounding
-            # noise: the log-likelihood at both minimisers must then agree (checked just above).
-            d = np.abs(eng["varfreq"][m, k] - ora["varfreq"][m, k])
-            flat_div += int((d > FREQ_ATOL).sum())
+            # A Brent minimiser may differ where the objective is flat to rounding noise (e.g. a
+            # configuration whose two alleles no read supports: every family term is the same constant
+            # times (f+g)^4).  Such a divergence is recognised by the likelihoods at both minimisers
+            # agreeing to FLAT_RTOL; any other divergence is bounded in number.
+            d = np.abs(eng["varfreq"][m, k] - ora["varfreq"][m, k]) > FREQ_ATOL
+            flat = rel <= FLAT_RTOL
+            flat_div += int((d & flat).sum())
+            nonflat_div += int((d & ~flat).sum())
             runs += int(m.sum())
     for f, tol in [("var_post_prob", 1e-9), ("poly_qual", QUAL_ATOL)]:
         d = np.abs(eng[f][called] - ora[f][called])
         if (d > tol).any():
             problems.append(f"{label}{f} max abs err {d.max():.3g}")
-    if flat_div > max(2, 1e-3 * runs):
-        problems.append(f"{label}{flat_div} flat-objective minimiser divergences in {runs} Brent runs (bound 1e-3)")
+    if nonflat_div > max(2, 1e-3 * runs):
+        problems.append(f"{label}{nonflat_div} minimiser divergences on non-flat objectives in {runs} Brent runs "
+                        f"(bound 1e-3)")
     em = ora["emit"] != 0
     for f, tol in [("af", FREQ_ATOL), ("ab", 1e-9), ("denovo_lr", QUAL_ATOL)]:
         d = np.abs(eng[f][em] - ora[f][em])
@@ -60,4 +66,4 @@ def compare_results(eng, ora, ecalls, ocalls, label=""):
     eval_mismatch = int(((eng["evals"] != ora["evals"]) & called[:, None]).any(axis=1).sum())
     assert not problems, "\n".join(problems)
     return {"sites": len(eng), "called": int(called.sum()), "emitted": int(em.sum()), "eval_path_mismatch": eval_mismatch,
-            "flat_divergence": flat_div, "brent_runs": runs}
+            "flat_divergence": flat_div, "nonflat_divergence": nonflat_div, "brent_runs": runs}

@@ -52,7 +52,7 @@ def test_oracle_matches_reference_dump(built, tmp_path, name):
     st = compare_to_dump(res, golden_dump(name), label=name + " ")
     assert st["sites"] == case["dumped_sites"]
     # same Brent in the same arithmetic order: identical evaluation counts and minimisers
-    assert st["eval_path_mismatch"] == 0 and st["flat_divergence"] == 0, st
+    assert st["eval_path_mismatch"] == 0 and st["flat_divergence"] == 0 and st["nonflat_divergence"] == 0, st
 
 
 @pytest.mark.parametrize("name", sorted(CASES))

@@ -46,6 +46,7 @@ def _run_both(ped, params, sections, batch=4096, chrom_of=lambda lab: pm.PM_CHR_
     return stats
 
 
+@pytest.mark.parametrize("numerics", [pm.NUM_PRODUCT, pm.NUM_EXACT, pm.NUM_POLY])
 @pytest.mark.parametrize("pedfile,kw", [
     ("test.ped", dict()),
     ("test.ped", dict(min_total_depth=150, max_total_depth=200, posterior=0.9)),
@@ -53,10 +54,10 @@ def _run_both(ped, params, sections, batch=4096, chrom_of=lambda lab: pm.PM_CHR_
     ("test.ped", dict(denovo=1, denovo_mut_rate=1.5e-7)),
     ("test.ped", dict(all_sites=1)),
 ])
-def test_example_sites_match_oracle(built, pedfile, kw):
+def test_example_sites_match_oracle(built, pedfile, kw, numerics):
     ped = pm.Pedigree(os.path.join(EXAMPLE, "test.dat"), os.path.join(EXAMPLE, pedfile))
     secs = _read_all(ped, EXAMPLE)
-    stats = _run_both(ped, pm.Params.defaults(**kw), secs)
+    stats = _run_both(ped, pm.Params.defaults(numerics=numerics, **kw), secs)
     assert sum(s["sites"] for s in stats) == 81016
 
 
@@ -75,10 +76,11 @@ def _golden_body(name):
     (["-p", "test.ped", "-d", "test.dat", "-g", "test.gif", "--nthreads", "4", "--denovo", "--rate_denovo", "1.5e-07"],
      "test.denovo.out.vcf"),
 ])
-def test_cli_reproduces_reference_goldens(built, tmp_path, args, golden):
+@pytest.mark.parametrize("numerics", ["product", "exact", "poly"])
+def test_cli_reproduces_reference_goldens(built, tmp_path, args, golden, numerics):
     out = tmp_path / "out.vcf"
-    r = subprocess.run([pm.BIN_PATH] + args + ["--out_vcf", str(out)], cwd=EXAMPLE, capture_output=True, text=True,
-                       timeout=300)
+    r = subprocess.run([pm.BIN_PATH] + args + ["--out_vcf", str(out), "--numerics", numerics], cwd=EXAMPLE,
+                       capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     got = [l for l in out.read_text().splitlines() if not l.startswith("##")]
     exp = _golden_body(golden)

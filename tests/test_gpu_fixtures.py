@@ -16,12 +16,12 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("name", sorted(CASES))
-@pytest.mark.parametrize("exact_log10", [0, 1])
-def test_engine_matches_reference_dump(built, tmp_path, name, exact_log10):
+@pytest.mark.parametrize("numerics", [pm.NUM_PRODUCT, pm.NUM_EXACT, pm.NUM_POLY])
+def test_engine_matches_reference_dump(built, tmp_path, name, numerics):
     case = make_dataset(name, str(tmp_path))
     ped, secs, sha = read_dataset(str(tmp_path))
     assert sha == case["block_sha256"]
-    par, chrom = params_and_chrom(case["flags"], exact_log10=exact_log10)
+    par, chrom = params_and_chrom(case["flags"], numerics=numerics)
     (label, pos, ref, pl, dm), = secs
     eng = pm.Engine(ped.view, par, max_batch=128)
     ora = Oracle(ped.view, par)
@@ -41,10 +41,11 @@ def test_engine_matches_reference_dump(built, tmp_path, name, exact_log10):
 
 
 @pytest.mark.parametrize("name", sorted(CASES))
-def test_cli_matches_reference_vcf(built, tmp_path, name):
+@pytest.mark.parametrize("numerics", ["product", "poly"])
+def test_cli_matches_reference_vcf(built, tmp_path, name, numerics):
     case = make_dataset(name, str(tmp_path))
-    r = subprocess.run([pm.BIN_PATH, "-p", "test.ped", "-d", "test.dat", "-g", "test.gif", "--out_vcf", "out.vcf"]
-                       + case["flags"], cwd=tmp_path, capture_output=True, text=True, timeout=600)
+    r = subprocess.run([pm.BIN_PATH, "-p", "test.ped", "-d", "test.dat", "-g", "test.gif", "--out_vcf", "out.vcf",
+                        "--numerics", numerics] + case["flags"], cwd=tmp_path, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:]
     exp = [l for l in golden_vcf_body(name) if l]
     p = tmp_path / "out.vcf"

@@ -14,8 +14,8 @@ B = 32768
 ped = bench.quad_pedigree(pm, nfam, 2)
 for v in variants:
     os.environ["PM_BRENT_TS"] = v
-    for exact in (0, 1):
-        eng = pm.Engine(ped, pm.Params.defaults(exact_log10=exact), max_batch=B)
+    for exact in [int(x) for x in os.environ.get("PM_SWEEP_NUMERICS", "0,2").split(",")]:
+        eng = pm.Engine(ped, pm.Params.defaults(numerics=exact), max_batch=B)
         d_pl, d_dm, d_ref = eng.alloc(B * ped.n_person * 10), eng.alloc(B * ped.n_person * 4), eng.alloc(B)
         eng.synth(B, 7, 0, d_pl, d_dm, d_ref)
         eng.run_device(B, d_pl, d_dm, d_ref); eng.sync()
@@ -26,7 +26,7 @@ for v in variants:
             eng.sync()
         dt = time.perf_counter() - t0
         ks = eng.kernel_stats()
-        print(f"T,S={v:8s} exact_log10={exact}  brent {ks.kernel_ms/4:8.3f} ms/step  total {dt/4*1e3:8.3f} ms/step  "
+        print(f"T,S={v:8s} numerics={exact}  brent {ks.kernel_ms/4:8.3f} ms/step  total {dt/4*1e3:8.3f} ms/step  "
               f"sites/s {4*B/dt:12.0f}  evals/item {ks.evals/max(1,ks.items):.2f}", flush=True)
         for p in (d_pl, d_dm, d_ref):
             eng.free(p)
