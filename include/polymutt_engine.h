@@ -66,8 +66,10 @@ typedef struct {
   const int8_t  *is_founder;   /* [n_person] Person::isFounder()                                 */
   const int32_t *father;       /* [n_person] person index of the father, -1 for founders          */
   const int32_t *mother;       /* [n_person] person index of the mother, -1 for founders          */
-  const int32_t *peel_start;   /* [n_fam+1] offsets into steps (empty range for non-extended)    */
-  const pm_peel_step *steps;   /* ES_Peeling::BuildPeelingOrder output, per extended family      */
+  const int32_t *peel_start;   /* [n_fam+1] offsets into steps (empty range for founders-only)    */
+  const pm_peel_step *steps;   /* ES_Peeling::BuildPeelingOrder output for every family with
+                                  offspring (FamilyLikelihoodSeq.cpp:14-35); nuclear families need
+                                  theirs only in vcf_mode (chrX/Y/MT or a single family)          */
   int32_t n_founders;          /* PedigreeGLF::nFounders   (sum of Family::founders)             */
   int32_t male_founders;       /* PedigreeGLF::maleFounders                                      */
   int32_t female_founders;     /* PedigreeGLF::femaleFounders                                    */
@@ -91,6 +93,9 @@ typedef struct {
   int32_t all_sites;           /* --all_sites */
   int32_t quick_call;          /* --quick_call */
   int32_t numerics;            /* pm_numerics: how the engine evaluates the Brent objective */
+  int32_t vcf_mode;            /* --in_vcf: FamilyLikelihoodSeq_VCF semantics (PedVCF.cpp:43-164) -- one (ref, alt)
+                                  Brent per site, ref[i] = refAllele | altAllele << 4, PL->lk table pow(10,-i/10),
+                                  no filters; res.varllk[0] = mono, varllk[1] = poly (no priors), af = minimiser */
 } pm_params;
 
 /* Objective-evaluation numerics.  All three compute CalcAllFamLogLikelihood; they differ in rounding only.

@@ -45,6 +45,7 @@ struct pmo_ctx {
   int denovo;                  /* par->denovo as currently seen by the objective (main.cpp:569-572 toggles it) */
   int unrelated;               /* --quick_call MakeUnrelated() in effect (FamilyLikelihoodSeq.cpp:54-59) */
   int any_postprob;            /* famlk[0].CalcPostProb has run at least once (sets the stale sex) */
+  int vcf_objective;           /* Brent objective is FamilyLikelihoodSeq_VCF::f (vcf_mode) */
   const uint8_t *pl;           /* current site */
   const uint32_t *dm;
   int refBase;
@@ -82,6 +83,8 @@ static void set_alleles(const pmo_ctx *c, lkobj *o, int a1, int a2) {
 /* ---------------- mutation model / transmission tables ---------------- */
 static void build_tables(pmo_ctx *c) {
   for (int i = 0; i <= 255; i++) c->lktab[i] = pow(0.1, i * 0.1);   /* core/BaseQualityHelper.cpp:12-13 */
+  if (c->par.vcf_mode)   /* FamilyLikelihoodSeq_VCF::PL2LK_table, src/FamilyLikelihoodSeq_VCF.cpp:21-22 (PL > 255 clamps, :57-63) */
+    for (int i = 0; i <= 255; i++) c->lktab[i] = pow(10, -(double)i / 10.0);
   /* AlleleMutationModel::SetAlleleMutMatrix, src/MutationModel.cpp:15-30 */
   double mu = c->par.denovo_mut_rate, tstv = c->par.denovo_tstv, A[4][4];
   for (int i = 0; i < 4; i++) for (int j = 0; j < 4; j++) A[i][j] = (i == j) ? 1 - mu : (1 - mu) / 3;
@@ -422,7 +425,11 @@ static double all_fam_loglik(pmo_ctx *c, lkobj *o, double freq) {
   return loglk;
 }
 
-static double objf(pmo_ctx *c, lkobj *o, double x) { o->evals++; return -all_fam_loglik(c, o, x); }  /* :39-42 */
+static double vcf_all_fam_loglik(pmo_ctx *c, lkobj *o, double freq);
+static double objf(pmo_ctx *c, lkobj *o, double x) {   /* :39-42; FamilyLikelihoodSeq_VCF.cpp:31-34 */
+  o->evals++;
+  return c->vcf_objective ? -vcf_all_fam_loglik(c, o, x) : -all_fam_loglik(c, o, x);
+}
 
 /* OptimizeFrequency (NucFamGenotypeLikelihood.cpp:432-444) + ScalarMinimizer::Brent (core/MathGold.cpp:81-177) */
 static int optimize(pmo_ctx *c, lkobj *o) {
@@ -776,6 +783,83 @@ static void fill_calls(pmo_ctx *c, pm_geno_call *calls) {
   }
 }
 
+/* ---------------- --in_vcf path (FamilyLikelihoodSeq_VCF, PedVCF) ---------------- */
+/* Family kinds as FamilyLikelihoodSeq_VCF::CalcAllFamLogLikelihood / CalcPostProb route them
+ * (src/FamilyLikelihoodSeq_VCF.cpp:93-109, :142-154): all-founder, nuclear closed form (only for
+ * nFam > 1 on autosomes), everything else Elston-Stewart BA peeling. */
+static int vcf_closed_form(const pmo_ctx *c, int f) {
+  return c->fam_kind[f] == PM_FAM_NUCLEAR && c->ped.n_fam > 1 && !c->isX && !c->isY && !c->isMT;
+}
+
+/* FamilyLikelihoodSeq_VCF::CalcAllFamLogLikelihood (:93-109) incl. CalcSingleFamLogLikelihood_Founders (:111-119) */
+static double vcf_all_fam_loglik(pmo_ctx *c, lkobj *o, double freq) {
+  double loglk = 0.0;
+  for (int f = 0; f < c->ped.n_fam; f++) {
+    const int p0 = c->fam_start[f], n = fam_count(c, f);
+    if (n == c->fam_founders[f]) {
+      double llk = 0.0;
+      for (int j = 0; j < n; j++) llk += log10(single_person(c, o, p0 + j, freq));
+      loglk += llk;
+    } else if (vcf_closed_form(c, f)) {
+      parent_marginal(c, o, f, freq, 0);   /* lkSingleFam :527-535; SetParentPrior since nFam > 1 */
+      double sum = 0.0;
+      for (int k = 0; k < 9; k++) sum += c->parentMarginal[k];
+      loglk += log10(sum);
+    } else {
+      loglk += log10(es_likelihood(c, o, f, freq, 3, -1, -1));   /* CalcSingleFamLogLikelihood_BA */
+    }
+  }
+  return loglk;
+}
+
+/* OptimizeFrequency + Brent over f = -CalcAllFamLogLikelihood (FamilyLikelihoodSeq_VCF::f :31-34) */
+static int vcf_optimize(pmo_ctx *c, lkobj *o) {
+  c->vcf_objective = 1;
+  int rc = optimize(c, o);
+  c->vcf_objective = 0;
+  return rc;
+}
+
+/* FamilyLikelihoodSeq_VCF::CalcPostProb (:140-156) */
+static void vcf_calc_post_prob(pmo_ctx *c, lkobj *o, double freq) {
+  for (int f = 0; f < c->ped.n_fam; f++) {
+    const int p0 = c->fam_start[f], n = fam_count(c, f);
+    if (n == c->fam_founders[f]) {   /* CalcPostProb_SingleFam_BA_Founders_VCF :158-165 */
+      for (int j = 0; j < n; j++) { o->sex = c->sex[p0 + j]; post_single_person(c, o, p0 + j, freq); }
+    } else if (vcf_closed_form(c, f)) {
+      post_nuc(c, o, f, freq, 0);    /* CalcPostProb_SingleNucFam :656-735 (same arithmetic as the GLF path) */
+    } else {
+      post_ext(c, o, f, freq, 0);    /* CalcPostProb_SingleExtendedPed_BA_VCF :207-262 */
+    }
+  }
+}
+
+/* One biallelic record with data of PedVCF::VarCallFromVCF (src/PedVCF.cpp:118-162): mono, one Brent,
+ * posteriors at the minimiser.  QUAL/AF/AC/DP formatting stays with the caller (host). */
+static int vcf_site(pmo_ctx *c, const uint8_t *pl, int32_t ref_alt, pm_site_result *R, pm_geno_call *calls) {
+  const int a1 = ref_alt & 15, a2 = (ref_alt >> 4) & 15;
+  if (a1 < 1 || a1 > 4 || a2 < 1 || a2 > 4 || a1 == a2) { R->status = PM_SITE_BAD_REF; return 0; }
+  R->status = PM_SITE_CALLED;
+  /* MonomorphismLogLikelihood (:74-83): loglk[homref] = -min(PL,255)/10, summed in family/person order */
+  double mono = 0.0; const int h = GI(a1, a1);
+  for (int p = 0; p < c->ped.n_person; p++) mono += -(double)(pl[p * 10 + h]) / 10;
+  lkobj *o = &c->lk[1];
+  o->evals = 0;
+  set_alleles(c, o, a1, a2);
+  if (vcf_optimize(c, o) != 0) return PM_EBRENT;
+  R->n_cfg = 2; R->maxidx = 1;
+  R->varllk[0] = mono; R->varllk[1] = -o->fmin;
+  R->varfreq[0] = 1.0; R->varfreq[1] = o->min;
+  R->evals[1] = (int32_t)o->evals;
+  R->allele1 = a1; R->allele2 = a2; R->af = o->min; R->ab = 0.5; R->denovo_lr = -1;
+  lkobj *o0 = &c->lk[0];
+  set_alleles(c, o0, a1, a2);
+  vcf_calc_post_prob(c, o0, o->min);
+  R->emit = 1; R->call_row = 0;
+  fill_calls(c, calls);
+  return 0;
+}
+
 /* ---------------- public API ---------------- */
 pmo_ctx *pmo_create(const pm_pedigree *ped, const pm_params *par) {
   pmo_ctx *c = (pmo_ctx *)calloc(1, sizeof(pmo_ctx));
@@ -843,8 +927,9 @@ double pmo_poly_loglik(pmo_ctx *c, const uint8_t *pl, int32_t a1, int32_t a2, in
 int pmo_site(pmo_ctx *c, const uint8_t *pl, const uint32_t *dm, int32_t refBase, pm_site_result *R, pm_geno_call *calls) {
   memset(R, 0, sizeof(*R));
   R->maxidx = -2; R->call_row = -1;
-  c->pl = pl; c->dm = dm; c->refBase = refBase;
+  c->pl = pl; c->dm = dm; c->refBase = refBase & 15;
   g_brent_err = 0;
+  if (c->par.vcf_mode) return vcf_site(c, pl, refBase, R, calls);
   if (refBase < 1 || refBase > 4) { R->status = PM_SITE_BAD_REF; return 0; }
   c->cnt.ref_base_counts[refBase]++;
   /* CalcReadStats, NucFamGenotypeLikelihood.cpp:520-546 */

@@ -39,14 +39,14 @@ class Params(C.Structure):
     _fields_ = [("theta", f64), ("poly_tstv", f64), ("precision", f64), ("posterior", f64),
                 ("min_total_depth", i32), ("max_total_depth", i32), ("min_ps", f64), ("min_map_quality", i32),
                 ("denovo", i32), ("denovo_mut_rate", f64), ("denovo_tstv", f64), ("denovo_min_llr", f64),
-                ("force_call", i32), ("all_sites", i32), ("quick_call", i32), ("numerics", i32)]
+                ("force_call", i32), ("all_sites", i32), ("quick_call", i32), ("numerics", i32), ("vcf_mode", i32)]
 
     @classmethod
     def defaults(cls, **kw):
         """Defaults of src/main.cpp:59-85."""
         p = cls(theta=0.001, poly_tstv=2.0, precision=0.0001, posterior=0.5, min_total_depth=0, max_total_depth=0,
                 min_ps=0.0, min_map_quality=0, denovo=0, denovo_mut_rate=1.5e-8, denovo_tstv=2.0,
-                denovo_min_llr=0.01, force_call=0, all_sites=0, quick_call=0, numerics=NUM_POLY)
+                denovo_min_llr=0.01, force_call=0, all_sites=0, quick_call=0, numerics=NUM_POLY, vcf_mode=0)
         for k, v in kw.items():
             setattr(p, k, v)
         return p

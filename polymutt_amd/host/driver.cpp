@@ -6,6 +6,7 @@
 #include <ctime>
 #include "glf.h"
 #include "vcf.h"
+#include "vcf_input.h"
 
 namespace pmhost {
 
@@ -15,7 +16,8 @@ pm_params Options::params() const {
   p.theta = theta; p.poly_tstv = tstv; p.precision = precision; p.posterior = posterior;
   p.min_total_depth = minTotalDepth; p.max_total_depth = maxTotalDepth; p.min_ps = minPS; p.min_map_quality = minMapQuality;
   p.denovo = denovo; p.denovo_mut_rate = denovo_rate; p.denovo_tstv = denovo_tstv; p.denovo_min_llr = denovo_llr;
-  p.force_call = force_call; p.all_sites = all_sites; p.quick_call = quick_call; p.numerics = exact_log10 ? PM_NUM_EXACT : numerics == "exact" ? PM_NUM_EXACT : numerics == "poly" ? PM_NUM_POLY : PM_NUM_PRODUCT;
+  p.force_call = force_call; p.all_sites = all_sites; p.quick_call = quick_call; p.vcf_mode = vcfInFile.empty() ? 0 : 1;
+  p.numerics = exact_log10 ? PM_NUM_EXACT : numerics == "exact" ? PM_NUM_EXACT : numerics == "poly" ? PM_NUM_POLY : PM_NUM_PRODUCT;
   return p;
 }
 
@@ -129,7 +131,7 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval) {
   if (opt.pedFile.empty()) throw FatalError("pedFile not provided for input!\n");
   if (opt.glfListFile.empty() && opt.vcfInFile.empty()) throw FatalError("glfListFile or input VCF file not provided for input!\n");
   if (opt.vcfOutFile.empty()) throw FatalError("vcfOutFile not provided for output!\n");
-  if (!opt.vcfInFile.empty()) throw FatalError("--in_vcf is not supported by this build yet\n");
+  if (!opt.vcfInFile.empty()) return run_polymutt_vcf(opt, ped, eval);   // main.cpp:238-246
   if (opt.denovo && opt.denovo_llr < 0) throw FatalError("denovo_min_LLR can only be greater than 0 !\n");
 
   std::map<std::string, int> positionMap;

@@ -274,7 +274,7 @@ void Pedigree::flatten() {
       father.push_back(p.founder() ? -1 : fam_start.back() + persons[p.father].traverse);
       mother.push_back(p.founder() ? -1 : fam_start.back() + persons[p.mother].traverse);
     }
-    if (kind == PM_FAM_EXTENDED) {
+    if (kind != PM_FAM_FOUNDERS) {   // every family with offspring gets a schedule (FamilyLikelihoodSeq.cpp:32)
       F.peel = build_peeling_order(F.count, lsex, lpar, F.famid, lpid);
       steps.insert(steps.end(), F.peel.begin(), F.peel.end());
     }

@@ -31,7 +31,7 @@ struct Family {
   int first = 0, count = 0, founders = 0, generations = 1;
   std::vector<int> path;       // person indices (global), founders first
   bool isNuclear() const { return generations == 2 && founders == 2; }
-  std::vector<pm_peel_step> peel;   // only for extended families
+  std::vector<pm_peel_step> peel;   // every family with offspring (nuclear ones too)
 };
 
 class Pedigree {

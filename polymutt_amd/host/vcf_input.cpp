@@ -1,0 +1,347 @@
+// vcf_input.cpp -- see vcf_input.h.  Restates PedVCF::VarCallFromVCF (src/PedVCF.cpp:43-164) and the
+// record handling of FamilyLikelihoodSeq_VCF (FillPenetrance :259-370, OutputVCF :412-521) with the
+// libVcf field semantics they rely on (VCFRecord::getFormatIndex prefix match, VCFIndividual::get:
+// a field is missing when absent or empty).  The likelihood work runs on the SiteEvaluator in vcf_mode.
+#include "vcf_input.h"
+#include <zlib.h>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+namespace pmhost {
+namespace {
+
+struct LineReader {   // plain or gzip text, lines of any length
+  gzFile fh = nullptr;
+  std::vector<char> buf = std::vector<char>(1 << 20);
+  ~LineReader() { if (fh) gzclose(fh); }
+  bool open(const std::string& p) {
+    fh = gzopen(p.c_str(), "rb");
+    if (fh) gzbuffer(fh, 1 << 20);
+    return fh != nullptr;
+  }
+  bool next(std::string& line) {
+    line.clear();
+    for (;;) {
+      if (!gzgets(fh, buf.data(), (int)buf.size())) return !line.empty();
+      size_t n = strlen(buf.data());
+      line.append(buf.data(), n);
+      if (n && buf[n - 1] == '\n') {
+        line.pop_back();
+        if (!line.empty() && line.back() == '\r') line.pop_back();
+        return true;
+      }
+    }
+  }
+};
+
+struct Span { int b = 0, e = 0; };
+
+void split(const std::string& s, char sep, std::vector<Span>& out) {
+  out.clear();
+  int b = 0;
+  const int n = (int)s.size();
+  for (int i = 0; i <= n; i++)
+    if (i == n || s[i] == sep) { out.push_back({b, i}); b = i + 1; }
+}
+
+// VCFRecord::getFormatIndex (libVcf/VCFRecord.h:283-308): first ':'-field that starts with `key`.
+int format_index(const std::string& line, Span fmt, const char* key) {
+  int b = fmt.b, idx = 0;
+  const int e = fmt.e, kl = (int)strlen(key);
+  while (b < e) {
+    if (b + kl <= (int)line.size() && line.compare(b, kl, key) == 0) return idx;
+    idx++;
+    while (line[b++] != ':')
+      if (b >= e) return -1;
+  }
+  return -1;
+}
+
+// VCFIndividual::get (libVcf/VCFIndividual.h:74-81): i-th ':' field; missing if absent or empty.
+bool get_field(const std::string& line, Span col, int i, Span& out) {
+  if (i < 0) return true;
+  int b = col.b, k = 0;
+  for (int p = col.b; p <= col.e; p++)
+    if (p == col.e || line[p] == ':') {
+      if (k == i) { out = {b, p}; return b == p; }
+      k++;
+      b = p + 1;
+    }
+  return true;
+}
+
+int allele2int(const std::string& a) {   // FamilyLikelihoodSeq_VCF::Allele2Int (:65-72)
+  if (a == "A" || a == "a") return 1;
+  if (a == "C" || a == "c") return 2;
+  if (a == "G" || a == "g") return 3;
+  if (a == "T" || a == "t") return 4;
+  return 0;
+}
+
+int gi(int b1, int b2) { return b1 < b2 ? (b1 - 1) * (10 - b1) / 2 + (b2 - b1) : (b2 - 1) * (10 - b2) / 2 + (b1 - b2); }
+bool is_ts(int a1, int a2) { return (a1 == 1 && a2 == 3) || (a1 == 2 && a2 == 4); }   // PedVCF::isTs (:25-28)
+
+struct Pending {          // one record awaiting output, in file order
+  std::string line;
+  std::vector<Span> cols;
+  bool computed = false;
+  int slot = -1;
+  int a1 = 0, a2 = 0;
+  bool indel = false;
+};
+
+struct State {            // what FamilyLikelihoodSeq_VCF holds between records (stale output, :412-521)
+  double qual = 0.0, min = 0.0;
+  std::vector<pm_geno_call> calls;   // per flattened person
+  int a_ref = 0;                     // allele of the label convention (always allele1 in this path)
+};
+
+std::string label_text(const pm_geno_call& c) {   // GetBestGenoLabel_vcfv4 (NucFamGenotypeLikelihood.cpp:1590-1608)
+  static const char* dip[3] = {"0/0", "0/1", "1/1"};
+  static const char* hap[3] = {"0", "ERROR", "1"};
+  if (c.label == PM_LBL_DOT) return ".";
+  const int b = c.best < 0 || c.best > 2 ? 0 : c.best;
+  return c.label == PM_LBL_VCF_HAPLOID ? hap[b] : dip[b];
+}
+
+}  // namespace
+
+int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eval) {
+  if (opt.vcfInFile == opt.vcfOutFile) throw FatalError("Input and output VCF files are the same!\n");
+  if (opt.vcfOutFile.empty()) throw FatalError("vcfOutFile not provided for output!\n");
+  LineReader in;
+  if (!in.open(opt.vcfInFile)) throw FatalError("Cannot open VCF file " + opt.vcfInFile + "\n");
+
+  const pm_pedigree pv = ped.view();
+  const int np = pv.n_person;
+  // pid -> flattened person (FamilyLikelihoodSeq_VCF::MapPID2Traverse :36-55, later families win)
+  std::map<std::string, int> pid2person;
+  for (int p = 0; p < np; p++) pid2person[ped.column_pid[p]] = p;
+
+  std::string line;
+  std::vector<Span> cols;
+  std::vector<std::string> samples;
+  while (in.next(line)) {
+    if (line.compare(0, 2, "##") == 0) continue;
+    if (line.compare(0, 1, "#") == 0) {
+      split(line, '\t', cols);
+      for (size_t i = 9; i < cols.size(); i++) samples.push_back(line.substr(cols[i].b, cols[i].e - cols[i].b));
+      break;
+    }
+  }
+  // included samples in VCF order (PedVCF.cpp:66-80); person index per VCF column (-1: not in the ped)
+  std::vector<int> col_person(samples.size(), -1);
+  std::vector<std::string> included;
+  for (size_t i = 0; i < samples.size(); i++) {
+    auto it = pid2person.find(samples[i]);
+    if (it != pid2person.end()) { col_person[i] = it->second; included.push_back(samples[i]); }
+  }
+
+  FILE* out = fopen(opt.vcfOutFile.c_str(), "w");
+  if (!out) throw FatalError("Open outpuf VCF file " + opt.vcfOutFile + " failed!\n");
+  std::string header = "#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT";
+  for (auto& s : included) header += "\t" + s;
+  fprintf(out, "##fileformat=VCFv4.1\n##Polymutt=%s\n", opt.cmd.c_str());
+  fprintf(out, "%s",
+          "##Note=VCF file modified by polymutt. Updated fileds include: QUAL, GT and GQ, AF and AC. NOTE: modification was "
+          "applied only to biallelic variants\n"
+          "##FILTER=<ID=LOWDP,Description=\"Low Depth filter when the average depth per sample is lessn than 1\">\n"
+          "##INFO=<ID=DP,Number=1,Type=Integer,Description=\"Total Read Depth\">\n"
+          "##INFO=<ID=AF,Number=A,Type=Float,Description=\"Alternative Allele Frequency\">\n"
+          "##INFO=<ID=AC,Number=1,Type=Integer,Description=\"Alternative Allele Count\">\n"
+          "##FORMAT=<ID=GT,Number=1,Type=String,Description=\"Genotype\">\n"
+          "##FORMAT=<ID=GQ,Number=1,Type=Integer,Description=\"Genotype Quality\">\n"
+          "##FORMAT=<ID=DP,Number=1,Type=Integer,Description=\"Read Depth\">\n"
+          "##FORMAT=<ID=PL,Number=3,Type=Integer,Description=\"Phred-scaled Genotype Likelihoods\">\n"
+          "##FORMAT=<ID=GL,Number=3,Type=Float,Description=\"Log10 Genotype Likelihoods\">\n");
+  fprintf(out, "%s\n", header.c_str());
+
+  // GetPolyPrior() once, before any SetNonAutosomeFlags (PedVCF.cpp:103): autosomal; GetPolyPrior_indel()
+  // returns the same `prior` (NucFamGenotypeLikelihood.cpp:313).  PedVCF's own tstv_ratio is 2.0 (:7).
+  double prior = 0;
+  for (int i = 1; i <= 2 * pv.n_founders; i++) prior += 1.0 / i;
+  prior *= opt.theta;
+  const double tstv = 2.0, prior_ts = tstv / (tstv + 1), prior_tv = 0.5 / (tstv + 1);
+
+  const int B = std::max(1, opt.batch);
+  std::vector<uint8_t> pl((size_t)B * np * 10), ref(B);
+  std::vector<uint32_t> dm((size_t)B * np, 0);
+  std::vector<pm_site_result> res(B);
+  std::vector<pm_geno_call> calls((size_t)B * np);
+  std::vector<Pending> pend;
+  int nb = 0, cur_chrom = -1, GL_idx = -1, PL_idx = -1, DP_index = -1, n_samples_with_data = 0, bad_allele = 0;
+  bool first = true;
+  State st;
+  st.calls.assign(np, pm_geno_call{0.0, 0, 0, PM_LBL_VCF_DIPLOID, {0, 0, 0}});
+
+  auto write_record = [&](const Pending& r, bool fresh, const pm_site_result* R, const pm_geno_call* C) {
+    if (fresh) {   // mono/poly -> QUAL (PedVCF.cpp:136-152), with the reference's operator-precedence slip
+      const double mono = R->varllk[0], poly = R->varllk[1];
+      double llk_alt, llk_ref;
+      if (!r.indel) {
+        llk_alt = log10((prior * (is_ts(r.a1, r.a2) ? 1 : 0)) ? prior_ts : prior_tv) + poly;
+        llk_ref = log10(1 - prior) + mono;
+      } else {
+        llk_alt = log10(prior) + poly;
+        llk_ref = log10(1 - prior) + mono;
+      }
+      if (llk_alt - llk_ref > 10) st.qual = 10.0 * (llk_alt - llk_ref);
+      else {
+        const double posterior = 1 / (1 + pow(10, llk_ref - llk_alt));
+        st.qual = -10 * log10(1 - posterior);
+      }
+      st.min = R->af;
+      for (int p = 0; p < np; p++) st.calls[p] = C[p];
+    }
+    // OutputVCF (FamilyLikelihoodSeq_VCF.cpp:412-521)
+    const std::string& L = r.line;
+    int AC = 0, totalDepth = 0;
+    bool missing = false;
+    Span f;
+    for (size_t i = 0; i < samples.size(); i++) {
+      if (col_person[i] < 0) continue;
+      AC += st.calls[col_person[i]].best;
+      int dp = 0;
+      if (DP_index > 0) {
+        missing = get_field(L, r.cols[9 + i], DP_index, f);
+        dp = missing ? 0 : atoi(L.c_str() + f.b);
+      }
+      if (missing) continue;
+      totalDepth += dp;
+    }
+    auto fld = [&](int k) { return L.substr(r.cols[k].b, r.cols[k].e - r.cols[k].b); };
+    fprintf(out, "%s\t%s\t%s\t%s\t%s\t%.2f\t%s\tAF=%.2f;AC=%d;DP=%d\t%s", fld(0).c_str(), fld(1).c_str(), fld(2).c_str(),
+            fld(3).c_str(), fld(4).c_str(), st.qual, fld(6).c_str(), 1 - st.min, AC, totalDepth,
+            PL_idx > 0 ? "GT:GQ:DP:PL" : "GT:GQ:DP:GL");
+    for (size_t i = 0; i < samples.size(); i++) {
+      const int p = col_person[i];
+      if (p < 0) continue;
+      const pm_geno_call& c = st.calls[p];
+      const std::string lab = label_text(c);
+      fprintf(out, "\t%s:%d:", (c.gq > 0 || lab == ".") ? lab.c_str() : "./.", (int)c.gq);
+      std::string dps = ".";
+      if (DP_index > 0) {
+        missing = get_field(L, r.cols[9 + i], DP_index, f);
+        if (!missing) dps = L.substr(f.b, f.e - f.b);
+      }
+      fprintf(out, "%s:", missing ? "." : dps.c_str());
+      missing = get_field(L, r.cols[9 + i], PL_idx > 0 ? PL_idx : GL_idx, f);
+      fprintf(out, "%s", missing ? "." : L.substr(f.b, f.e - f.b).c_str());
+    }
+    fprintf(out, "\n");
+  };
+
+  auto flush = [&]() {
+    int rows = 0;
+    if (nb > 0) eval.run(nb, pl.data(), dm.data(), ref.data(), res.data(), calls.data(), &rows);
+    for (auto& r : pend) {
+      if (r.computed) write_record(r, true, &res[r.slot], calls.data() + (size_t)res[r.slot].call_row * np);
+      else write_record(r, false, nullptr, nullptr);
+    }
+    pend.clear();
+    nb = 0;
+  };
+
+  std::string refS, altS;
+  Span f;
+  while (in.next(line)) {
+    if (line.empty() || line[0] == '#') continue;
+    Pending r;
+    r.line.swap(line);
+    split(r.line, '\t', r.cols);
+    if (r.cols.size() < 9) throw FatalError("Malformed VCF record (fewer than 9 columns)\n");
+    const std::string& L = r.line;
+    auto fld = [&](int k) { return L.substr(r.cols[k].b, r.cols[k].e - r.cols[k].b); };
+    if (first) {   // FillPenetrance on the first record (:270-282), then VarCallFromVCF's banner (:117)
+      for (size_t i = 0; i < samples.size(); i++) {
+        if (col_person[i] < 0) { printf("Sample ID \"%s\" not included in the analysis!\n", samples[i].c_str()); continue; }
+        n_samples_with_data++;
+      }
+    }
+    refS = fld(3); altS = fld(4);
+    bool biallelic = refS != altS && altS.find(',') == std::string::npos;
+    if (biallelic) {
+      r.indel = refS.size() > 1 || altS.size() > 1;
+      r.a1 = r.indel ? 1 : allele2int(refS);
+      r.a2 = r.indel ? 2 : allele2int(altS);
+      if (DP_index < 0) DP_index = format_index(L, r.cols[8], "DP");
+      if (GL_idx < 0 && PL_idx < 0) {
+        GL_idx = format_index(L, r.cols[8], "GL");
+        PL_idx = format_index(L, r.cols[8], "PL");
+        if (GL_idx < 0 && PL_idx < 0) {
+          fprintf(stderr, "NO GL or PL field was found. Please check the vcf file at chr:%s and position:%d", fld(0).c_str(),
+                  atoi(fld(1).c_str()));
+          exit(1);
+        }
+        if (included.empty()) throw FatalError("NO individual IDs match in the ped and vcf file!\n");
+      }
+      // non-ACGT single-base alleles index the genotype tables out of range in the reference (undefined
+      // behaviour); a case-only REF/ALT difference gives a degenerate pair: both are skipped here
+      if (r.a1 == 0 || r.a2 == 0 || r.a1 == r.a2) { bad_allele++; biallelic = false; }
+    }
+    if (first) { printf("Total samples in both VCF and PED files: %d\n\n", n_samples_with_data); first = false; }
+    if (!biallelic) continue;   // OutputVCF returns at once for these records (:419)
+
+    // penetrances / log-likelihoods of the record (:318-366) into a dense block row
+    const int slot = nb;
+    uint8_t* row = pl.data() + (size_t)slot * np * 10;
+    memset(row, 0, (size_t)np * 10);
+    const int g0 = gi(r.a1, r.a1), g1 = gi(r.a1, r.a2), g2 = gi(r.a2, r.a2);
+    int withdata = 0;
+    for (size_t i = 0; i < samples.size(); i++) {
+      const int p = col_person[i];
+      if (p < 0) continue;
+      if (get_field(L, r.cols[9 + i], GL_idx > 0 ? GL_idx : PL_idx, f)) break;   // missing: the reference returns (:332-343)
+      double v[3];
+      int nv = 0, b = f.b;
+      for (int q = f.b; q <= f.e; q++)
+        if (q == f.e || L[q] == ',') {
+          if (nv < 3) v[nv] = strtod(std::string(L, b, q - b).c_str(), nullptr);
+          nv++;
+          b = q + 1;
+        }
+      if (nv != 3)
+        throw FatalError("GL or PL filed does not have 3 values separated by commas at: " + fld(0) + " " + fld(1) + "!\n");
+      if (v[0] != 0.0 || v[1] != 0.0 || v[2] != 0.0) withdata++;
+      const int gix[3] = {g0, g1, g2};
+      for (int k = 0; k < 3; k++) {
+        const int phred = (int)(PL_idx > 0 ? v[k] : -10 * v[k]);   // PL2LK(int(...)) (:361-363, :57-63)
+        if (phred < 0) throw FatalError("Phred-scaled likelihood " + std::to_string(phred) + " can not be negative\n");
+        row[(size_t)p * 10 + gix[k]] = (uint8_t)(phred > 255 ? 255 : phred);
+      }
+    }
+    // chromosome class of the record (PedVCF.cpp:121-124)
+    const std::string chrom = fld(0);
+    const int cls = chrom == opt.chrX ? PM_CHR_X : chrom == opt.chrY ? PM_CHR_Y : chrom == opt.MT ? PM_CHR_MT : PM_CHR_AUTO;
+    if (withdata == 0) {   // written with the previous record's QUAL / AF / genotypes (:113)
+      pend.push_back(std::move(r));
+      continue;
+    }
+    if (cls != cur_chrom) {
+      if (nb > 0) {   // the row is already packed in `slot`; move it to slot 0 after the flush
+        std::vector<uint8_t> keep(row, row + (size_t)np * 10);
+        flush();
+        memcpy(pl.data(), keep.data(), keep.size());
+      } else if (!pend.empty()) flush();
+      eval.begin_section(cls);
+      cur_chrom = cls;
+    }
+    r.computed = true;
+    r.slot = nb;
+    ref[nb] = (uint8_t)(r.a1 | (r.a2 << 4));
+    nb++;
+    pend.push_back(std::move(r));
+    if (nb == B) flush();
+  }
+  flush();
+  fclose(out);
+  if (bad_allele) fprintf(stderr, "%d biallelic records with non-ACGT alleles were skipped\n", bad_allele);
+  return 0;
+}
+
+}  // namespace pmhost

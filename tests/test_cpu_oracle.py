@@ -66,3 +66,15 @@ def test_cpu_driver_matches_reference_vcf(cpu_driver, tmp_path, name):
     assert len(got) == len(exp)
     diff = [i for i, (a, b) in enumerate(zip(got, exp)) if a != b]
     assert not diff, f"{len(diff)} lines differ; first:\n{got[diff[0]][:300]}\n{exp[diff[0]][:300]}"
+
+
+def test_cpu_driver_reproduces_vcf_input_golden(cpu_driver, tmp_path):
+    """--in_vcf (PedVCF / FamilyLikelihoodSeq_VCF): example/testvcf.in.vcf -> example/testvcf.out.vcf."""
+    out = tmp_path / "out.vcf"
+    r = subprocess.run([cpu_driver, "-p", "test.ped", "-d", "test.dat", "--in_vcf",
+                        os.path.join(EXAMPLE, "testvcf.in.vcf.gz"), "--out_vcf", str(out)], cwd=EXAMPLE,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:]
+    assert "Total samples in both VCF and PED files: 12" in r.stdout
+    exp = gzip.open(os.path.join(EXAMPLE, "testvcf.out.vcf.body.gz"), "rt").read().splitlines()
+    assert _body(out) == exp
