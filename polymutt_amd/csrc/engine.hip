@@ -94,6 +94,8 @@ struct DevArgs {
   int ws_per_lane;         // doubles per lane (max over ES families of n*ns + couples*ns*ns)
   int unrelated;           // --quick_call MakeUnrelated(): every family is all-founder
   double theta_one;        // 1.0 (opaque to the compiler; timing experiments only)
+  int vcf;                 // vcf_mode: one (ref, alt) Brent per site, FamilyLikelihoodSeq_VCF family rules
+  int nuc_es;              // nuclear families are peeled (vcf_mode plan 1)
   // tables
   const double* lktab;     // [256]
   const double* M;         // [100] genotype mutation matrix
@@ -450,7 +452,8 @@ __device__ __forceinline__ void block_sum3(double& x, double& y, double& z, doub
 
 // per-lane partial of CalcAllFamLogLikelihood(freq) over the lane's units
 template <int S, bool GEN>
-__device__ __forceinline__ double lane_loglik(double f, const int4* unit, const double (*cond)[9], const int* fl, int pmode) {
+__device__ __forceinline__ double lane_loglik(double f, const int4* unit, const double (*cond)[9], const int* fl, int pmode,
+                                              bool log_each = false) {
   double pp[9];
   d_parent_prior(pmode, f, pp);
   const double g = 1 - f;
@@ -473,9 +476,10 @@ __device__ __forceinline__ double lane_loglik(double f, const int4* unit, const 
         double sp = 0.0;
         if (b & 1) sp = sp + cond[s][3 * j] * f + cond[s][3 * j + 1] * 0 + cond[s][3 * j + 2] * g;
         else sp = sp + cond[s][3 * j] * P0 + cond[s][3 * j + 1] * P1 + cond[s][3 * j + 2] * P2;
-        prod *= sp;
+        if (log_each) part += log10(sp);   // VCF path: sum of per-person log10
+        else prod *= sp;
       }
-      if (unit[s].w & UF_LAST) part += log10(prod);
+      if (!log_each && (unit[s].w & UF_LAST)) part += log10(prod);
     }
   }
   return part;
@@ -694,7 +698,8 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
     const int site = item >> 3, cfg = item & 7;
     const int r = A.ref[site];
     ItemCtx I;
-    if (cfg == 7) { I.a1 = A.res[site].allele1; I.a2 = A.res[site].allele2; }
+    if (A.vcf) { I.a1 = r & 15; I.a2 = r >> 4; }
+    else if (cfg == 7) { I.a1 = A.res[site].allele1; I.a2 = A.res[site].allele2; }
     else cfg_alleles(cfg, r, &I.a1, &I.a2);
     I.g11 = d_gi(I.a1, I.a1); I.g12 = d_gi(I.a1, I.a2); I.g22 = d_gi(I.a2, I.a2);
     I.denovo = GEN ? (A.denovo && cfg != 7) : 0;
@@ -731,7 +736,7 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
     }
     double* raw = A.raw + (size_t)site * 8;
     double* wsl = ES ? A.ws + (size_t)blockIdx.x * A.ws_per_lane * T + threadIdx.x : nullptr;
-    const bool single = (cfg == 0) || (A.single_nuclear && !A.unrelated);
+    const bool single = !A.vcf && ((cfg == 0) || (A.single_nuclear && !A.unrelated));
     // One evaluation site for the objective: the three bracketing evaluations of OptimizeFrequency
     // (:432-444) and every Brent step (core/MathGold.cpp:81-177) run through the same loop body.
     const double tol = A.precision;
@@ -775,7 +780,7 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
           }
         tot = block_logprod<T>(m, e, s_red, s_rede, par);
       } else {
-        double part = lane_loglik<S, GEN>(x, unit, (const double(*)[9])cond, fl, pmode);
+        double part = lane_loglik<S, GEN>(x, unit, (const double(*)[9])cond, fl, pmode, A.vcf != 0);
         if (ES && A.ext_count)
           for (int q = 0; q < A.ext_count[threadIdx.x]; q++) {
             const int f = A.ext_fam[q * T + threadIdx.x];
@@ -866,11 +871,12 @@ __global__ void __launch_bounds__(256) k_prep(DevArgs A) {
   const int site = wave;
   bool valid = false;
   if (site < A.n) {
-    const int r = A.ref[site];
+    const int rb = A.ref[site];
+    const int r = A.vcf ? (rb & 15) : rb, alt = rb >> 4;
     const int np = A.n_person;
     const uint8_t* pl = A.pl + (size_t)site * np * 10;
     const uint32_t* dm = A.dm + (size_t)site * np;
-    const bool okref = r >= 1 && r <= 4;
+    const bool okref = r >= 1 && r <= 4 && (!A.vcf || (alt >= 1 && alt <= 4 && alt != r));
     const int h = okref ? d_gi(r, r) : 0;
     long long dsum = 0, mqsum = 0, nsd = 0;
     double mono = 0.0;
@@ -897,8 +903,9 @@ __global__ void __launch_bounds__(256) k_prep(DevArgs A) {
         double avgmq = 0., ps = 0.;
         if (n > 0) { avgmq = (double)mqsum / (double)n; ps = (double)n / (double)np; }
         O.total_depth = td; O.num_samp_with_data = n; O.avg_map_qual = avgmq; O.perc_samp_with_data = ps;
-        int st = 0;   // filters, main.cpp:345-348
-        if (td < A.min_total_depth) st = PM_SITE_MIN_DEPTH;
+        int st = 0;   // filters, main.cpp:345-348 (the VCF path has none)
+        if (A.vcf) st = 0;
+        else if (td < A.min_total_depth) st = PM_SITE_MIN_DEPTH;
         else if (A.max_total_depth > 0 && td > A.max_total_depth) st = PM_SITE_MAX_DEPTH;
         else if (ps * 100 < A.min_ps) st = PM_SITE_MIN_PS;
         else if (avgmq < A.min_map_quality) st = PM_SITE_MIN_MAPQ;
@@ -906,7 +913,10 @@ __global__ void __launch_bounds__(256) k_prep(DevArgs A) {
         else { O.status = PM_SITE_CALLED; valid = true; }
       }
       A.res[site] = O;
-      if (valid && A.unrelated) {   // --quick_call pre-filter first (main.cpp:354-437)
+      if (valid && A.vcf) {   // PedVCF.cpp:131: PolymorphismLogLikelihood(ref, alt), one Brent
+        const int slot = atomicAdd(&A.counts[0], 1);
+        A.items[0][slot] = (site << 3) | 1;
+      } else if (valid && A.unrelated) {   // --quick_call pre-filter first (main.cpp:354-437)
         const int slot = atomicAdd(&A.counts[1], 3);
         for (int k = 0; k < 3; k++) A.items[1][slot + k] = (site << 3) | (k + 1);
       } else if (valid) {
@@ -1071,6 +1081,23 @@ __global__ void __launch_bounds__(256) k_finalize(DevArgs A) {
     // map to pm_counters layout: [9] homo_ref .. [14] tvs1tvs2, [15] nocall
     atomicAdd(&A.counters[threadIdx.x], s_c[threadIdx.x]);
   }
+}
+
+// vcf_mode: one record per called site (PedVCF.cpp:125-162); QUAL/AF/AC formatting is the host's.
+__global__ void k_finalize_vcf(DevArgs A) {
+  const int site = blockIdx.x * blockDim.x + threadIdx.x;
+  if (site >= A.n) return;
+  pm_site_result* R = A.res + site;
+  if (R->status != PM_SITE_CALLED) return;
+  const int rb = A.ref[site];
+  R->n_cfg = 2; R->maxidx = 1;
+  R->varllk[0] = A.mono_plain[site];              // MonomorphismLogLikelihood (:74-83)
+  R->varllk[1] = A.raw[(size_t)site * 8 + 1];     // PolymorphismLogLikelihood (:85-91)
+  R->varfreq[0] = 1.0; R->varfreq[1] = A.minv[site * 8 + 1];
+  R->evals[1] = A.evals[site * 8 + 1];
+  R->allele1 = rb & 15; R->allele2 = rb >> 4;
+  R->af = A.minv[site * 8 + 1];                   // GetMinimizer(): CalcPostProb frequency, AF = 1 - min
+  R->emit = 1;
 }
 
 // member `sex` of famlk[0] before site `site`'s CalcPostProb / re-optimisation (non-de-novo only
@@ -1240,7 +1267,7 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
         }
         continue;
       }
-      if (ES && kind == PM_FAM_EXTENDED) {   // CalcPostProb_SingleExtendedPed_BA :171-216 / _denovo :140-169
+      if (ES && (kind == PM_FAM_EXTENDED || (A.nuc_es && kind == PM_FAM_NUCLEAR))) {   // CalcPostProb_SingleExtendedPed_BA :171-216 / _denovo :140-169
         double* wsl = A.ws + gid_base;
         const size_t st = stride;
         for (int j = 0; j < n; j++) {
@@ -1503,6 +1530,12 @@ struct pm_engine {
   int8_t* d_is_founder = nullptr;
   int2* d_steps = nullptr;
   double *d_T10 = nullptr, *d_T10dn = nullptr, *d_ws = nullptr;
+  // vcf_mode on chrX/Y/MT or with a single family: nuclear families go through ES peeling as well
+  // (FamilyLikelihoodSeq_VCF.cpp:97-103), so a second lane plan with them in the per-lane ES lists
+  bool vcf = false, plan1_ok = false, use_plan1 = false;
+  int T1 = 0, S1 = 0, grid1 = 0, n_ext1 = 0, max_ext1 = 0, has_fp1 = 0;
+  int4* d_units1 = nullptr;
+  int *d_ext_count1 = nullptr, *d_ext_fam1 = nullptr;
   // --quick_call: the MakeUnrelated() plan (every family an all-founder product) with its own geometry
   int Tq = 0, Sq = 0, grid_q = 0;
   int4* d_units_q = nullptr;
@@ -1556,14 +1589,15 @@ static const struct { int T, S; } kVariants[] = {{64, 1}, {64, 2}, {64, 4}, {128
 // kept on one lane.  Returns false if the plan does not fit T x S.
 // Extended families are not units: they go to per-lane lists (plan_ext).  unrelated = the --quick_call
 // MakeUnrelated() view (FamilyLikelihoodSeq.cpp:54-59): every family is an all-founder product.
-static bool plan_units(const pm_pedigree* ped, int T, int S, std::vector<int4>& units, bool unrelated = false) {
+static bool plan_units(const pm_pedigree* ped, int T, int S, std::vector<int4>& units, bool unrelated = false,
+                       bool nuc_es = false) {
   units.assign((size_t)T * S, make_int4(U_NONE, -1, 0, 0));
   std::vector<int> used(T, 0);
   int lane = 0;
   for (int f = 0; f < ped->n_fam; f++) {
     const int p0 = ped->fam_start[f], n = ped->fam_start[f + 1] - p0, kind = unrelated ? PM_FAM_FOUNDERS : ped->fam_kind[f];
     std::vector<int4> us;
-    if (kind == PM_FAM_EXTENDED) continue;
+    if (kind == PM_FAM_EXTENDED || (nuc_es && kind == PM_FAM_NUCLEAR)) continue;
     if (kind == PM_FAM_NUCLEAR) us.push_back(make_int4(U_NUC, f, p0, n));
     else if (kind == PM_FAM_FOUNDERS) {
       for (int j = 0; j < n; j += 3) {
@@ -1658,7 +1692,7 @@ extern "C" {
 void pm_engine_destroy(pm_engine* E) {
   if (!E) return;
   hipSetDevice(E->device);
-  void* bufs[] = {E->d_fam_founders, E->d_peel_start, E->d_ext_count, E->d_ext_fam, E->d_is_founder, E->d_steps, E->d_T10,
+  void* bufs[] = {E->d_units1, E->d_ext_count1, E->d_ext_fam1, E->d_fam_founders, E->d_peel_start, E->d_ext_count, E->d_ext_fam, E->d_is_founder, E->d_steps, E->d_T10,
                   E->d_T10dn, E->d_ws, E->d_units_q,
                   E->d_fam_start, E->d_fam_kind, E->d_fa, E->d_mo, E->d_sex, E->d_units, E->d_lktab, E->d_M, E->d_syn,
                   E->d_pl, E->d_ref, E->d_dm, E->d_res, E->d_calls, E->d_raw, E->d_minv, E->d_mono, E->d_evals,
@@ -1691,11 +1725,15 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
   pm_engine* E = new pm_engine;
   E->device = device;
   E->par = *par;
+  E->vcf = par->vcf_mode != 0;
+  if (E->vcf) { E->par.denovo = 0; E->par.quick_call = 0; }   // the VCF path has neither (PedVCF.cpp)
+  par = &E->par;
   E->n_fam = ped->n_fam;
   E->n_person = ped->n_person;
   E->max_batch = max_batch;
   E->n_founders = ped->n_founders; E->male_founders = ped->male_founders; E->female_founders = ped->female_founders;
-  E->single_nuclear = (ped->n_fam == 1 && ped->fam_kind[0] == PM_FAM_NUCLEAR) ? 1 : 0;
+  // a lone nuclear family is evaluated once at 0.5 (FamilyLikelihoodSeq.cpp:91-104); the VCF path always runs Brent
+  E->single_nuclear = (!E->vcf && ped->n_fam == 1 && ped->fam_kind[0] == PM_FAM_NUCLEAR) ? 1 : 0;
   for (int f = 0; f < ped->n_fam; f++)
     if (ped->fam_kind[f] == PM_FAM_NUCLEAR) E->max_nuc = std::max(E->max_nuc, ped->fam_start[f + 1] - ped->fam_start[f]);
   for (int f = 0; f < ped->n_fam; f++) {
@@ -1743,6 +1781,8 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
   // tables
   double lk[256];
   for (int i = 0; i <= 255; i++) lk[i] = pow(0.1, i * 0.1);   // core/BaseQualityHelper.cpp:13 (host glibc)
+  if (E->vcf)   // FamilyLikelihoodSeq_VCF::PL2LK_table (src/FamilyLikelihoodSeq_VCF.cpp:21-22)
+    for (int i = 0; i <= 255; i++) lk[i] = pow(10, -double(i) / 10.0);
   geno_mut_matrix(par->denovo_mut_rate, par->denovo_tstv, E->M_h);
   static pm_synth_tables syn;
   pm_synth_build_tables(&syn);
@@ -1778,15 +1818,19 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
     std::vector<int2> steps;
     std::vector<int> founders(ped->fam_founders, ped->fam_founders + ped->n_fam);
     int wsmax = 0;
+    E->plan1_ok = E->vcf;
     for (int f = 0; f < ped->n_fam; f++) {
       peel_start[f] = (int)steps.size();
-      if (ped->fam_kind[f] != PM_FAM_EXTENDED) continue;
+      const int kind = ped->fam_kind[f];
+      if (kind == PM_FAM_FOUNDERS || (kind == PM_FAM_NUCLEAR && !E->vcf)) continue;
+      const size_t mark = steps.size();
       const int w = pack_steps(ped, f, ns, steps);
-      if (w < 0) {
+      if (w < 0 && kind == PM_FAM_EXTENDED) {
         pm_engine_destroy(E);
         pm_set_last_error("pm_engine_create: extended family without a usable peeling schedule (or > 255 members)");
         return PM_EPED;
       }
+      if (w < 0) { steps.resize(mark); E->plan1_ok = false; continue; }   // nuclear without a schedule: no plan 1
       wsmax = std::max(wsmax, w);
     }
     peel_start[ped->n_fam] = (int)steps.size();
@@ -1816,14 +1860,48 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
     HIP_TRY(hipMemcpy(E->d_T10, T10.data(), sizeof(double) * 1000, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(E->d_T10dn, T10dn.data(), sizeof(double) * 1000, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_TBA), kTBA, sizeof(kTBA)));
-    // workspace: the Brent grid and the posterior grid are capped so each needs <= 1 GiB
+    // vcf_mode plan 1: nuclear families peeled too (chrX/Y/MT sections, or a single family)
+    if (E->plan1_ok) {
+      int n1 = 0;
+      for (int f = 0; f < ped->n_fam; f++) {
+        if (ped->fam_kind[f] != PM_FAM_FOUNDERS) n1++;
+        else E->has_fp1 = 1;
+      }
+      int tmin = 1;
+      while (tmin < std::min(std::max(n1, 1), 256)) tmin *= 2;
+      static const int2 gp[] = {{64, 1}, {64, 2}, {64, 4}, {64, 8}, {256, 4}, {512, 4}, {1024, 4}, {1024, 8}};
+      std::vector<int4> u1;
+      for (auto g : gp)
+        if (g.x >= tmin && plan_units(ped, g.x, g.y, u1, false, true)) { E->T1 = g.x; E->S1 = g.y; break; }
+      if (!E->T1) E->plan1_ok = false;
+      else {
+        E->n_ext1 = n1;
+        E->max_ext1 = (n1 + E->T1 - 1) / E->T1;
+        std::vector<int> c1(E->T1, 0), e1((size_t)std::max(1, E->max_ext1) * E->T1, -1);
+        int q1 = 0;
+        for (int f = 0; f < ped->n_fam; f++)
+          if (ped->fam_kind[f] != PM_FAM_FOUNDERS) { const int lane = q1 % E->T1; e1[(size_t)c1[lane]++ * E->T1 + lane] = f; q1++; }
+        DALLOC(E->d_units1, u1.size());
+        DALLOC(E->d_ext_count1, E->T1);
+        DALLOC(E->d_ext_fam1, e1.size());
+        HIP_TRY(hipMemcpy(E->d_units1, u1.data(), sizeof(int4) * u1.size(), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(E->d_ext_count1, c1.data(), sizeof(int) * E->T1, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(E->d_ext_fam1, e1.data(), sizeof(int) * e1.size(), hipMemcpyHostToDevice));
+        E->grid1 = E->n_cu * std::max(1, 1024 / E->T1);
+      }
+    }
+    // workspace: the Brent grids and the posterior grid are capped so each needs <= 1 GiB
     E->grid_post = E->n_cu * 8;
     if (wsmax > 0) {
       const size_t cap = (size_t)1 << 30, per_lane = (size_t)wsmax * sizeof(double);
       E->grid_brent = (int)std::max<size_t>(E->n_cu, std::min<size_t>(E->grid_brent, cap / (per_lane * T)));
       E->grid_brent -= E->grid_brent % 8;   // keep the XCD-aware item order exact
+      if (E->T1) {
+        E->grid1 = (int)std::max<size_t>(E->n_cu, std::min<size_t>(E->grid1, cap / (per_lane * E->T1)));
+        E->grid1 -= E->grid1 % 8;
+      }
       E->grid_post = (int)std::max<size_t>(E->n_cu, std::min<size_t>(E->grid_post, cap / (per_lane * 256)));
-      const size_t lanes = std::max((size_t)E->grid_brent * T, (size_t)E->grid_post * 256);
+      const size_t lanes = std::max({(size_t)E->grid_brent * T, (size_t)E->grid1 * E->T1, (size_t)E->grid_post * 256});
       DALLOC(E->d_ws, lanes * wsmax);
     }
   }
@@ -1866,6 +1944,12 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
 int pm_engine_begin_section(pm_engine* E, int32_t chrom) {
   if (!E || chrom < 0 || chrom > 3) { pm_set_last_error("pm_engine_begin_section: invalid arguments"); return PM_EINVAL; }
   E->chrom = chrom;
+  E->use_plan1 = E->vcf && (chrom != PM_CHR_AUTO || E->n_fam == 1);
+  if (E->use_plan1 && !E->plan1_ok) {
+    pm_set_last_error("pm_engine_begin_section: vcf_mode on chrX/Y/MT (or with a single family) needs a peeling schedule "
+                      "for every nuclear family (pm_pedigree.steps)");
+    return PM_EPED;
+  }
   // GetPolyPrior (NucFamGenotypeLikelihood.cpp:231-304)
   int n;
   if (chrom == PM_CHR_X) n = E->female_founders * 2 + E->male_founders;
@@ -1895,6 +1979,11 @@ static DevArgs make_args(pm_engine* E, int n, const uint8_t* pl, const uint32_t*
   A.T10 = E->d_T10; A.T10dn = E->d_T10dn; A.ws = E->d_ws; A.ws_per_lane = E->ws_per_lane;
   A.theta_one = 1.0;
   A.unrelated = E->par.quick_call ? 1 : 0;   // k_prep: route sites through the quick pre-filter first
+  A.vcf = E->vcf ? 1 : 0;
+  if (E->use_plan1) {
+    A.units = E->d_units1; A.T = E->T1; A.S = E->S1;
+    A.ext_count = E->n_ext1 ? E->d_ext_count1 : nullptr; A.ext_fam = E->d_ext_fam1; A.nuc_es = 1;
+  }
   A.lktab = E->d_lktab; A.M = E->d_M; A.syn = E->d_syn;
   A.precision = E->par.precision; A.posterior = E->par.posterior; A.theta = E->par.theta;
   A.min_total_depth = E->par.min_total_depth; A.max_total_depth = E->par.max_total_depth; A.min_map_quality = E->par.min_map_quality;
@@ -1944,11 +2033,13 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
   int T = E->T, S = E->S, grid = E->grid_brent;
   // lean kernel: autosome, no de novo model, nuclear families only (the common case)
   bool gen = E->chrom != PM_CHR_AUTO || E->par.denovo || E->has_fp || E->n_fam == 1;
+  int n_ext = E->n_ext;
+  if (E->use_plan1) { T = E->T1; S = E->S1; grid = E->grid1; gen = true; n_ext = E->n_ext1; }
   if (unrelated) {   // MakeUnrelated(): all-founder products over the quick plan, no ES, no de novo model
     A.units = E->d_units_q; A.T = T = E->Tq; A.S = S = E->Sq; grid = E->grid_q;
     A.ext_count = nullptr; A.unrelated = 1; A.denovo = 0; gen = true;
   } else A.unrelated = 0;
-  BrentFn fn = brent_kernel(T, S, E->par.numerics, gen, !unrelated && E->n_ext > 0);
+  BrentFn fn = brent_kernel(T, S, E->par.numerics, gen, !unrelated && n_ext > 0);
   if (!fn) { pm_set_last_error("launch_brent: no kernel variant for the lane plan"); return PM_EINVAL; }
   hipEvent_t a, b;
   HIP_TRY(hipEventCreate(&a));
@@ -1985,11 +2076,16 @@ static int run_pipeline(pm_engine* E, int n, const uint8_t* pl, const uint32_t* 
     HIP_TRY(hipMemsetAsync(E->d_counts + 1, 0, 2 * sizeof(int), E->stream));
   }
   if ((rc = launch_brent(E, A, 0))) return rc;
-  hipLaunchKernelGGL(k_select, dim3(gb), dim3(tb), 0, E->stream, A);
-  HIP_TRY(hipGetLastError());
-  if ((rc = launch_brent(E, A, 1))) return rc;
-  hipLaunchKernelGGL(k_finalize, dim3(gb), dim3(tb), 0, E->stream, A);
-  HIP_TRY(hipGetLastError());
+  if (E->vcf) {
+    hipLaunchKernelGGL(k_finalize_vcf, dim3(gb), dim3(tb), 0, E->stream, A);
+    HIP_TRY(hipGetLastError());
+  } else {
+    hipLaunchKernelGGL(k_select, dim3(gb), dim3(tb), 0, E->stream, A);
+    HIP_TRY(hipGetLastError());
+    if ((rc = launch_brent(E, A, 1))) return rc;
+    hipLaunchKernelGGL(k_finalize, dim3(gb), dim3(tb), 0, E->stream, A);
+    HIP_TRY(hipGetLastError());
+  }
   if (E->par.denovo) {
     hipLaunchKernelGGL(k_prepare_items7, dim3(gb), dim3(tb), 0, E->stream, A);
     if ((rc = launch_brent(E, A, 2))) return rc;
@@ -1999,12 +2095,13 @@ static int run_pipeline(pm_engine* E, int n, const uint8_t* pl, const uint32_t* 
   hipLaunchKernelGGL(k_rows, dim3(1), dim3(1024), 0, E->stream, A);
   HIP_TRY(hipGetLastError());
   {
-    void (*post)(DevArgs) = E->par.denovo ? (E->n_ext ? k_posterior<true, true> : k_posterior<true, false>)
-                                          : (E->n_ext ? k_posterior<false, true> : k_posterior<false, false>);
+    const bool es = (E->use_plan1 ? E->n_ext1 : E->n_ext) > 0;
+    void (*post)(DevArgs) = E->par.denovo ? (es ? k_posterior<true, true> : k_posterior<true, false>)
+                                          : (es ? k_posterior<false, true> : k_posterior<false, false>);
     hipLaunchKernelGGL(post, dim3(E->grid_post), dim3(256), 0, E->stream, A);
   }
   HIP_TRY(hipGetLastError());
-  if (!E->par.denovo && E->chrom == PM_CHR_AUTO) {
+  if (!E->par.denovo && E->chrom == PM_CHR_AUTO && !E->vcf) {
     hipLaunchKernelGGL(k_ab, dim3(E->n_cu * 8), dim3(256), 0, E->stream, A);
     HIP_TRY(hipGetLastError());
   }
@@ -2039,7 +2136,7 @@ int pm_engine_sync(pm_engine* E) {
   HIP_TRY(hipMemcpy(counts, E->d_counts, sizeof(counts), hipMemcpyDeviceToHost));
   if (counts[4] != 0x7fffffff) E->carry_postprob = true;
   E->stats.items += (int64_t)counts[0] + counts[1] + counts[2] + counts[8];
-  E->stats.site_visits += (int64_t)counts[0] / (E->par.denovo ? 4 : 3) + counts[1] / 3 + counts[2] + counts[9];
+  E->stats.site_visits += (int64_t)counts[0] / (E->vcf ? 1 : E->par.denovo ? 4 : 3) + counts[1] / 3 + counts[2] + counts[9];
   E->stats.sites += E->last_n;
   int rc = collect_stats(E);
   if (rc) return rc;

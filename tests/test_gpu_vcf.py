@@ -1,0 +1,72 @@
+"""GPU tests of the --in_vcf path (PedVCF / FamilyLikelihoodSeq_VCF on the engine's vcf_mode).
+
+* The product CLI reproduces the reference's example/testvcf.out.vcf byte-for-byte (every numerics mode).
+* The engine in vcf_mode matches the CPU oracle's VCF restatement on synthetic pedigrees of every family
+  kind, on autosomes and on chrX/Y/MT.  Outside the nuclear autosomal case (covered by the golden) the
+  oracle's VCF path is pinned only through the code it shares with the GLF path: the reference's VCF
+  path needs tabix/bgzf/pcre and cannot be built here, so those cases are "parity unpinned"
+  against the reference itself.
+"""
+import gzip
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import polymutt_amd as pm
+from conftest import EXAMPLE
+from fixtures import read_dataset
+from oracle_binding import Oracle
+from parity import compare_results
+
+pytestmark = pytest.mark.gpu
+
+TS = {1: 3, 2: 4, 3: 1, 4: 2}
+
+
+@pytest.mark.parametrize("numerics", ["product", "exact", "poly"])
+def test_cli_reproduces_vcf_input_golden(built, tmp_path, numerics):
+    out = tmp_path / "out.vcf"
+    r = subprocess.run([pm.BIN_PATH, "-p", "test.ped", "-d", "test.dat", "--in_vcf",
+                        os.path.join(EXAMPLE, "testvcf.in.vcf.gz"), "--out_vcf", str(out), "--numerics", numerics],
+                       cwd=EXAMPLE, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:]
+    exp = gzip.open(os.path.join(EXAMPLE, "testvcf.out.vcf.body.gz"), "rt").read().splitlines()
+    got = [l for l in out.read_text().splitlines() if not l.startswith("##")]
+    assert len(got) == len(exp)
+    diff = [i for i, (a, b) in enumerate(zip(got, exp)) if a != b]
+    assert not diff, f"{len(diff)} lines differ; first:\n{got[diff[0]][:300]}\n{exp[diff[0]][:300]}"
+
+
+def _vcf_block(pl, ref, seed):
+    """Biallelic (ref, alt) per site: alt = transition, or a transversion on a third of the sites."""
+    rng = np.random.default_rng(seed)
+    alt = np.array([TS[int(r)] for r in ref], np.uint8)
+    tv = rng.random(len(ref)) < 0.33
+    alt[tv] = np.array([1 + (int(r) % 4) for r in ref[tv]], np.uint8)
+    alt[alt == ref] = np.array([1 + ((int(r) + 1) % 4) for r in ref[alt == ref]], np.uint8)
+    return (ref | (alt << 4)).astype(np.uint8)
+
+
+@pytest.mark.parametrize("shape,nfam", [("quad", 40), ("mixed", 31), ("single", 12), ("ext10", 8), ("roof", 8),
+                                        ("quad", 1)])
+@pytest.mark.parametrize("chrom", [pm.PM_CHR_AUTO, pm.PM_CHR_X, pm.PM_CHR_Y, pm.PM_CHR_MT])
+@pytest.mark.parametrize("numerics", [pm.NUM_POLY, pm.NUM_EXACT])
+def test_engine_vcf_mode_matches_oracle(built, tmp_path, shape, nfam, chrom, numerics):
+    pm.synth_write_dataset(str(tmp_path), shape, nfam, 300, 29)
+    ped, secs, _ = read_dataset(str(tmp_path))
+    (label, pos, ref, pl, dm), = secs
+    refalt = _vcf_block(pl, ref, 5)
+    par = pm.Params.defaults(vcf_mode=1, numerics=numerics)
+    eng = pm.Engine(ped.view, par, max_batch=128)
+    ora = Oracle(ped.view, par)
+    eng.begin_section(chrom)
+    ora.begin_section(chrom)
+    zeros = np.zeros_like(dm)
+    for s in range(0, len(ref), 128):
+        e, ec = eng.run(pl[s:s + 128], zeros[s:s + 128], refalt[s:s + 128])
+        o, oc = ora.run(pl[s:s + 128], zeros[s:s + 128], refalt[s:s + 128])
+        st = compare_results(e, o, ec, oc, label=f"{shape}/{chrom}[{s}] ")
+        assert st["emitted"] == st["called"] == len(e)
+    eng.close()
