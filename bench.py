@@ -46,7 +46,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--families", type=int, default=1000)
-    ap.add_argument("--shape", choices=["quad", "trio"], default="quad")
+    ap.add_argument("--shape", choices=["quad", "trio", "ext10", "mixed"], default="quad",
+                    help="quad/trio: BASELINE configs 2-3; ext10: config 4 (3-generation pedigrees, ES peeling); "
+                         "mixed: trios and quads (config 5 with --vcf)")
+    ap.add_argument("--vcf", action="store_true", help="BASELINE config 5: the --in_vcf engine mode (one Brent per site)")
     ap.add_argument("--denovo", action="store_true", help="BASELINE config 3: --denovo MutationModel")
     ap.add_argument("--batch", type=int, default=65536, help="sites per step per GPU")
     ap.add_argument("--pool", type=int, default=2, help="distinct resident batches cycled by the steps")
@@ -147,16 +150,32 @@ def main():
     import polymutt_amd as pm
     from polymutt_amd.shard import allreduce_counters, max_over_ranks
 
-    kids = 2 if args.shape == "quad" else 1
-    ped = nuclear_pedigree(pm, args.families, kids)
+    kids = {"quad": 2, "trio": 1, "mixed": 2, "ext10": 2}[args.shape]
+    if args.shape in ("quad", "trio"):
+        ped = nuclear_pedigree(pm, args.families, kids)
+        ped_keep = None
+    else:   # pedigrees with ES schedules come from the native loader (synthetic .ped written once)
+        tmpd = tempfile.mkdtemp(prefix="pm_ped_", dir=os.environ.get("TMPDIR", "/tmp"))
+        pm.synth_write_dataset(tmpd, args.shape, args.families, 1, args.seed)
+        ped_keep = pm.Pedigree(os.path.join(tmpd, "test.dat"), os.path.join(tmpd, "test.ped"))
+        shutil.rmtree(tmpd, ignore_errors=True)
+        ped = ped_keep.view
     B, P = args.batch, args.pool
-    params = pm.Params.defaults(denovo=1 if args.denovo else 0)
+    params = pm.Params.defaults(denovo=1 if args.denovo else 0, vcf_mode=1 if args.vcf else 0)
     eng = pm.Engine(ped, params, device=local, max_batch=B)
     npers = ped.n_person
     bufs = []
     for p in range(P):   # this rank's shard of the synthetic site stream (weak scaling)
         d_pl, d_dm, d_ref = eng.alloc(B * npers * 10), eng.alloc(B * npers * 4), eng.alloc(B)
         eng.synth(B, args.seed, (rank * P + p) * B, d_pl, d_dm, d_ref)
+        if args.vcf:   # (ref, alt = transition) per site, as a biallelic VCF record carries it
+            href = np.empty(B, np.uint8)
+            eng.to_host(href, d_ref, B)
+            ts = np.array([0, 3, 4, 1, 2], np.uint8)
+            href = (href | (ts[href] << 4)).astype(np.uint8)
+            eng.free(d_ref)
+            d_ref = eng.alloc(B)
+            eng.to_device(d_ref, href, B)
         bufs.append((d_pl, d_dm, d_ref))
 
     host = None
@@ -217,8 +236,8 @@ def main():
             "value": value, "unit": "sites/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": f"{nf} nuclear {args.shape} families (2 parents + {K} kids), synthetic GLF-shaped "
-                                   f"sites per SURVEY 8(d) generated in HBM" + (", --denovo" if args.denovo else ""),
+            "config": {"workload": f"{nf} {args.shape} families, synthetic GLF-shaped sites per SURVEY 8(d) generated in "
+                                   f"HBM" + (", --denovo" if args.denovo else "") + (", --in_vcf engine mode" if args.vcf else ""),
                        "families": nf, "persons": npers, "sites_per_step_per_gpu": B,
                        "distinct_sites_per_gpu": B * P, "parallelism": f"site-shard x{world}",
                        "inputs": "host (PCIe-inclusive)" if args.host_inputs else "HBM-resident"},

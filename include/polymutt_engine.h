@@ -201,6 +201,7 @@ int pm_engine_synth(pm_engine *eng, int32_t n, uint64_t seed, uint64_t site_offs
 int pm_device_alloc(pm_engine *eng, uint64_t bytes, void **d_ptr);
 int pm_device_free(pm_engine *eng, void *d_ptr);
 int pm_copy_to_host(pm_engine *eng, void *h_dst, const void *d_src, uint64_t bytes);
+int pm_copy_to_device(pm_engine *eng, void *d_dst, const void *h_src, uint64_t bytes);
 
 /* Timing of the dominant (Brent) kernel over the last run: launches, summed kernel ms (HIP events on the
  * engine stream), total objective evaluations and family-evaluations (for roofline accounting). */

@@ -1399,8 +1399,9 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
   }
 }
 
-// CalculateAB (:1006-1039) for emitted autosomal non-de-novo sites: per-person terms in parallel,
-// the two sums accumulated serially in person order (bit-identical to the reference).
+// CalculateAB (:1006-1039) for emitted autosomal non-de-novo sites: wave per row, per-person terms in
+// parallel, the two sums reduced as lane partials + butterfly.  The reference sums in person order; the
+// reordering changes AB by ~1e-16 relative (AB is printed with %.3f; parity tolerance 1e-9).
 __global__ void __launch_bounds__(256) k_ab(DevArgs A) {
   __shared__ double s_lk[256];
   for (int i = threadIdx.x; i < 256; i += blockDim.x) s_lk[i] = A.lktab[i];
@@ -1418,34 +1419,24 @@ __global__ void __launch_bounds__(256) k_ab(DevArgs A) {
     const double fr = R->af;
     const double p11 = fr * fr, p12 = 2 * fr * (1 - fr), p22 = (1 - fr) * (1 - fr);
     double Asum = 0.0, Bsum = 0.0;
-    for (int base = 0; base < np; base += 64) {
-      const int p = base + lane;
-      double ta = 0.0, tb = 0.0;
-      bool use = false;
-      if (p < np) {
-        const int depth = (int)(dm[p] & 0xFFFFFF);
-        const uint8_t* Rr = pl + (size_t)p * 10;
-        const int k11 = Rr[g11], k12 = Rr[g12], k22 = Rr[g22];
-        const double l11 = s_lk[k11], l12 = s_lk[k12], l22 = s_lk[k22];
-        const double PHet = (p12 * l12) / (p11 * l11 + p12 * l12 + p22 * l22);
-        if (PHet > 1e-05 && depth > 0) {
-          int scale = k22 + k11 - 2 * k12 + 6 * depth;
-          const int minimum = abs(k22 - k11);
-          if (scale < 4) scale = 4;
-          if (scale < minimum) scale = minimum;
-          const int nRef = (int)(0.5 * depth * (1 + (k22 - k11) / (scale + 1e-30)));
-          ta = PHet * nRef; tb = PHet * depth; use = true;
-        }
-      }
-      // A += PHet*nRef; B += PHet*depth in person order (only contributing persons change the sums)
-      unsigned long long m = __ballot(use);
-      while (m) {
-        const int l = __ffsll((long long)m) - 1;
-        m &= m - 1;
-        Asum += __shfl(ta, l, 64);
-        Bsum += __shfl(tb, l, 64);
+    for (int p = lane; p < np; p += 64) {
+      const int depth = (int)(dm[p] & 0xFFFFFF);
+      const uint8_t* Rr = pl + (size_t)p * 10;
+      const int k11 = Rr[g11], k12 = Rr[g12], k22 = Rr[g22];
+      const double l11 = s_lk[k11], l12 = s_lk[k12], l22 = s_lk[k22];
+      const double PHet = (p12 * l12) / (p11 * l11 + p12 * l12 + p22 * l22);
+      if (PHet > 1e-05 && depth > 0) {
+        int scale = k22 + k11 - 2 * k12 + 6 * depth;
+        const int minimum = abs(k22 - k11);
+        if (scale < 4) scale = 4;
+        if (scale < minimum) scale = minimum;
+        const int nRef = (int)(0.5 * depth * (1 + (k22 - k11) / (scale + 1e-30)));
+        Asum += PHet * nRef;
+        Bsum += PHet * depth;
       }
     }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { Asum += __shfl_xor(Asum, o, 64); Bsum += __shfl_xor(Bsum, o, 64); }
     if (lane == 0) A.res[site].ab = (0.05 + Asum) / (0.1 + Bsum);
   }
 }
@@ -2224,6 +2215,14 @@ int pm_copy_to_host(pm_engine* E, void* dst, const void* src, uint64_t bytes) {
   HIP_TRY(hipSetDevice(E->device));
   HIP_TRY(hipStreamSynchronize(E->stream));
   HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  return PM_OK;
+}
+
+int pm_copy_to_device(pm_engine* E, void* dst, const void* src, uint64_t bytes) {
+  if (!E) return PM_EINVAL;
+  HIP_TRY(hipSetDevice(E->device));
+  HIP_TRY(hipStreamSynchronize(E->stream));
+  HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
   return PM_OK;
 }
 

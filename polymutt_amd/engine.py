@@ -103,6 +103,7 @@ EXPORTS = {
     "pm_device_alloc": (i32, [C.c_void_p, u64, P(C.c_void_p)]),
     "pm_device_free": (i32, [C.c_void_p, C.c_void_p]),
     "pm_copy_to_host": (i32, [C.c_void_p, C.c_void_p, C.c_void_p, u64]),
+    "pm_copy_to_device": (i32, [C.c_void_p, C.c_void_p, C.c_void_p, u64]),
     "pm_engine_kernel_stats": (i32, [C.c_void_p, P(KernelStats), i32]),
     "pm_last_error": (C.c_char_p, []),
     "pm_abi_version": (i32, []),
@@ -266,6 +267,10 @@ class Engine:
 
     def free(self, p):
         self._check(self.lib.pm_device_free(self.h, p))
+
+    def to_device(self, d_dst, src, nbytes):
+        src = np.ascontiguousarray(src)
+        self._check(self.lib.pm_copy_to_device(self.h, d_dst, _ptr(src), nbytes))
 
     def to_host(self, dst, d_src, nbytes):
         self._check(self.lib.pm_copy_to_host(self.h, _ptr(dst), d_src, nbytes))
