@@ -176,8 +176,9 @@ int pm_engine_begin_section(pm_engine *eng, int32_t chrom);
  *   dm  [n][n_person]      depth (bits 0-23) | mapQ << 24   (0 when absent)
  *   ref [n]                refBase 1..4 (anything else -> PM_SITE_BAD_REF)
  * inputs_on_device != 0: pl/dm/ref are device pointers on this engine's GPU, else host pointers.
- * Outputs are host pointers: res[n]; calls[n_rows * n_person] receives one row per emitted site
- * (row index = res[i].call_row, rows numbered in site order); *n_rows is set to the row count.
+ * Outputs are host pointers: res[n]; calls[n_rows * n_person] receives one row per written record
+ * (emit == 1; row index = res[i].call_row, rows numbered in site order, -1 for every other site: a
+ * suppressed de novo record, emit == 2, prints nothing and gets no row); *n_rows is set to the row count.
  * Counters accumulate into the section totals.  Synchronous. */
 int pm_engine_run(pm_engine *eng, int32_t n, const uint8_t *pl, const uint32_t *dm, const uint8_t *ref,
                   int32_t inputs_on_device, pm_site_result *res, pm_geno_call *calls, int32_t *n_rows);

@@ -233,7 +233,8 @@ struct ItemCtx {
   int chrom;
 };
 
-template <bool GEN>
+// GEN: chrX/Y/MT branches; DN: the de novo kid terms (the lean polynomial kernel takes DN without GEN)
+template <bool GEN, bool DN = GEN>
 __device__ __forceinline__ void hoist_nuc(const DevArgs& A, const ItemCtx& I, const uint8_t* pl, const double* lk, const double* M,
                                           int p0, int n, double* cond) {
   const uint8_t* F = pl + (size_t)p0 * 10;
@@ -250,7 +251,7 @@ __device__ __forceinline__ void hoist_nuc(const DevArgs& A, const ItemCtx& I, co
   for (int k = 0; k < 9; k++) kids[k] = 1.0;
   for (int j = 2; j < n; j++) {
     const uint8_t* K = pl + (size_t)(p0 + j) * 10;
-    if (!GEN || !I.denovo) {
+    if (!DN || !I.denovo) {
       const double l11 = lk[K[I.g11]], l12 = lk[K[I.g12]], l22 = lk[K[I.g22]];
 #pragma unroll
       for (int k = 0; k < 9; k++) kids[k] *= d_one_kid(k, GEN ? I.chrom : (int)PM_CHR_AUTO, I.sex, l11, l12, l22);
@@ -603,6 +604,93 @@ __device__ __forceinline__ void hoist_poly4(const DevArgs& A, const ItemCtx& I, 
   }
 }
 
+// De novo variant of hoist_poly4 (autosomal --denovo items, families of <= 4 persons): the kid terms are
+// likelihoodONEKid_denovo's CalcDenovoMutLk dot products over all 10 genotype likelihoods (:1553-1562,
+// :1266-1296), so each kid's whole 10-byte PL record is loaded.  Chunks of PM_HOIST_CHUNK_DN slots keep
+// the in-flight bytes small next to the 5 x S hoisted coefficients.  Arithmetic is hoist_nuc's, same order.
+#ifndef PM_HOIST_CHUNK_DN
+#define PM_HOIST_CHUNK_DN 2
+#endif
+template <int S, int T>
+__device__ __forceinline__ void hoist_poly4_dn(const DevArgs& A, const ItemCtx& I, const uint8_t* pl, const double* lk,
+                                               const double* M, double (*a)[5], unsigned& live) {
+  constexpr int C = S < PM_HOIST_CHUNK_DN ? S : PM_HOIST_CHUNK_DN;
+#pragma unroll
+  for (int c0 = 0; c0 < S; c0 += C) {
+    uint32_t par[C][6], kid[C][2][10];
+    int nn[C];
+    // mutation-matrix rows: laundered per chunk so the compiler re-reads them from LDS instead of keeping
+    // all 30 doubles live across the whole hoisting phase (which spills the 5 x S coefficients)
+    int r11 = I.g11 * 10, r12 = I.g12 * 10, r22 = I.g22 * 10;
+    asm volatile("" : "+v"(r11), "+v"(r12), "+v"(r22));
+#pragma unroll
+    for (int j = 0; j < C; j++) {
+      const int4 u = A.units[(c0 + j) * T + threadIdx.x];
+      const bool nuc = u.x == U_NUC;
+      nn[j] = nuc ? u.w : 0;
+      const uint8_t* F = pl + (size_t)u.z * 10;
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const bool ok = q < nn[j];
+        const uint8_t* R = F + (ok ? q * 10 : 0);
+        par[j][3 * q + 0] = ok ? R[I.g11] : 0;
+        par[j][3 * q + 1] = ok ? R[I.g12] : 0;
+        par[j][3 * q + 2] = ok ? R[I.g22] : 0;
+      }
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const bool ok = q + 2 < nn[j];
+        const uint8_t* R = F + (ok ? (q + 2) * 10 : 0);
+#pragma unroll
+        for (int g = 0; g < 10; g++) kid[j][q][g] = ok ? R[g] : 0;
+      }
+      if (nuc) live |= 1u << (c0 + j);
+    }
+#pragma unroll
+    for (int j = 0; j < C; j++) {
+      double c9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+      if (nn[j] >= 2) {
+        double kids[9];
+#pragma unroll
+        for (int k = 0; k < 9; k++) kids[k] = 1.0;
+#pragma unroll
+        for (int q = 0; q < 2; q++)
+          if (q + 2 < nn[j]) {
+            double D11 = 0.0, D12 = 0.0, D22 = 0.0;
+            if (I.denovo) {
+#pragma unroll
+              for (int g = 0; g < 10; g++) {
+                const double pg = lk[kid[j][q][g]];
+                D11 += M[r11 + g] * pg;
+                D12 += M[r12 + g] * pg;
+                D22 += M[r22 + g] * pg;
+              }
+            } else {   // cfg-7 items: likelihoodONEKid's autosomal terms are d_one_kid_dn's on (l11, l12, l22)
+              uint32_t b11 = 0, b12 = 0, b22 = 0;   // register selects (a dynamic index would go to scratch)
+#pragma unroll
+              for (int g = 0; g < 10; g++) {
+                b11 = g == I.g11 ? kid[j][q][g] : b11;
+                b12 = g == I.g12 ? kid[j][q][g] : b12;
+                b22 = g == I.g22 ? kid[j][q][g] : b22;
+              }
+              D11 = lk[b11]; D12 = lk[b12]; D22 = lk[b22];
+            }
+#pragma unroll
+            for (int k = 0; k < 9; k++) kids[k] *= d_one_kid_dn(k, D11, D12, D22);
+          }
+        const double lF[3] = {lk[par[j][0]], lk[par[j][1]], lk[par[j][2]]};
+        const double lM[3] = {lk[par[j][3]], lk[par[j][4]], lk[par[j][5]]};
+#pragma unroll
+        for (int x = 0; x < 3; x++)
+#pragma unroll
+          for (int y = 0; y < 3; y++) c9[3 * x + y] = kids[3 * x + y] * (lF[x] * lM[y]);
+      }
+      fold_poly(c9, a[c0 + j]);
+    }
+    __builtin_amdgcn_sched_barrier(0);   // keep the next chunk's loads from being hoisted above this one
+  }
+}
+
 // Four interleaved (mantissa, exponent) accumulators: short dependency chains, few live registers.
 // Slots below `full` are occupied on every lane (families are dealt round-robin); only the slot rows at
 // or above it can be empty and are masked (h = 1).
@@ -670,7 +758,9 @@ __device__ __forceinline__ double block_logprod(double m, int e, double* red, in
 template <int T, int S, int NUM, bool GEN>
 constexpr int brent_waves() { return (NUM == PM_NUM_POLY && !GEN && T == 64 && S >= 8) ? PM_POLY_WAVES : 1; }
 
-template <int T, int S, int NUM, bool GEN, bool ES>
+// DN: lean polynomial kernel for autosomal --denovo (instantiated separately so the common kernel carries
+// no de novo hoisting code or register pressure).
+template <int T, int S, int NUM, bool GEN, bool ES, bool DN = false>
 __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(DevArgs A, int list) {
   constexpr bool PROD = NUM != PM_NUM_EXACT;
   __shared__ double s_lk[256];
@@ -702,7 +792,8 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
     else if (cfg == 7) { I.a1 = A.res[site].allele1; I.a2 = A.res[site].allele2; }
     else cfg_alleles(cfg, r, &I.a1, &I.a2);
     I.g11 = d_gi(I.a1, I.a1); I.g12 = d_gi(I.a1, I.a2); I.g22 = d_gi(I.a2, I.a2);
-    I.denovo = GEN ? (A.denovo && cfg != 7) : 0;
+    // the lean polynomial kernel also runs autosomal --denovo items (its hoisting has the de novo kid terms)
+    I.denovo = (GEN || (POLYK && DN)) ? (A.denovo && cfg != 7) : 0;
     I.sex = (GEN && cfg == 7) ? A.item_sex[site] : 0;
     I.chrom = GEN ? A.chrom : PM_CHR_AUTO;
     int pmode;
@@ -720,7 +811,11 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
     unsigned live = 0;
     bool hoisted = false;
     if constexpr (POLY) {
-      if (A.max_nuc <= 4) { hoist_poly4<S, T>(A, I, pl, s_lk, cond, live); hoisted = true; }
+      if (A.max_nuc <= 4) {
+        if constexpr (DN) hoist_poly4_dn<S, T>(A, I, pl, s_lk, s_M, cond, live);   // de novo and cfg-7 items
+        else hoist_poly4<S, T>(A, I, pl, s_lk, cond, live);
+        hoisted = true;
+      }
     }
 #pragma unroll
     for (int s = 0; s < S; s++) {
@@ -729,7 +824,7 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
       if constexpr (POLY) {
         const int4 u = A.units[s * T + threadIdx.x];   // L1/L2-resident; not kept in registers
         double c9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-        if (u.x == U_NUC) { hoist_nuc<GEN>(A, I, pl, s_lk, s_M, u.z, u.w, c9); live |= 1u << s; }
+        if (u.x == U_NUC) { hoist_nuc<false, DN>(A, I, pl, s_lk, s_M, u.z, u.w, c9); live |= 1u << s; }
         fold_poly(c9, cond[s]);
       } else if (unit[s].x == U_NUC) hoist_nuc<GEN>(A, I, pl, s_lk, s_M, unit[s].z, unit[s].w, cond[s]);
       else if (GEN && unit[s].x == U_FP) fl[s] = hoist_fp(A, I, pl, s_lk, unit[s].z, unit[s].w & 0xFF, cond[s]);
@@ -1442,13 +1537,17 @@ __global__ void __launch_bounds__(256) k_ab(DevArgs A) {
 }
 
 __global__ void k_rows(DevArgs A) {
-  // emitted sites -> rows, in site order (single block scan; batches are <= a few million sites)
+  // written records -> rows, in site order (single block scan; batches are <= a few million sites)
   __shared__ int s_base;
   if (threadIdx.x == 0) s_base = 0;
   __syncthreads();
   for (int base = 0; base < A.n; base += blockDim.x) {
     const int site = base + threadIdx.x;
-    const int e = (site < A.n && A.res[site].emit) ? 1 : 0;
+    // rows only for written records: an OutputVCF_denovo call that returns before the record (emit 2,
+    // NucFamGenotypeLikelihood.cpp:1868) has no observable genotype output, so its posteriors are skipped
+    const int em = site < A.n ? A.res[site].emit : 0;
+    const int e = em == 1 ? 1 : 0;
+    if (em == 2) A.res[site].call_row = -1;
     // wave-level exclusive scan via ballot
     const unsigned long long bal = __ballot(e);
     const int lane = threadIdx.x & 63;
@@ -1753,7 +1852,7 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
   // is spread over 2-8 waves (one barrier per evaluation).  Sections on chrX/Y/MT run the generic
   // kernel on the same plan.
   {
-    const bool gen = par->denovo || E->has_fp || ped->n_fam == 1;
+    const bool gen = (par->denovo && par->numerics != PM_NUM_POLY) || E->has_fp || ped->n_fam == 1;
     static const int2 lean[] = {{64, 1}, {64, 2}, {64, 4}, {64, 8}, {64, 16}, {512, 4}, {1024, 4}, {1024, 8}};
     static const int2 generic[] = {{64, 1}, {64, 2}, {64, 4}, {64, 8}, {256, 4}, {512, 4}, {1024, 4}, {1024, 8}};
     const int2* pref = gen ? generic : lean;
@@ -1998,8 +2097,14 @@ static DevArgs make_args(pm_engine* E, int n, const uint8_t* pl, const uint32_t*
 typedef void (*BrentFn)(DevArgs, int);
 // numerics: PM_NUM_PRODUCT / PM_NUM_EXACT for every flavour; PM_NUM_POLY only for the lean kernel
 // (the generic and ES flavours fall back to PRODUCT numerics).
-static BrentFn brent_kernel(int T, int S, int num, bool gen, bool es) {
+static BrentFn brent_kernel(int T, int S, int num, bool gen, bool es, bool dn = false) {
   const int n = (num == PM_NUM_POLY && gen) ? PM_NUM_PRODUCT : num;
+  if (dn && !gen && !es && n == PM_NUM_POLY) {   // lean autosomal --denovo
+#define PMKD(t, s) if (T == t && S == s) return k_brent<t, s, PM_NUM_POLY, false, false, true>;
+    PMKD(64, 1) PMKD(64, 2) PMKD(64, 4) PMKD(64, 8) PMKD(64, 16) PMKD(512, 4) PMKD(1024, 4) PMKD(1024, 8)
+#undef PMKD
+    return nullptr;
+  }
 #define PMK(t, s)                                                                                             \
   if (T == t && S == s) {                                                                                     \
     if (gen) return n == PM_NUM_EXACT ? k_brent<t, s, PM_NUM_EXACT, true, false> : k_brent<t, s, PM_NUM_PRODUCT, true, false>; \
@@ -2023,14 +2128,15 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
   DevArgs A = A0;
   int T = E->T, S = E->S, grid = E->grid_brent;
   // lean kernel: autosome, no de novo model, nuclear families only (the common case)
-  bool gen = E->chrom != PM_CHR_AUTO || E->par.denovo || E->has_fp || E->n_fam == 1;
+  // (with POLY numerics the lean kernel also takes autosomal --denovo: its hoisting has the de novo kid terms)
+  bool gen = E->chrom != PM_CHR_AUTO || (E->par.denovo && E->par.numerics != PM_NUM_POLY) || E->has_fp || E->n_fam == 1;
   int n_ext = E->n_ext;
   if (E->use_plan1) { T = E->T1; S = E->S1; grid = E->grid1; gen = true; n_ext = E->n_ext1; }
   if (unrelated) {   // MakeUnrelated(): all-founder products over the quick plan, no ES, no de novo model
     A.units = E->d_units_q; A.T = T = E->Tq; A.S = S = E->Sq; grid = E->grid_q;
     A.ext_count = nullptr; A.unrelated = 1; A.denovo = 0; gen = true;
   } else A.unrelated = 0;
-  BrentFn fn = brent_kernel(T, S, E->par.numerics, gen, !unrelated && n_ext > 0);
+  BrentFn fn = brent_kernel(T, S, E->par.numerics, gen, !unrelated && n_ext > 0, A.denovo != 0);
   if (!fn) { pm_set_last_error("launch_brent: no kernel variant for the lane plan"); return PM_EINVAL; }
   hipEvent_t a, b;
   HIP_TRY(hipEventCreate(&a));

@@ -186,7 +186,7 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval) {
       for (int i = 0; i < B.n && !stop; i++) {
         const pm_site_result& r = B.res[i];
         if (!r.emit) continue;
-        W.output(label, B.pos[i], B.ref[i], r, B.calls.data() + (size_t)r.call_row * np, B.pl.data() + (size_t)i * np * 10,
+        W.output(label, B.pos[i], B.ref[i], r, r.call_row >= 0 ? B.calls.data() + (size_t)r.call_row * np : nullptr, B.pl.data() + (size_t)i * np * 10,
                  B.dm.data() + (size_t)i * np);
         out_cnt++;
         if (opt.force_call && out_cnt >= (int)positionMap.size()) stop = true;   // main.cpp:593 returns without a summary

@@ -21,7 +21,7 @@ class OracleEvaluator : public SiteEvaluator {
     for (int i = 0; i < n; i++) {
       int rc = pmo_site(ctx_, pl + (size_t)i * np_ * 10, dm + (size_t)i * np_, ref[i], &res[i], calls + (size_t)rows * np_);
       if (rc == PM_EBRENT) { printf("\nFATAL NUMERIC ERROR - ScalarMinimizer::Brent got stuck\n\n"); exit(1); }
-      if (res[i].emit) res[i].call_row = rows++;
+      res[i].call_row = res[i].emit == 1 ? rows++ : -1;
     }
     *n_rows = rows;
   }

@@ -64,9 +64,11 @@ class Oracle:
                                  res[i:i + 1].ctypes.data, calls[rows].ctypes.data)
             if rc != 0:
                 raise FloatingPointError("ScalarMinimizer::Brent got stuck")
-            if res[i]["emit"]:
+            if res[i]["emit"] == 1:   # rows for written records only (emit 2 = suppressed de novo record)
                 res[i]["call_row"] = rows
                 rows += 1
+            else:
+                res[i]["call_row"] = -1
         return res, calls[:rows]
 
     def counters(self):

@@ -111,3 +111,26 @@ def test_synthetic_device_generator_and_parity(built, shape, nfam, nsites, tmp_p
     eng.close()
     stats = _run_both(ped, pm.Params.defaults(), secs, batch=256)
     assert sum(s["called"] for s in stats) > 0
+
+
+
+@pytest.mark.parametrize("numerics", [pm.NUM_PRODUCT, pm.NUM_POLY])
+@pytest.mark.parametrize("shape", ["quad+dn", "trio+dn"])
+def test_denovo_planted_parity(built, tmp_path, numerics, shape):
+    """--denovo on synthetic nuclear families with planted de novo kids: written records (10-state kid
+    posteriors) next to suppressed records (emit 2, no genotype row).  POLY runs the lean polynomial de novo
+    kernel, PRODUCT the generic one; both against the oracle."""
+    d = str(tmp_path / "dn")
+    pm.synth_write_dataset(d, shape, 40, 700, 31)
+    ped = pm.Pedigree(os.path.join(d, "test.dat"), os.path.join(d, "test.ped"))
+    label, pos, ref, pl, dm = _read_all(ped, d)[0]
+    params = pm.Params.defaults(denovo=1, denovo_mut_rate=1e-5, numerics=numerics)
+    eng = pm.Engine(ped.view, params, max_batch=len(ref))
+    ora = Oracle(ped.view, params)
+    e, ec = eng.run(pl, dm, ref)
+    o, oc = ora.run(pl, dm, ref)
+    st = compare_results(e, o, ec, oc, label="denovo ")
+    eng.close()
+    assert (o["emit"] == 1).sum() > 0 and (o["emit"] == 2).sum() > 0, np.unique(o["emit"], return_counts=True)
+    assert ((e["call_row"] >= 0) == (o["emit"] == 1)).all()
+    assert st["called"] > 0
