@@ -600,6 +600,7 @@ __device__ __forceinline__ void hoist_poly4(const DevArgs& A, const ItemCtx& I, 
           for (int y = 0; y < 3; y++) c9[3 * x + y] = kids[3 * x + y] * (lF[x] * lM[y]);
       }
       fold_poly(c9, a[c0 + j]);
+      if (nn[j] == 0) a[c0 + j][4] = 1.0;   // empty slot: h(r) = 1 exactly (lane_poly_r)
     }
   }
 }
@@ -686,6 +687,7 @@ __device__ __forceinline__ void hoist_poly4_dn(const DevArgs& A, const ItemCtx& 
           for (int y = 0; y < 3; y++) c9[3 * x + y] = kids[3 * x + y] * (lF[x] * lM[y]);
       }
       fold_poly(c9, a[c0 + j]);
+      if (nn[j] == 0) a[c0 + j][4] = 1.0;   // empty slot: h(r) = 1 exactly (lane_poly_r)
     }
     __builtin_amdgcn_sched_barrier(0);   // keep the next chunk's loads from being hoisted above this one
   }
@@ -693,10 +695,10 @@ __device__ __forceinline__ void hoist_poly4_dn(const DevArgs& A, const ItemCtx& 
 
 // Four interleaved (mantissa, exponent) accumulators: short dependency chains, few live registers.
 // Slots below `full` are occupied on every lane (families are dealt round-robin); only the slot rows at
-// or above it can be empty and are masked (h = 1).
-template <int S>
-__device__ __forceinline__ void lane_poly(bool lo, double t, int full, unsigned live, const double (*a)[5], double& m,
-                                          int& e) {
+// or above it can be empty and are masked (h = 1).  LO selects the Horner direction (t = f / (1 - f) or
+// its inverse); the hot path is lane_poly_r, this form only serves f = 1.
+template <int S, bool LO>
+__device__ __forceinline__ void lane_poly_dir(double t, int full, unsigned live, const double (*a)[5], double& m, int& e) {
   constexpr int NA = S < 4 ? S : 4;
   double am[NA];
   int ae[NA];
@@ -705,7 +707,7 @@ __device__ __forceinline__ void lane_poly(bool lo, double t, int full, unsigned 
 #pragma unroll
   for (int s = 0; s < S; s++) {
     double h;
-    if (lo) h = fma(t, fma(t, fma(t, fma(t, a[s][0], a[s][1]), a[s][2]), a[s][3]), a[s][4]);
+    if (LO) h = fma(t, fma(t, fma(t, fma(t, a[s][0], a[s][1]), a[s][2]), a[s][3]), a[s][4]);
     else h = fma(t, fma(t, fma(t, fma(t, a[s][4], a[s][3]), a[s][2]), a[s][1]), a[s][0]);
     if (s >= full) h = ((live >> s) & 1) ? h : 1.0;
     int x;
@@ -724,16 +726,67 @@ __device__ __forceinline__ void lane_poly(bool lo, double t, int full, unsigned 
   e = ae[0];
 }
 
+// Hot form: h(r) = a0 r^4 + a1 r^3 + a2 r^2 + a3 r + a4 with r = f / (1 - f) >= 0 (non-negative coefficients:
+// no cancellation, relative error <= ~8 ulp for any r); empty slots hold (0, 0, 0, 0, 1), so h = 1 exactly.
+template <int S>
+__device__ __forceinline__ void lane_poly_r(double r, const double (*a)[5], double& m, int& e) {
+  constexpr int NA = S < 4 ? S : 4;
+  double am[NA];
+  int ae[NA];
+#pragma unroll
+  for (int j = 0; j < NA; j++) { am[j] = 1.0; ae[j] = 0; }
+#pragma unroll
+  for (int s = 0; s < S; s++) {
+    const double h = fma(r, fma(r, fma(r, fma(r, a[s][0], a[s][1]), a[s][2]), a[s][3]), a[s][4]);
+    int x;
+    am[s % NA] = frexp(am[s % NA] * h, &x);
+    ae[s % NA] += x;
+  }
+#pragma unroll
+  for (int w = 1; w < NA; w *= 2)
+#pragma unroll
+    for (int j = 0; j + w < NA; j += 2 * w) {
+      int x;
+      am[j] = frexp(am[j] * am[j + w], &x);
+      ae[j] += ae[j + w] + x;
+    }
+  m = am[0];
+  e = ae[0];
+}
+
+
+// One step of the wave product reduction on the DPP crossbar (VALU latency, no LDS round trip): multiply
+// by the (mantissa, exponent) of the lane selected by CTRL; rows outside ROWMASK keep their value (the
+// DPP `old` operand is the identity 1.0 x 2^0).
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ void dpp_prod_step(double& m, int& e) {
+  const int lo = __double2loint(m), hi = __double2hiint(m);
+  const int olo = __builtin_amdgcn_update_dpp(0, lo, CTRL, ROWMASK, 0xF, false);
+  const int ohi = __builtin_amdgcn_update_dpp(0x3FF00000, hi, CTRL, ROWMASK, 0xF, false);
+  const int oe = __builtin_amdgcn_update_dpp(0, e, CTRL, ROWMASK, 0xF, false);
+  int ev;
+  m = frexp(m * __hiloint2double(ohi, olo), &ev);
+  e += oe + ev;
+}
+
+// Product of the 64 lanes' (m, e), in a fixed order: quad xor 1, quad xor 2, half-row mirror, row mirror
+// (every lane of a row of 16 then holds the row product), row_bcast15 / row_bcast31 (lane 63 ends with
+// ((R3 R2)(R1 R0))), broadcast from lane 63.  Deterministic for any batch, identical in every lane.
+__device__ __forceinline__ void wave_prod(double& m, int& e) {
+  dpp_prod_step<0xB1, 0xF>(m, e);    // quad_perm [1,0,3,2]
+  dpp_prod_step<0x4E, 0xF>(m, e);    // quad_perm [2,3,0,1]
+  dpp_prod_step<0x141, 0xF>(m, e);   // row_half_mirror
+  dpp_prod_step<0x140, 0xF>(m, e);   // row_mirror
+  dpp_prod_step<0x142, 0xA>(m, e);   // row_bcast:15 -> rows 1, 3
+  dpp_prod_step<0x143, 0xC>(m, e);   // row_bcast:31 -> rows 2, 3
+  const int lo = __builtin_amdgcn_readlane(__double2loint(m), 63), hi = __builtin_amdgcn_readlane(__double2hiint(m), 63);
+  m = __hiloint2double(hi, lo);
+  e = __builtin_amdgcn_readlane(e, 63);
+}
+
 template <int T>
 __device__ __forceinline__ double block_logprod(double m, int e, double* red, int* rede, int& par) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {   // commutative butterfly: identical (m, e) in every lane
-    const double mo = __shfl_xor(m, o, 64);
-    const int eo = __shfl_xor(e, o, 64);
-    int ev;
-    m = frexp(m * mo, &ev);
-    e += eo + ev;
-  }
+  wave_prod(m, e);
   if (T > 64) {
     constexpr int W = T / 64;
     if ((threadIdx.x & 63) == 0) { red[par * 16 + (threadIdx.x >> 6)] = m; rede[par * 16 + (threadIdx.x >> 6)] = e; }
@@ -826,6 +879,7 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
         double c9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
         if (u.x == U_NUC) { hoist_nuc<false, DN>(A, I, pl, s_lk, s_M, u.z, u.w, c9); live |= 1u << s; }
         fold_poly(c9, cond[s]);
+        if (u.x != U_NUC) cond[s][4] = 1.0;   // empty slot: h(r) = 1 exactly (lane_poly_r)
       } else if (unit[s].x == U_NUC) hoist_nuc<GEN>(A, I, pl, s_lk, s_M, unit[s].z, unit[s].w, cond[s]);
       else if (GEN && unit[s].x == U_FP) fl[s] = hoist_fp(A, I, pl, s_lk, unit[s].z, unit[s].w & 0xFF, cond[s]);
     }
@@ -843,23 +897,18 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
     for (;;) {
       double tot;
       if constexpr (POLY) {
+        // L_fam(f) = g^4 h(f / g) (g = 1 - f): one Horner direction, no per-slot masking (empty slots hold
+        // h = 1).  f = 1 (the de novo monomorphism item) takes the reverse form M = f, t = g / f.
         const double g = 1 - x;
-        const bool lo = x <= g;
-        const double M = lo ? g : x;
-        double m; int e;
-        lane_poly<S>(lo, (lo ? x : g) / M, full, live, (const double(*)[5])cond, m, e);
-        tot = block_logprod<T>(m, e, s_red, s_rede, par) + (4.0 * A.n_fam) * log10(M);
-#ifdef PM_EXP_EVAL_TWICE   // timing experiment only: a second, identical evaluation the compiler cannot merge
-        {
-          const double x2 = x * A.theta_one;
-          const double g2 = 1 - x2;
-          const bool lo2 = x2 <= g2;
-          const double M2 = lo2 ? g2 : x2;
-          double m2; int e2;
-          lane_poly<S>(lo2, (lo2 ? x2 : g2) / M2, full, live, (const double(*)[5])cond, m2, e2);
-          tot = 0.5 * (tot + block_logprod<T>(m2, e2, s_red, s_rede, par) + (4.0 * A.n_fam) * log10(M2));
+        double m, lg; int e;
+        if (__builtin_amdgcn_readfirstlane((int)(g > 0.0))) {
+          lane_poly_r<S>(x / g, (const double(*)[5])cond, m, e);
+          lg = log10(g);
+        } else {
+          lane_poly_dir<S, false>(g / x, full, live, (const double(*)[5])cond, m, e);
+          lg = log10(x);
         }
-#endif
+        tot = block_logprod<T>(m, e, s_red, s_rede, par) + (4.0 * A.n_fam) * lg;
       } else if (PROD) {
         double m; int e;
         lane_prod<S, GEN>(x, unit, (const double(*)[9])cond, fl, pmode, m, e);
