@@ -96,6 +96,7 @@ struct DevArgs {
   double theta_one;        // 1.0 (opaque to the compiler; timing experiments only)
   int vcf;                 // vcf_mode: one (ref, alt) Brent per site, FamilyLikelihoodSeq_VCF family rules
   int nuc_es;              // nuclear families are peeled (vcf_mode plan 1)
+  int mono_dn;             // k_prep computes the de novo monomorphism item (cfg 0) itself (lean --denovo)
   // tables
   const double* lktab;     // [256]
   const double* M;         // [100] genotype mutation matrix
@@ -1008,7 +1009,13 @@ __device__ __forceinline__ double wave_serial_add(double s, double t, bool nz) {
 // (serial double sum, kept in the reference's person order) -- NucFamGenotypeLikelihood.cpp:502-546.
 __global__ void __launch_bounds__(256) k_prep(DevArgs A) {
   __shared__ unsigned long long s_c[9];
+  __shared__ double s_lk[256];
+  __shared__ double s_M[100];
   if (threadIdx.x < 9) s_c[threadIdx.x] = 0;
+  if (A.mono_dn) {
+    s_lk[threadIdx.x] = A.lktab[threadIdx.x];
+    if (threadIdx.x < 100) s_M[threadIdx.x] = A.M[threadIdx.x];
+  }
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -1024,6 +1031,13 @@ __global__ void __launch_bounds__(256) k_prep(DevArgs A) {
     const int h = okref ? d_gi(r, r) : 0;
     long long dsum = 0, mqsum = 0, nsd = 0;
     double mono = 0.0;
+    // lean --denovo: MonomorphismLogLikelihood_denovo (the cfg-0 item: CalcAllFamLogLikelihood at f = 1).
+    // SetParentPrior(1) = (1, 0, ..., 0), so each nuclear family contributes cond[0] = (Prod_kids
+    // CalcDenovoMutLk(geno11)) * F11 * M11 (:1041-1132, :1553-1562): a product of per-person factors --
+    // founders lk[geno11], kids their g11 dot product -- taken here as one normalised product per site.
+    const bool mdn = A.mono_dn && okref;
+    double dm_m = 1.0;
+    int dm_e = 0;
     for (int base = 0; base < np; base += 64) {
       const int p = base + lane;
       uint32_t x = 0;
@@ -1032,6 +1046,28 @@ __global__ void __launch_bounds__(256) k_prep(DevArgs A) {
       const int d = (int)(x & 0xFFFFFF);
       dsum += d; mqsum += (x >> 24); nsd += d > 0;
       mono = wave_serial_add(mono, -(double)hr / 10, hr != 0);
+      if (mdn && p < np) {
+        double fct;
+        if (A.is_founder[p]) fct = s_lk[hr];
+        else {
+          const uint8_t* K = pl + (size_t)p * 10;
+          fct = 0.0;
+#pragma unroll
+          for (int g = 0; g < 10; g++) fct += s_M[h * 10 + g] * s_lk[K[g]];
+        }
+        int xe;
+        dm_m = frexp(dm_m * fct, &xe);
+        dm_e += xe;
+      }
+    }
+    if (mdn) {
+      wave_prod(dm_m, dm_e);
+      if (lane == 0) {
+        const double de = (double)dm_e;
+        A.raw[(size_t)site * 8] = log10(dm_m) + (de * PM_LOG10_2_HI + de * PM_LOG10_2_LO);
+        A.minv[site * 8] = 0.0;
+        A.evals[site * 8] = 1;
+      }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) { dsum += __shfl_xor(dsum, o, 64); mqsum += __shfl_xor(mqsum, o, 64); nsd += __shfl_xor(nsd, o, 64); }
@@ -1064,9 +1100,10 @@ __global__ void __launch_bounds__(256) k_prep(DevArgs A) {
         const int slot = atomicAdd(&A.counts[1], 3);
         for (int k = 0; k < 3; k++) A.items[1][slot + k] = (site << 3) | (k + 1);
       } else if (valid) {
-        const int nit = A.denovo ? 4 : 3;
+        const int k0 = (A.denovo && !A.mono_dn) ? 0 : 1;   // cfg 0: de novo monomorphism (unless done above)
+        const int nit = 4 - k0;
         const int slot = atomicAdd(&A.counts[0], nit);
-        for (int k = 0; k < nit; k++) A.items[0][slot + k] = (site << 3) | (A.denovo ? k : k + 1);
+        for (int k = 0; k < nit; k++) A.items[0][slot + k] = (site << 3) | (k + k0);
       }
     }
   }
@@ -2104,6 +2141,13 @@ int pm_engine_begin_section(pm_engine* E, int32_t chrom) {
   return PM_OK;
 }
 
+// lean autosomal --denovo (POLY numerics, nuclear families only, no quick pre-filter): k_prep evaluates
+// the cfg-0 de novo monomorphism item itself instead of enqueueing it for k_brent
+static bool mono_dn_in_prep(const pm_engine* E) {
+  return E->par.denovo && E->par.numerics == PM_NUM_POLY && !E->par.quick_call && !E->vcf && E->chrom == PM_CHR_AUTO &&
+         !E->has_fp && E->n_ext == 0 && E->n_fam > 1;
+}
+
 static DevArgs make_args(pm_engine* E, int n, const uint8_t* pl, const uint32_t* dm, const uint8_t* ref, pm_site_result* res,
                          pm_geno_call* calls) {
   DevArgs A;
@@ -2140,6 +2184,7 @@ static DevArgs make_args(pm_engine* E, int n, const uint8_t* pl, const uint32_t*
   for (int l = 0; l < N_LISTS; l++) A.items[l] = E->d_items[l];
   A.counts = E->d_counts; A.eval_total = E->d_eval_total; A.row_site = E->d_row_site; A.counters = E->d_counters;
   A.carry_postprob = E->carry_postprob ? 1 : 0;
+  A.mono_dn = mono_dn_in_prep(E) ? 1 : 0;
   return A;
 }
 
@@ -2282,7 +2327,8 @@ int pm_engine_sync(pm_engine* E) {
   HIP_TRY(hipMemcpy(counts, E->d_counts, sizeof(counts), hipMemcpyDeviceToHost));
   if (counts[4] != 0x7fffffff) E->carry_postprob = true;
   E->stats.items += (int64_t)counts[0] + counts[1] + counts[2] + counts[8];
-  E->stats.site_visits += (int64_t)counts[0] / (E->vcf ? 1 : E->par.denovo ? 4 : 3) + counts[1] / 3 + counts[2] + counts[9];
+  E->stats.site_visits += (int64_t)counts[0] / (E->vcf ? 1 : (E->par.denovo && !mono_dn_in_prep(E)) ? 4 : 3) + counts[1] / 3 +
+                          counts[2] + counts[9];
   E->stats.sites += E->last_n;
   int rc = collect_stats(E);
   if (rc) return rc;
