@@ -544,6 +544,10 @@ __device__ __forceinline__ void lane_prod(double f, const int4* unit, const doub
 // (a0 = c0, a1 = 2(c1+c3), a2 = c2+4c4+c6, a3 = 2(c5+c7), a4 = c8; SetParentPrior :323-331).  With
 // M = max(f, g) and t = min(f, g)/M <= 1 it is M^4 h(t), h a 4-FMA Horner polynomial with non-negative
 // coefficients (no cancellation: relative error <= ~8 ulp); M^(4 nFam) leaves the product as one log10.
+// Empty lane slot: the "phantom family" (f + g)^4 = 1 -- coefficients (1, 4, 6, 4, 1) -- so lane_poly_r
+// needs no per-slot mask.  In floating point g^4 h(r) = ((1 + r) g)^4 is 1 to within a few ulp.
+__device__ __forceinline__ void phantom_poly(double* a) { a[0] = 1.0; a[1] = 4.0; a[2] = 6.0; a[3] = 4.0; a[4] = 1.0; }
+
 __device__ __forceinline__ void fold_poly(const double* c, double* a) {
   a[0] = c[0];
   a[1] = 2 * (c[1] + c[3]);
@@ -601,7 +605,7 @@ __device__ __forceinline__ void hoist_poly4(const DevArgs& A, const ItemCtx& I, 
           for (int y = 0; y < 3; y++) c9[3 * x + y] = kids[3 * x + y] * (lF[x] * lM[y]);
       }
       fold_poly(c9, a[c0 + j]);
-      if (nn[j] == 0) a[c0 + j][4] = 1.0;   // empty slot: h(r) = 1 exactly (lane_poly_r)
+      if (nn[j] == 0) phantom_poly(a[c0 + j]);   // empty slot (lane_poly_r)
     }
   }
 }
@@ -689,7 +693,7 @@ __device__ __forceinline__ void hoist_poly4_dn(const DevArgs& A, const ItemCtx& 
           for (int y = 0; y < 3; y++) c9[3 * x + y] = kids[3 * x + y] * (lF[x] * lM[y]);
       }
       fold_poly(c9, a[c0 + j]);
-      if (nn[j] == 0) a[c0 + j][4] = 1.0;   // empty slot: h(r) = 1 exactly (lane_poly_r)
+      if (nn[j] == 0) phantom_poly(a[c0 + j]);   // empty slot (lane_poly_r)
     }
     __builtin_amdgcn_sched_barrier(0);   // keep the next chunk's loads from being hoisted above this one
   }
@@ -728,10 +732,11 @@ __device__ __forceinline__ void lane_poly_dir(double t, int full, unsigned live,
   e = ae[0];
 }
 
-// Hot form: h(r) = a0 r^4 + a1 r^3 + a2 r^2 + a3 r + a4 with r = f / (1 - f) >= 0 (non-negative coefficients:
-// no cancellation, relative error <= ~8 ulp for any r); empty slots hold (0, 0, 0, 0, 1), so h = 1 exactly.
+// Hot form: L_fam(f) = g^4 h(r), h(r) = a0 r^4 + a1 r^3 + a2 r^2 + a3 r + a4 with r = f / g, g = 1 - f
+// (non-negative coefficients: no cancellation, relative error <= ~8 ulp for any r).  g4 = g^4 is folded
+// into every slot, so the objective needs no log10(g); empty slots hold the phantom family (f + g)^4.
 template <int S>
-__device__ __forceinline__ void lane_poly_r(double r, const double (*a)[5], double& m, int& e) {
+__device__ __forceinline__ void lane_poly_r(double r, double g4, const double (*a)[5], double& m, int& e) {
   constexpr int NA = S < 4 ? S : 4;
   double am[NA];
   int ae[NA];
@@ -739,7 +744,7 @@ __device__ __forceinline__ void lane_poly_r(double r, const double (*a)[5], doub
   for (int j = 0; j < NA; j++) { am[j] = 1.0; ae[j] = 0; }
 #pragma unroll
   for (int s = 0; s < S; s++) {
-    const double h = fma(r, fma(r, fma(r, fma(r, a[s][0], a[s][1]), a[s][2]), a[s][3]), a[s][4]);
+    const double h = fma(r, fma(r, fma(r, fma(r, a[s][0], a[s][1]), a[s][2]), a[s][3]), a[s][4]) * g4;
     int x;
     am[s % NA] = frexp(am[s % NA] * h, &x);
     ae[s % NA] += x;
@@ -881,7 +886,7 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
         double c9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
         if (u.x == U_NUC) { hoist_nuc<false, DN>(A, I, pl, s_lk, s_M, u.z, u.w, c9); live |= 1u << s; }
         fold_poly(c9, cond[s]);
-        if (u.x != U_NUC) cond[s][4] = 1.0;   // empty slot: h(r) = 1 exactly (lane_poly_r)
+        if (u.x != U_NUC) phantom_poly(cond[s]);   // empty slot (lane_poly_r)
       } else if (unit[s].x == U_NUC) hoist_nuc<GEN>(A, I, pl, s_lk, s_M, unit[s].z, unit[s].w, cond[s]);
       else if (GEN && unit[s].x == U_FP) fl[s] = hoist_fp(A, I, pl, s_lk, unit[s].z, unit[s].w & 0xFF, cond[s]);
     }
@@ -899,18 +904,18 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
     for (;;) {
       double tot;
       if constexpr (POLY) {
-        // L_fam(f) = g^4 h(f / g) (g = 1 - f): one Horner direction, no per-slot masking (empty slots hold
-        // h = 1).  f = 1 (the de novo monomorphism item) takes the reverse form M = f, t = g / f.
+        // L_fam(f) = g^4 h(f / g) (g = 1 - f): one Horner direction, g^4 folded per slot, no per-slot
+        // masking (empty slots hold the phantom family), one log10 per evaluation.  f = 1 (the generic-path
+        // de novo monomorphism item) takes the reverse form M = f, t = g / f with masking.
         const double g = 1 - x;
-        double m, lg; int e;
+        double m; int e;
         if (__builtin_amdgcn_readfirstlane((int)(g > 0.0))) {
-          lane_poly_r<S>(x / g, (const double(*)[5])cond, m, e);
-          lg = log10(g);
+          lane_poly_r<S>(x / g, (g * g) * (g * g), (const double(*)[5])cond, m, e);
+          tot = block_logprod<T>(m, e, s_red, s_rede, par);
         } else {
           lane_poly_dir<S, false>(g / x, full, live, (const double(*)[5])cond, m, e);
-          lg = log10(x);
+          tot = block_logprod<T>(m, e, s_red, s_rede, par) + (4.0 * A.n_fam) * log10(x);
         }
-        tot = block_logprod<T>(m, e, s_red, s_rede, par) + (4.0 * A.n_fam) * lg;
       } else if (PROD) {
         double m; int e;
         lane_prod<S, GEN>(x, unit, (const double(*)[9])cond, fl, pmode, m, e);
