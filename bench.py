@@ -186,11 +186,12 @@ def main():
         bufs.append((d_pl, d_dm, d_ref))
 
     host = None
-    if args.host_inputs:   # copy the resident batches to (pageable) host arrays once
+    if args.host_inputs:   # the same sites as person-major host arrays (pageable), pm_engine_run's layout
         host = []
-        for d_pl, d_dm, d_ref in bufs:
-            hpl, hdm, href = np.empty(B * npers * 10, np.uint8), np.empty(B * npers, np.uint32), np.empty(B, np.uint8)
-            eng.to_host(hpl, d_pl, hpl.nbytes); eng.to_host(hdm, d_dm, hdm.nbytes); eng.to_host(href, d_ref, href.nbytes)
+        for p in range(P):
+            hpl, hdm, href = pm.synth_block_host(ped, B, args.seed, (rank * P + p) * B)
+            if args.vcf:
+                eng.to_host(href, bufs[p][2], B)
             host.append((hpl, hdm, href))
 
     def step(i):

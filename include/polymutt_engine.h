@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 2
+#define PM_ABI_VERSION 3
 #define PM_NCFG 7           /* varllk slots: 0 mono, 1 ref/ts, 2 ref/tv1, 3 ref/tv2, 4 ts/tv1, 5 ts/tv2, 6 tv1/tv2 */
 
 typedef enum { PM_OK = 0, PM_EINVAL = -1, PM_EHIP = -2, PM_ENOMEM = -3, PM_EBRENT = -4, PM_EPED = -5 } pm_status;
@@ -185,16 +185,25 @@ int pm_engine_run(pm_engine *eng, int32_t n, const uint8_t *pl, const uint32_t *
 
 /* Device-resident variant for benchmarking / multi-GPU sharding: all pointers are device pointers,
  * results stay on the device (d_res[n], d_calls[n * n_person] indexed by site), launched on the
- * engine's stream; returns immediately.  pm_engine_sync waits. */
+ * engine's stream; returns immediately.  pm_engine_sync waits.
+ * d_pl is in the engine's GENOTYPE-PLANAR layout: [n][10][n_person] (site block of 10 planes, plane g
+ * holding every person's phred for genotype g), so the engine's wavefronts read consecutive persons as
+ * consecutive bytes.  pm_engine_synth writes this layout; pm_engine_to_planar converts person-major
+ * GLF-record blocks (the layout of pm_engine_run). */
 int pm_engine_run_device(pm_engine *eng, int32_t n, const uint8_t *d_pl, const uint32_t *d_dm, const uint8_t *d_ref,
                          pm_site_result *d_res, pm_geno_call *d_calls);
 int pm_engine_sync(pm_engine *eng);
+
+/* Person-major device block [n][n_person][10] -> genotype-planar [n][10][n_person] (distinct buffers),
+ * on the engine's stream (asynchronous, like pm_engine_run_device). */
+int pm_engine_to_planar(pm_engine *eng, int32_t n, const uint8_t *d_src, uint8_t *d_dst);
 
 /* Section counters accumulated so far (device -> host copy). */
 int pm_engine_counters(pm_engine *eng, pm_counters *out);
 
 /* Deterministic synthetic GLF block generator on the device (SURVEY.md section 8(d) recipe):
- * families shaped by the engine's pedigree, 10% polymorphic sites, depth U{8..29}, error 1%. */
+ * families shaped by the engine's pedigree, 10% polymorphic sites, depth U{8..29}, error 1%.
+ * Writes d_pl in the genotype-planar layout of pm_engine_run_device. */
 int pm_engine_synth(pm_engine *eng, int32_t n, uint64_t seed, uint64_t site_offset,
                     uint8_t *d_pl, uint32_t *d_dm, uint8_t *d_ref);
 

@@ -9,5 +9,5 @@ native library is missing.
 from .engine import (  # noqa: F401
     LIB_PATH, BIN_PATH, load_library, Engine, Pedigree, GlfReader, Params, SiteResult, GenoCall, Counters,
     KernelStats, PedigreeStruct, NUM_PRODUCT, NUM_EXACT, NUM_POLY, PM_CHR_AUTO, PM_CHR_X, PM_CHR_Y, PM_CHR_MT, FAM_NUCLEAR, FAM_FOUNDERS,
-    FAM_EXTENDED, synth_write_dataset, synth_block_host, pedigree_from_arrays,
+    FAM_EXTENDED, synth_write_dataset, synth_block_host, planar, pedigree_from_arrays,
 )

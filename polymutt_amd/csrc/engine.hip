@@ -128,6 +128,11 @@ struct DevArgs {
 };
 
 // ------------------------------------------------------------------------------------------------
+// Genotype-planar site block (the engine's HBM layout): a site's 10 x n_person phred bytes are stored
+// plane by plane, plane g holding every person's value for genotype g (AA, AC, ..., TT), so the lanes of a
+// wave -- consecutive persons or families -- read consecutive bytes.  PLB(site block, n_person, person, g).
+#define PLB(pl, np, p, g) (pl)[(size_t)(g) * (np) + (p)]
+
 // small helpers (restating src/PedigreeGLF.h:14-53, core/glfHandler.h:102-106)
 __device__ __forceinline__ int d_gi(int b1, int b2) {
   return b1 < b2 ? (b1 - 1) * (10 - b1) / 2 + (b2 - b1) : (b2 - 1) * (10 - b2) / 2 + (b1 - b2);
@@ -238,10 +243,9 @@ struct ItemCtx {
 template <bool GEN, bool DN = GEN>
 __device__ __forceinline__ void hoist_nuc(const DevArgs& A, const ItemCtx& I, const uint8_t* pl, const double* lk, const double* M,
                                           int p0, int n, double* cond) {
-  const uint8_t* F = pl + (size_t)p0 * 10;
-  const uint8_t* Mo = F + 10;
-  double F11 = lk[F[I.g11]], F12 = lk[F[I.g12]], F22 = lk[F[I.g22]];
-  double M11 = lk[Mo[I.g11]], M12 = lk[Mo[I.g12]], M22 = lk[Mo[I.g22]];
+  const int np = A.n_person;
+  double F11 = lk[PLB(pl, np, p0, I.g11)], F12 = lk[PLB(pl, np, p0, I.g12)], F22 = lk[PLB(pl, np, p0, I.g22)];
+  double M11 = lk[PLB(pl, np, p0 + 1, I.g11)], M12 = lk[PLB(pl, np, p0 + 1, I.g12)], M22 = lk[PLB(pl, np, p0 + 1, I.g22)];
   if (GEN && !I.denovo) {   // CalcParentMarginal :1049-1051
     if (I.chrom == PM_CHR_X) F12 = 0.0;
     if (I.chrom == PM_CHR_Y) { M11 = M12 = M22 = 1.0; F12 = 0.0; }
@@ -251,16 +255,16 @@ __device__ __forceinline__ void hoist_nuc(const DevArgs& A, const ItemCtx& I, co
 #pragma unroll
   for (int k = 0; k < 9; k++) kids[k] = 1.0;
   for (int j = 2; j < n; j++) {
-    const uint8_t* K = pl + (size_t)(p0 + j) * 10;
+    const uint8_t* K = pl + p0 + j;   // person p0 + j of plane 0; plane g at K[g * np]
     if (!DN || !I.denovo) {
-      const double l11 = lk[K[I.g11]], l12 = lk[K[I.g12]], l22 = lk[K[I.g22]];
+      const double l11 = lk[K[(size_t)I.g11 * np]], l12 = lk[K[(size_t)I.g12 * np]], l22 = lk[K[(size_t)I.g22 * np]];
 #pragma unroll
       for (int k = 0; k < 9; k++) kids[k] *= d_one_kid(k, GEN ? I.chrom : (int)PM_CHR_AUTO, I.sex, l11, l12, l22);
     } else {
       double D11 = 0.0, D12 = 0.0, D22 = 0.0;
 #pragma unroll
       for (int g = 0; g < 10; g++) {
-        const double pg = lk[K[g]];
+        const double pg = lk[K[(size_t)g * np]];
         D11 += M[I.g11 * 10 + g] * pg;
         D12 += M[I.g12 * 10 + g] * pg;
         D22 += M[I.g22 * 10 + g] * pg;
@@ -282,8 +286,8 @@ __device__ __forceinline__ int hoist_fp(const DevArgs& A, const ItemCtx& I, cons
   int fl = 0;
   for (int j = 0; j < 3; j++) {
     if (j >= cnt) { cond[3 * j] = cond[3 * j + 1] = cond[3 * j + 2] = 0.0; fl |= 2 << (2 * j); continue; }
-    const uint8_t* R = pl + (size_t)(p + j) * 10;
-    double l11 = lk[R[I.g11]], l12 = lk[R[I.g12]], l22 = lk[R[I.g22]];
+    const int np = A.n_person;
+    double l11 = lk[PLB(pl, np, p + j, I.g11)], l12 = lk[PLB(pl, np, p + j, I.g12)], l22 = lk[PLB(pl, np, p + j, I.g22)];
     const int sx = A.sex[p + j];
     int hap = 0, skip = 0;   // lkSinglePerson :987-1004
     if (I.chrom == PM_CHR_X && sx == MALE) { l12 = 0; hap = 1; }
@@ -328,7 +332,8 @@ __device__ __forceinline__ double d_es_lk(const DevArgs& A, int f, const uint8_t
   for (int i = 0; i < n; i++) {
     const int sx = A.sex[p0 + i];
     const bool fo = A.is_founder[p0 + i] != 0;
-    const uint8_t* R = pl + (size_t)(p0 + i) * 10;
+    const uint8_t* R = pl + p0 + i;   // plane g at R[g * n_person]
+    const size_t np = (size_t)A.n_person;
     if (NS == 3) {
       double pr[3] = {0.0, 0.0, 0.0};
       if (i < nf) {
@@ -339,7 +344,7 @@ __device__ __forceinline__ double d_es_lk(const DevArgs& A, int f, const uint8_t
       }
 #pragma unroll
       for (int j = 0; j < 3; j++) {
-        const double pen = (zp == i && gidx[j] != zg) ? 0.0 : lk[R[gidx[j]]];
+        const double pen = (zp == i && gidx[j] != zg) ? 0.0 : lk[R[gidx[j] * np]];
         PP(i, j) = (Y && sx == FEMALE) ? 1.0 : (fo ? pr[j] * pen : pen);
       }
     } else {
@@ -357,7 +362,7 @@ __device__ __forceinline__ double d_es_lk(const DevArgs& A, int f, const uint8_t
       }
 #pragma unroll
       for (int j = 0; j < 10; j++) {
-        const double pen = (zp == i && j != zg) ? 0.0 : lk[R[j]];
+        const double pen = (zp == i && j != zg) ? 0.0 : lk[R[j * np]];
         PP(i, j) = fo ? pr[j] * pen : pen;
       }
     }
@@ -563,6 +568,10 @@ template <int S, int T>
 __device__ __forceinline__ void hoist_poly4(const DevArgs& A, const ItemCtx& I, const uint8_t* pl, const double* lk,
                                             double (*a)[5], unsigned& live) {
   constexpr int C = S < PM_HOIST_CHUNK ? S : PM_HOIST_CHUNK;
+  const size_t np = (size_t)A.n_person;
+  const uint8_t* P11 = pl + I.g11 * np;   // the three genotype planes of the item
+  const uint8_t* P12 = pl + I.g12 * np;
+  const uint8_t* P22 = pl + I.g22 * np;
 #pragma unroll
   for (int c0 = 0; c0 < S; c0 += C) {
     uint32_t by[C][12];
@@ -572,14 +581,13 @@ __device__ __forceinline__ void hoist_poly4(const DevArgs& A, const ItemCtx& I, 
       const int4 u = A.units[(c0 + j) * T + threadIdx.x];
       const bool nuc = u.x == U_NUC;
       nn[j] = nuc ? u.w : 0;
-      const uint8_t* F = pl + (size_t)u.z * 10;
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const bool ok = q < nn[j];
-        const uint8_t* R = F + (ok ? q * 10 : 0);
-        by[j][3 * q + 0] = ok ? R[I.g11] : 0;
-        by[j][3 * q + 1] = ok ? R[I.g12] : 0;
-        by[j][3 * q + 2] = ok ? R[I.g22] : 0;
+        const int pp = u.z + (ok ? q : 0);
+        by[j][3 * q + 0] = ok ? P11[pp] : 0;
+        by[j][3 * q + 1] = ok ? P12[pp] : 0;
+        by[j][3 * q + 2] = ok ? P22[pp] : 0;
       }
       if (nuc) live |= 1u << (c0 + j);
     }
@@ -621,6 +629,7 @@ template <int S, int T>
 __device__ __forceinline__ void hoist_poly4_dn(const DevArgs& A, const ItemCtx& I, const uint8_t* pl, const double* lk,
                                                const double* M, double (*a)[5], unsigned& live) {
   constexpr int C = S < PM_HOIST_CHUNK_DN ? S : PM_HOIST_CHUNK_DN;
+  const size_t np = (size_t)A.n_person;
 #pragma unroll
   for (int c0 = 0; c0 < S; c0 += C) {
     uint32_t par[C][6], kid[C][2][10];
@@ -634,21 +643,20 @@ __device__ __forceinline__ void hoist_poly4_dn(const DevArgs& A, const ItemCtx& 
       const int4 u = A.units[(c0 + j) * T + threadIdx.x];
       const bool nuc = u.x == U_NUC;
       nn[j] = nuc ? u.w : 0;
-      const uint8_t* F = pl + (size_t)u.z * 10;
 #pragma unroll
       for (int q = 0; q < 2; q++) {
         const bool ok = q < nn[j];
-        const uint8_t* R = F + (ok ? q * 10 : 0);
-        par[j][3 * q + 0] = ok ? R[I.g11] : 0;
-        par[j][3 * q + 1] = ok ? R[I.g12] : 0;
-        par[j][3 * q + 2] = ok ? R[I.g22] : 0;
+        const uint8_t* R = pl + u.z + (ok ? q : 0);
+        par[j][3 * q + 0] = ok ? R[I.g11 * np] : 0;
+        par[j][3 * q + 1] = ok ? R[I.g12 * np] : 0;
+        par[j][3 * q + 2] = ok ? R[I.g22 * np] : 0;
       }
 #pragma unroll
       for (int q = 0; q < 2; q++) {
         const bool ok = q + 2 < nn[j];
-        const uint8_t* R = F + (ok ? (q + 2) * 10 : 0);
+        const uint8_t* R = pl + u.z + (ok ? q + 2 : 0);
 #pragma unroll
-        for (int g = 0; g < 10; g++) kid[j][q][g] = ok ? R[g] : 0;
+        for (int g = 0; g < 10; g++) kid[j][q][g] = ok ? R[g * np] : 0;
       }
       if (nuc) live |= 1u << (c0 + j);
     }
@@ -816,7 +824,7 @@ __device__ __forceinline__ double block_logprod(double m, int e, double* red, in
 // Occupancy target (waves per SIMD) of a Brent flavour: the lean polynomial kernel keeps 5 doubles per
 // family, so even at S=16 two items fit on a SIMD if the hoisting phase is kept from spreading out.
 template <int T, int S, int NUM, bool GEN>
-constexpr int brent_waves() { return (NUM == PM_NUM_POLY && !GEN && T == 64 && S >= 8) ? PM_POLY_WAVES : 1; }
+constexpr int brent_waves() { return (NUM == PM_NUM_POLY && !GEN && (T == 64 || T == 128) && S >= 8) ? PM_POLY_WAVES : 1; }
 
 // DN: lean polynomial kernel for autosomal --denovo (instantiated separately so the common kernel carries
 // no de novo hoisting code or register pressure).
@@ -997,22 +1005,31 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
 }
 
 // ------------------------------------------------------------------------------------------------
-// In-order accumulation of one wave's 64 per-lane terms into a running sum held by every lane:
-// s = (((s + t_0) + t_1) + ... + t_63), lanes in ascending order -- the reference's serial loop order.
-// Lanes whose term is an exact zero are skipped: adding +-0.0 never changes a running sum that is not
-// -0.0 (the sums here start at +0.0), so the result is bit-identical to the full serial loop.
-__device__ __forceinline__ double wave_serial_add(double s, double t, bool nz) {
-  unsigned long long m = __ballot(nz);
-  while (m) {
-    const int l = __ffsll((long long)m) - 1;
-    m &= m - 1;
-    s += __shfl(t, l, 64);
-  }
-  return s;
+// k_prep: one wave per site.  CalcReadStats (integer sums, order-free) and MonomorphismLogLikelihood
+// (serial double sum, kept in the reference's person order) -- NucFamGenotypeLikelihood.cpp:502-546.
+// k_prep per-lane loads: VEC consecutive persons per lane and iteration, fetched with vector loads (16 B
+// of dm, VEC bytes of a genotype plane) so each wave keeps several KB in flight -- the loop is HBM-latency
+// bound otherwise.  VEC = 16/8/4 needs n_person % VEC == 0 (all block offsets then stay 16-B aligned).
+template <int VEC>
+__device__ __forceinline__ void load_bytes(const uint8_t* p, uint8_t* out) {
+  if constexpr (VEC == 16) { const uint4 v = *(const uint4*)p; memcpy(out, &v, 16); }
+  else if constexpr (VEC == 8) { const uint2 v = *(const uint2*)p; memcpy(out, &v, 8); }
+  else if constexpr (VEC == 4) { const uint32_t v = *(const uint32_t*)p; memcpy(out, &v, 4); }
+  else out[0] = p[0];
+}
+template <int VEC>
+__device__ __forceinline__ void load_dwords(const uint32_t* p, uint32_t* out) {
+  if constexpr (VEC >= 4) {
+#pragma unroll
+    for (int q = 0; q < VEC / 4; q++) { const uint4 v = ((const uint4*)p)[q]; out[4 * q] = v.x; out[4 * q + 1] = v.y; out[4 * q + 2] = v.z; out[4 * q + 3] = v.w; }
+  } else out[0] = p[0];
 }
 
 // k_prep: one wave per site.  CalcReadStats (integer sums, order-free) and MonomorphismLogLikelihood
-// (serial double sum, kept in the reference's person order) -- NucFamGenotypeLikelihood.cpp:502-546.
+// (NucFamGenotypeLikelihood.cpp:502-546).  SERIAL (PM_NUM_EXACT): the mono sum -PL/10 is accumulated in
+// the reference's person order (VEC = 1, lanes ascending via ballot); otherwise it is -(Sum PL)/10 from
+// the exact integer sum -- correctly rounded, within ~1e-14 relative of the serial sum.
+template <int VEC, bool SERIAL>
 __global__ void __launch_bounds__(256) k_prep(DevArgs A) {
   __shared__ unsigned long long s_c[9];
   __shared__ double s_lk[256];
@@ -1035,7 +1052,7 @@ __global__ void __launch_bounds__(256) k_prep(DevArgs A) {
     const uint32_t* dm = A.dm + (size_t)site * np;
     const bool okref = r >= 1 && r <= 4 && (!A.vcf || (alt >= 1 && alt <= 4 && alt != r));
     const int h = okref ? d_gi(r, r) : 0;
-    long long dsum = 0, mqsum = 0, nsd = 0;
+    long long dsum = 0, mqsum = 0, nsd = 0, plsum = 0;
     double mono = 0.0;
     // lean --denovo: MonomorphismLogLikelihood_denovo (the cfg-0 item: CalcAllFamLogLikelihood at f = 1).
     // SetParentPrior(1) = (1, 0, ..., 0), so each nuclear family contributes cond[0] = (Prod_kids
@@ -1044,26 +1061,52 @@ __global__ void __launch_bounds__(256) k_prep(DevArgs A) {
     const bool mdn = A.mono_dn && okref;
     double dm_m = 1.0;
     int dm_e = 0;
-    for (int base = 0; base < np; base += 64) {
-      const int p = base + lane;
-      uint32_t x = 0;
-      int hr = 0;
-      if (p < np) { x = dm[p]; hr = pl[(size_t)p * 10 + h]; }
-      const int d = (int)(x & 0xFFFFFF);
-      dsum += d; mqsum += (x >> 24); nsd += d > 0;
-      mono = wave_serial_add(mono, -(double)hr / 10, hr != 0);
-      if (mdn && p < np) {
-        double fct;
-        if (A.is_founder[p]) fct = s_lk[hr];
-        else {
-          const uint8_t* K = pl + (size_t)p * 10;
-          fct = 0.0;
+    const uint8_t* plane_h = pl + (size_t)h * np;
+    for (int base = 0; base < np; base += 64 * VEC) {
+      const int p0 = base + lane * VEC;
+      uint32_t x[VEC];
+      uint8_t hr[VEC];
+      if (p0 < np) {   // np % VEC == 0: a lane's VEC persons are all present or all absent
+        load_dwords<VEC>(dm + p0, x);
+        load_bytes<VEC>(plane_h + p0, hr);
+      } else {
 #pragma unroll
-          for (int g = 0; g < 10; g++) fct += s_M[h * 10 + g] * s_lk[K[g]];
+        for (int k = 0; k < VEC; k++) { x[k] = 0; hr[k] = 0; }
+      }
+#pragma unroll
+      for (int k = 0; k < VEC; k++) {
+        const int d = (int)(x[k] & 0xFFFFFF);
+        dsum += d; mqsum += (x[k] >> 24); nsd += d > 0;
+        plsum += hr[k];
+      }
+      if constexpr (SERIAL) {   // VEC == 1: lanes in ascending person order
+        unsigned long long m = __ballot(hr[0] != 0);   // zero terms add -0.0: no change to a sum starting at +0.0
+        const double t = -(double)hr[0] / 10;
+        while (m) {
+          const int l = __ffsll((long long)m) - 1;
+          m &= m - 1;
+          mono += __shfl(t, l, 64);
         }
-        int xe;
-        dm_m = frexp(dm_m * fct, &xe);
-        dm_e += xe;
+      }
+      if (mdn && p0 < np) {
+        uint8_t fo[VEC];
+        load_bytes<VEC>((const uint8_t*)A.is_founder + p0, fo);
+        uint8_t kb[10][VEC];
+#pragma unroll
+        for (int g = 0; g < 10; g++) load_bytes<VEC>(pl + (size_t)g * np + p0, kb[g]);
+#pragma unroll
+        for (int k = 0; k < VEC; k++) {
+          double fct;
+          if (fo[k]) fct = s_lk[hr[k]];
+          else {
+            fct = 0.0;
+#pragma unroll
+            for (int g = 0; g < 10; g++) fct += s_M[h * 10 + g] * s_lk[kb[g][k]];
+          }
+          int xe;
+          dm_m = frexp(dm_m * fct, &xe);
+          dm_e += xe;
+        }
       }
     }
     if (mdn) {
@@ -1074,6 +1117,11 @@ __global__ void __launch_bounds__(256) k_prep(DevArgs A) {
         A.minv[site * 8] = 0.0;
         A.evals[site * 8] = 1;
       }
+    }
+    if constexpr (!SERIAL) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) plsum += __shfl_xor(plsum, o, 64);
+      mono = plsum ? -(double)plsum / 10 : 0.0;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) { dsum += __shfl_xor(dsum, o, 64); mqsum += __shfl_xor(mqsum, o, 64); nsd += __shfl_xor(nsd, o, 64); }
@@ -1341,13 +1389,12 @@ __device__ __forceinline__ void d_emit_call(pm_geno_call* C, const double* post,
 }
 
 // likelihoodKidGenotype, :1334-1443
-__device__ void d_kid_geno(int chrom, const uint8_t* pl, const double* lk, int p0, int n, const int8_t* sexv, int g11, int g12, int g22,
-                           int kid, int k, double* out) {
+__device__ void d_kid_geno(int chrom, const uint8_t* pl, int np, const double* lk, int p0, int n, const int8_t* sexv, int g11, int g12,
+                           int g22, int kid, int k, double* out) {
   const bool X = chrom == PM_CHR_X, Y = chrom == PM_CHR_Y, MT = chrom == PM_CHR_MT;
   double G11 = 1.0, G12 = 1.0, G22 = 1.0, l = 0.0, q11 = 0, q12 = 0, q22 = 0;
   for (int i = 2; i < n; i++) {
-    const uint8_t* R = pl + (size_t)(p0 + i) * 10;
-    const double l11 = lk[R[g11]], l12 = lk[R[g12]], l22 = lk[R[g22]];
+    const double l11 = lk[PLB(pl, np, p0 + i, g11)], l12 = lk[PLB(pl, np, p0 + i, g12)], l22 = lk[PLB(pl, np, p0 + i, g22)];
     const int sex = sexv[p0 + i];
     switch (k) {
       case 0: l = l11; q11 = l11; q12 = q22 = 0; break;
@@ -1434,8 +1481,7 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
       if (kind == PM_FAM_FOUNDERS) {
         for (int j = 0; j < n; j++) {   // CalcPostProb_SinglePerson :754-795
           const int p = p0 + j, sx = A.sex[p];
-          const uint8_t* Rr = pl + (size_t)p * 10;
-          const double l11 = s_lk[Rr[g11]], l12 = s_lk[Rr[g12]], l22 = s_lk[Rr[g22]];
+          const double l11 = s_lk[PLB(pl, np, p, g11)], l12 = s_lk[PLB(pl, np, p, g12)], l22 = s_lk[PLB(pl, np, p, g22)];
           const double fq = freq, gq = 1 - freq;
           double pr0 = fq * fq, pr1 = fq * gq * 2, pr2 = gq * gq;
           if (chrom == PM_CHR_X) { if (sx == MALE) { pr0 = fq; pr1 = 0.; pr2 = 1 - fq; } else { pr0 = fq * fq; pr1 = 2 * fq * gq; pr2 = gq * gq; } }
@@ -1497,10 +1543,8 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
       else pmode = chrom == PM_CHR_X ? PR_X : chrom == PM_CHR_Y ? PR_Y : chrom == PM_CHR_MT ? PR_MT : PR_AUTO;
       d_parent_prior(pmode, freq, pp);
       {
-        const uint8_t* F = pl + (size_t)p0 * 10;
-        const uint8_t* Mo = F + 10;
-        double F11 = s_lk[F[g11]], F12 = s_lk[F[g12]], F22 = s_lk[F[g22]];
-        double M11 = s_lk[Mo[g11]], M12 = s_lk[Mo[g12]], M22 = s_lk[Mo[g22]];
+        double F11 = s_lk[PLB(pl, np, p0, g11)], F12 = s_lk[PLB(pl, np, p0, g12)], F22 = s_lk[PLB(pl, np, p0, g22)];
+        double M11 = s_lk[PLB(pl, np, p0 + 1, g11)], M12 = s_lk[PLB(pl, np, p0 + 1, g12)], M22 = s_lk[PLB(pl, np, p0 + 1, g22)];
         if (!dn) {
           if (chrom == PM_CHR_X) F12 = 0.0;
           if (chrom == PM_CHR_Y) { M11 = M12 = M22 = 1.0; F12 = 0.0; }
@@ -1527,7 +1571,7 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
         } else if (!dn) {   // KidJointGenoLikelihood :798-835
           double J[9][3];
           for (int k = 0; k < 9; k++) {
-            d_kid_geno(chrom, pl, s_lk, p0, n, A.sex, g11, g12, g22, j, k, J[k]);
+            d_kid_geno(chrom, pl, np, s_lk, p0, n, A.sex, g11, g12, g22, j, k, J[k]);
             const double w = pg[k] * pp[k];
             J[k][0] *= w; J[k][1] *= w; J[k][2] *= w;
           }
@@ -1546,11 +1590,11 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
             double Jk[10];
             for (int t = 0; t < 10; t++) Jk[t] = 1.0;
             for (int i = 2; i < n; i++) {
-              const uint8_t* K = pl + (size_t)(p0 + i) * 10;
+              const uint8_t* K = pl + p0 + i;   // plane g at K[g * np]
               if (i != j) {
                 double D11 = 0.0, D12 = 0.0, D22 = 0.0;
                 for (int gg = 0; gg < 10; gg++) {
-                  const double pv = s_lk[K[gg]];
+                  const double pv = s_lk[K[(size_t)gg * np]];
                   D11 += s_M[g11 * 10 + gg] * pv; D12 += s_M[g12 * 10 + gg] * pv; D22 += s_M[g22 * 10 + gg] * pv;
                 }
                 const double l = d_one_kid_dn(k, D11, D12, D22);
@@ -1566,7 +1610,7 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
                     case 5: case 7: mm = 0.5 * s_M[g12 * 10 + t] + 0.5 * s_M[g22 * 10 + t]; break;
                     default: mm = s_M[g22 * 10 + t]; break;
                   }
-                  Jk[t] *= mm * s_lk[K[t]];
+                  Jk[t] *= mm * s_lk[K[(size_t)t * np]];
                 }
               }
             }
@@ -1608,8 +1652,7 @@ __global__ void __launch_bounds__(256) k_ab(DevArgs A) {
     double Asum = 0.0, Bsum = 0.0;
     for (int p = lane; p < np; p += 64) {
       const int depth = (int)(dm[p] & 0xFFFFFF);
-      const uint8_t* Rr = pl + (size_t)p * 10;
-      const int k11 = Rr[g11], k12 = Rr[g12], k22 = Rr[g22];
+      const int k11 = PLB(pl, np, p, g11), k12 = PLB(pl, np, p, g12), k22 = PLB(pl, np, p, g22);
       const double l11 = s_lk[k11], l12 = s_lk[k12], l22 = s_lk[k22];
       const double PHet = (p12 * l12) / (p11 * l11 + p12 * l12 + p22 * l22);
       if (PHet > 1e-05 && depth > 0) {
@@ -1669,8 +1712,22 @@ __global__ void k_synth(DevArgs A, int n, uint64_t seed, uint64_t off, uint8_t* 
   const int s = A.fam_start[f], cnt = A.fam_start[f + 1] - s;
   uint8_t hap[32];
   if (cnt > 32) return;
+  // genotype-planar site block: person s + j, genotype k at pl[i * 10 * np + k * np + s + j]
   pm_syn_family(A.syn, seed, off + (uint64_t)i, r, af, cnt, A.fa_local + s, A.mo_local + s, (uint64_t)s,
-                pl + ((size_t)i * A.n_person + s) * 10, dm + (size_t)i * A.n_person + s, hap);
+                pl + (size_t)i * A.n_person * 10 + s, 1, (size_t)A.n_person, dm + (size_t)i * A.n_person + s, hap);
+}
+
+// person-major GLF records [site][person][10] -> genotype-planar site blocks [site][10][person]: thread per
+// (site, person); consecutive threads write consecutive bytes of each plane
+__global__ void k_to_planar(int n, int np, const uint8_t* __restrict__ src, uint8_t* __restrict__ dst) {
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long long)n * np) return;
+  const long long site = gid / np;
+  const int p = (int)(gid - site * np);
+  const uint8_t* r = src + (size_t)gid * 10;
+  uint8_t* d = dst + (size_t)site * np * 10 + p;
+#pragma unroll
+  for (int g = 0; g < 10; g++) d[(size_t)g * np] = r[g];
 }
 
 // ================================================================================================
@@ -1700,6 +1757,7 @@ struct pm_engine {
   double *d_lktab = nullptr, *d_M = nullptr;
   pm_synth_tables* d_syn = nullptr;
   uint8_t *d_pl = nullptr, *d_ref = nullptr;
+  uint8_t* d_stage = nullptr;   // person-major staging block of pm_engine_run (transposed into d_pl)
   uint32_t* d_dm = nullptr;
   pm_site_result* d_res = nullptr;
   pm_geno_call* d_calls = nullptr;
@@ -1877,7 +1935,7 @@ void pm_engine_destroy(pm_engine* E) {
   void* bufs[] = {E->d_units1, E->d_ext_count1, E->d_ext_fam1, E->d_fam_founders, E->d_peel_start, E->d_ext_count, E->d_ext_fam, E->d_is_founder, E->d_steps, E->d_T10,
                   E->d_T10dn, E->d_ws, E->d_units_q,
                   E->d_fam_start, E->d_fam_kind, E->d_fa, E->d_mo, E->d_sex, E->d_units, E->d_lktab, E->d_M, E->d_syn,
-                  E->d_pl, E->d_ref, E->d_dm, E->d_res, E->d_calls, E->d_raw, E->d_minv, E->d_mono, E->d_evals,
+                  E->d_pl, E->d_stage, E->d_ref, E->d_dm, E->d_res, E->d_calls, E->d_raw, E->d_minv, E->d_mono, E->d_evals,
                   E->d_item_sex, E->d_items[0], E->d_items[1], E->d_items[2], E->d_counts, E->d_eval_total, E->d_row_site,
                   E->d_counters};
   for (void* b : bufs) if (b) hipFree(b);
@@ -2105,6 +2163,7 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
   // batch buffers
   const size_t nb = (size_t)max_batch, np = (size_t)ped->n_person;
   DALLOC(E->d_pl, nb * np * 10);
+  DALLOC(E->d_stage, nb * np * 10);
   DALLOC(E->d_dm, nb * np);
   DALLOC(E->d_ref, nb);
   DALLOC(E->d_res, nb);
@@ -2262,7 +2321,15 @@ static int run_pipeline(pm_engine* E, int n, const uint8_t* pl, const uint32_t* 
     const int big = 0x7fffffff;   // counts[4] = first emitted site (atomicMin)
     HIP_TRY(hipMemcpyAsync(E->d_counts + 4, &big, sizeof(int), hipMemcpyHostToDevice, E->stream));
   }
-  hipLaunchKernelGGL(k_prep, dim3((n + 3) / 4), dim3(256), 0, E->stream, A);
+  {   // persons per lane of k_prep: vector loads when n_person allows; the reference's serial mono order in EXACT
+    const int np = E->n_person;
+    int vmax = 8;   // measured best on 1000 quads (16 and 4 within 1%)
+    if (const char* ev = getenv("PM_PREP_VEC")) vmax = atoi(ev);   // geometry experiments
+    void (*prep)(DevArgs) = E->par.numerics == PM_NUM_EXACT ? k_prep<1, true>
+                          : (np % 16 == 0 && vmax >= 16) ? k_prep<16, false> : (np % 8 == 0 && vmax >= 8) ? k_prep<8, false>
+                          : (np % 4 == 0 && vmax >= 4) ? k_prep<4, false> : k_prep<1, false>;
+    hipLaunchKernelGGL(prep, dim3((n + 3) / 4), dim3(256), 0, E->stream, A);
+  }
   HIP_TRY(hipGetLastError());
   int rc;
   const int tb = 256, gb = (n + tb - 1) / tb;
@@ -2353,16 +2420,18 @@ int pm_engine_run(pm_engine* E, int32_t n, const uint8_t* pl, const uint32_t* dm
   if (n == 0) return PM_OK;
   HIP_TRY(hipSetDevice(E->device));
   const size_t np = E->n_person;
-  const uint8_t* dpl = pl;
+  const uint8_t* spl = pl;   // person-major GLF records (host or device)
   const uint32_t* ddm = dm;
   const uint8_t* dref = ref;
   if (!on_device) {
-    HIP_TRY(hipMemcpyAsync(E->d_pl, pl, (size_t)n * np * 10, hipMemcpyHostToDevice, E->stream));
+    HIP_TRY(hipMemcpyAsync(E->d_stage, pl, (size_t)n * np * 10, hipMemcpyHostToDevice, E->stream));
     HIP_TRY(hipMemcpyAsync(E->d_dm, dm, (size_t)n * np * 4, hipMemcpyHostToDevice, E->stream));
     HIP_TRY(hipMemcpyAsync(E->d_ref, ref, (size_t)n, hipMemcpyHostToDevice, E->stream));
-    dpl = E->d_pl; ddm = E->d_dm; dref = E->d_ref;
+    spl = E->d_stage; ddm = E->d_dm; dref = E->d_ref;
   }
-  int rc = run_pipeline(E, n, dpl, ddm, dref, E->d_res, E->d_calls);
+  int rc = pm_engine_to_planar(E, n, spl, E->d_pl);   // the engine's genotype-planar layout
+  if (rc) return rc;
+  rc = run_pipeline(E, n, E->d_pl, ddm, dref, E->d_res, E->d_calls);
   if (rc) return rc;
   rc = pm_engine_sync(E);
   if (rc) return rc;
@@ -2372,6 +2441,17 @@ int pm_engine_run(pm_engine* E, int32_t n, const uint8_t* pl, const uint32_t* dm
   *n_rows = counts[3];
   if (calls && counts[3] > 0)
     HIP_TRY(hipMemcpy(calls, E->d_calls, sizeof(pm_geno_call) * np * counts[3], hipMemcpyDeviceToHost));
+  return PM_OK;
+}
+
+int pm_engine_to_planar(pm_engine* E, int32_t n, const uint8_t* d_src, uint8_t* d_dst) {
+  if (!E || n < 0 || !d_src || !d_dst || d_src == d_dst) { pm_set_last_error("pm_engine_to_planar: invalid arguments"); return PM_EINVAL; }
+  if (n == 0) return PM_OK;
+  HIP_TRY(hipSetDevice(E->device));
+  const long long total = (long long)n * E->n_person;
+  const int tb = 256;
+  hipLaunchKernelGGL(k_to_planar, dim3((unsigned)((total + tb - 1) / tb)), dim3(tb), 0, E->stream, n, E->n_person, d_src, d_dst);
+  HIP_TRY(hipGetLastError());
   return PM_OK;
 }
 

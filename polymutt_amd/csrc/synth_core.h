@@ -54,10 +54,11 @@ PM_HD static inline void pm_syn_site(uint64_t seed, uint64_t site, int* ref, dou
 
 // One family's persons (path order, parents before children).  gbase = global index of the
 // family's first person (used as the RNG person key).  fa/mo are family-local parent indices (-1 for
-// founders).  Writes pl[j*10..], dm[j].
+// founders).  Writes person j's genotype k at pl[j * ps + k * gs] (ps = 10, gs = 1: person-major GLF
+// records; ps = 1, gs = n_person: the engine's genotype-planar site block) and dm[j].
 PM_HD static inline void pm_syn_family(const pm_synth_tables* T, uint64_t seed, uint64_t site, int ref, double af, int n,
-                                       const int32_t* fa, const int32_t* mo, uint64_t gbase, uint8_t* pl, uint32_t* dm,
-                                       uint8_t* hap /* scratch [n] */) {
+                                       const int32_t* fa, const int32_t* mo, uint64_t gbase, uint8_t* pl, size_t ps, size_t gs,
+                                       uint32_t* dm, uint8_t* hap /* scratch [n] */) {
   const int alt = pm_syn_ts(ref);
   const int i0 = pm_syn_gi(ref, ref), i1 = pm_syn_gi(ref, alt), i2 = pm_syn_gi(alt, alt);
   for (int j = 0; j < n; j++) {
@@ -77,11 +78,11 @@ PM_HD static inline void pm_syn_family(const pm_synth_tables* T, uint64_t seed, 
     const double u = pm_u01(seed, site, key, 5);
     int nalt = 0;
     while (nalt < depth && u >= T->cdf[g][depth][nalt]) nalt++;
-    uint8_t* rec = pl + (size_t)j * 10;
-    for (int k = 0; k < 10; k++) rec[k] = 255;
-    rec[i0] = T->pl[depth][nalt][0];
-    rec[i1] = T->pl[depth][nalt][1];
-    rec[i2] = T->pl[depth][nalt][2];
+    uint8_t* rec = pl + (size_t)j * ps;
+    for (int k = 0; k < 10; k++) rec[k * gs] = 255;
+    rec[i0 * gs] = T->pl[depth][nalt][0];
+    rec[i1 * gs] = T->pl[depth][nalt][1];
+    rec[i2 * gs] = T->pl[depth][nalt][2];
     dm[j] = (uint32_t)depth | (60u << 24);
   }
 }

@@ -98,6 +98,7 @@ EXPORTS = {
     "pm_engine_run": (i32, [C.c_void_p, i32, C.c_void_p, C.c_void_p, C.c_void_p, i32, C.c_void_p, C.c_void_p, P(i32)]),
     "pm_engine_run_device": (i32, [C.c_void_p, i32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "pm_engine_sync": (i32, [C.c_void_p]),
+    "pm_engine_to_planar": (i32, [C.c_void_p, i32, C.c_void_p, C.c_void_p]),
     "pm_engine_counters": (i32, [C.c_void_p, P(Counters)]),
     "pm_engine_synth": (i32, [C.c_void_p, i32, u64, u64, C.c_void_p, C.c_void_p, C.c_void_p]),
     "pm_device_alloc": (i32, [C.c_void_p, u64, P(C.c_void_p)]),
@@ -250,7 +251,12 @@ class Engine:
         return res, calls[: rows.value]
 
     def run_device(self, n, d_pl, d_dm, d_ref, d_res=None, d_calls=None):
+        """d_pl in the engine's genotype-planar layout [n][10][n_person] (pm_engine_synth, to_planar)."""
         self._check(self.lib.pm_engine_run_device(self.h, n, d_pl, d_dm, d_ref, d_res, d_calls))
+
+    def to_planar(self, n, d_src, d_dst):
+        """Person-major device block [n][n_person][10] -> genotype-planar [n][10][n_person]."""
+        self._check(self.lib.pm_engine_to_planar(self.h, n, d_src, d_dst))
 
     def sync(self):
         self._check(self.lib.pm_engine_sync(self.h))
@@ -340,8 +346,15 @@ def synth_write_dataset(directory, shape, n_fam, n_sites, seed):
         raise RuntimeError(_err(lib))
 
 
+def planar(pl):
+    """Person-major [n][n_person][10] -> the engine's genotype-planar [n][10][n_person] (numpy)."""
+    n = pl.shape[0]
+    return np.ascontiguousarray(np.asarray(pl).reshape(n, -1, 10).transpose(0, 2, 1))
+
+
 def synth_block_host(ped_struct, n, seed, site_offset=0):
-    """Host-side generation of the dense block pm_engine_synth writes on the device (same RNG)."""
+    """Host-side generation of the sites pm_engine_synth writes on the device (same RNG), as person-major
+    GLF records [n][n_person][10] (pm_engine_run's layout; planar(pl) gives the device layout)."""
     lib = load_library()
     npers = ped_struct.n_person
     pl = np.zeros((n, npers, 10), np.uint8)

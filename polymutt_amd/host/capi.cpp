@@ -114,7 +114,7 @@ int pmh_synth_block(const pm_pedigree* ped, int32_t n, uint64_t seed, uint64_t o
     ref[i] = (uint8_t)r;
     for (int f = 0; f < ped->n_fam; f++) {
       int s = ped->fam_start[f], cnt = ped->fam_start[f + 1] - s;
-      pm_syn_family(&T, seed, off + i, r, af, cnt, fa.data() + s, mo.data() + s, (uint64_t)s, pl + ((size_t)i * np + s) * 10,
+      pm_syn_family(&T, seed, off + i, r, af, cnt, fa.data() + s, mo.data() + s, (uint64_t)s, pl + ((size_t)i * np + s) * 10, 10, 1,
                     dm + (size_t)i * np + s, hap.data());
     }
   }

@@ -130,7 +130,7 @@ int synth_write_dataset(const std::string& dir, const std::string& shape_arg, in
       int n = (int)F.size();
       fa.resize(n); mo.resize(n); pl.resize((size_t)n * 10); dm.resize(n); hap.resize(n);
       for (int j = 0; j < n; j++) { fa[j] = F[j].fa; mo[j] = F[j].mo; }
-      pm_syn_family(&T, seed, (uint64_t)s, ref, af, n, fa.data(), mo.data(), gbase[f], pl.data(), dm.data(), hap.data());
+      pm_syn_family(&T, seed, (uint64_t)s, ref, af, n, fa.data(), mo.data(), gbase[f], pl.data(), 10, 1, dm.data(), hap.data());
       if (plant && pm_u01(seed, (uint64_t)s, 0, 901) < 0.03 &&
           (int)(pm_u01(seed, (uint64_t)s, 0, 902) * nfam) == f) {
         int kids[64], nk = 0;

@@ -103,9 +103,17 @@ def test_synthetic_device_generator_and_parity(built, shape, nfam, nsites, tmp_p
     eng = pm.Engine(ped.view, pm.Params.defaults(), max_batch=nsites)
     d_pl, d_dm, d_ref = eng.alloc(pl.nbytes), eng.alloc(dm.nbytes), eng.alloc(ref.nbytes)
     eng.synth(nsites, 7, 0, d_pl, d_dm, d_ref)
-    gpl, gdm, gref = np.zeros_like(pl), np.zeros_like(dm), np.zeros_like(ref)
+    gpl, gdm, gref = np.zeros_like(pm.planar(pl)), np.zeros_like(dm), np.zeros_like(ref)
     eng.to_host(gpl, d_pl, pl.nbytes); eng.to_host(gdm, d_dm, dm.nbytes); eng.to_host(gref, d_ref, ref.nbytes)
-    assert (gpl == pl).all() and (gdm == dm).all() and (gref == ref).all()
+    assert (gpl == pm.planar(pl)).all() and (gdm == dm).all() and (gref == ref).all()   # planar device layout
+    # pm_engine_to_planar: person-major device block -> the same planar block
+    d_pm, d_pl2 = eng.alloc(pl.nbytes), eng.alloc(pl.nbytes)
+    eng.to_device(d_pm, pl, pl.nbytes)
+    eng.to_planar(nsites, d_pm, d_pl2)
+    gpl2 = np.zeros_like(gpl)
+    eng.to_host(gpl2, d_pl2, pl.nbytes)
+    assert (gpl2 == gpl).all()
+    eng.free(d_pm); eng.free(d_pl2)
     for p in (d_pl, d_dm, d_ref):
         eng.free(p)
     eng.close()
