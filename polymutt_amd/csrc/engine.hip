@@ -97,6 +97,7 @@ struct DevArgs {
   int vcf;                 // vcf_mode: one (ref, alt) Brent per site, FamilyLikelihoodSeq_VCF family rules
   int nuc_es;              // nuclear families are peeled (vcf_mode plan 1)
   int mono_dn;             // k_prep computes the de novo monomorphism item (cfg 0) itself (lean --denovo)
+  int pf_npad;             // lean kernel: > 0 = the item's 3 genotype planes are prefetched into LDS (stride)
   // tables
   const double* lktab;     // [256]
   const double* M;         // [100] genotype mutation matrix
@@ -618,6 +619,83 @@ __device__ __forceinline__ void hoist_poly4(const DevArgs& A, const ItemCtx& I, 
   }
 }
 
+// Item -> allele pair (cfg_alleles, the VCF path's (ref, alt), the cfg-7 re-optimisation's alleles).
+__device__ __forceinline__ void item_alleles(const DevArgs& A, int site, int cfg, int r, int* a1, int* a2) {
+  if (A.vcf) { *a1 = r & 15; *a2 = r >> 4; }
+  else if (cfg == 7) { *a1 = A.res[site].allele1; *a2 = A.res[site].allele2; }
+  else cfg_alleles(cfg, r, a1, a2);
+}
+
+// Lean-kernel plane prefetch: the three genotype planes (g11, g12, g22) of an item's site block are
+// copied into this wave's LDS buffer with LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave-instruction,
+// no VGPRs), issued right after the previous item's hoisting so the copy runs under that item's Brent
+// evaluations.  Needs n_person % 16 == 0 (16-B aligned planes); lanes past a plane's end re-read its
+// last 16 bytes (never used), so no access leaves the site block.
+__device__ __forceinline__ void prefetch_planes(const DevArgs& A, const int* items, int it, int nItems, uint8_t* buf) {
+  if (it >= nItems) return;
+  const int item = items[it];
+  const int site = item >> 3, cfg = item & 7;
+  int a1, a2;
+  item_alleles(A, site, cfg, A.ref[site], &a1, &a2);
+  const int np = A.n_person, npad = A.pf_npad;
+  const int gs[3] = {d_gi(a1, a1), d_gi(a1, a2), d_gi(a2, a2)};
+  const uint8_t* base = A.pl + (size_t)site * np * 10;
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const uint8_t* plane = base + (size_t)gs[k] * np;
+    for (int c = 0; c < npad; c += 1024) {
+      const int off = min(c + lane * 16, np - 16);
+      __builtin_amdgcn_global_load_lds((const void*)(plane + off), (void*)(buf + k * npad + c), 16, 0, 0);
+    }
+  }
+}
+
+// hoist_poly4 reading the item's planes from the LDS buffer of prefetch_planes (same arithmetic and order).
+template <int S, int T>
+__device__ __forceinline__ void hoist_poly4_lds(const DevArgs& A, const uint8_t* buf, const double* lk, double (*a)[5],
+                                                unsigned& live) {
+  const int npad = A.pf_npad;
+  constexpr int C = S < PM_HOIST_CHUNK ? S : PM_HOIST_CHUNK;
+#pragma unroll
+  for (int s = 0; s < S; s++) {
+    if (s % C == 0) __builtin_amdgcn_sched_barrier(0);   // chunks of C slots: bounded bytes in flight
+    const int4 u = A.units[s * T + threadIdx.x];
+    const int nn = u.x == U_NUC ? u.w : 0;
+    uint32_t by[12];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const bool ok = q < nn;
+      const int pp = u.z + (ok ? q : 0);
+      by[3 * q + 0] = ok ? buf[pp] : 0;
+      by[3 * q + 1] = ok ? buf[npad + pp] : 0;
+      by[3 * q + 2] = ok ? buf[2 * npad + pp] : 0;
+    }
+    if (nn) live |= 1u << s;
+    double c9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (nn >= 2) {
+      double kids[9];
+#pragma unroll
+      for (int k = 0; k < 9; k++) kids[k] = 1.0;
+#pragma unroll
+      for (int q = 2; q < 4; q++)
+        if (q < nn) {
+          const double l11 = lk[by[3 * q]], l12 = lk[by[3 * q + 1]], l22 = lk[by[3 * q + 2]];
+#pragma unroll
+          for (int k = 0; k < 9; k++) kids[k] *= d_one_kid(k, PM_CHR_AUTO, 0, l11, l12, l22);
+        }
+      const double lF[3] = {lk[by[0]], lk[by[1]], lk[by[2]]};
+      const double lM[3] = {lk[by[3]], lk[by[4]], lk[by[5]]};
+#pragma unroll
+      for (int x = 0; x < 3; x++)
+#pragma unroll
+        for (int y = 0; y < 3; y++) c9[3 * x + y] = kids[3 * x + y] * (lF[x] * lM[y]);
+    }
+    fold_poly(c9, a[s]);
+    if (nn == 0) phantom_poly(a[s]);
+  }
+}
+
 // De novo variant of hoist_poly4 (autosomal --denovo items, families of <= 4 persons): the kid terms are
 // likelihoodONEKid_denovo's CalcDenovoMutLk dot products over all 10 genotype likelihoods (:1553-1562,
 // :1266-1296), so each kid's whole 10-byte PL record is loaded.  Chunks of PM_HOIST_CHUNK_DN slots keep
@@ -845,7 +923,8 @@ constexpr int brent_waves() { return (NUM == PM_NUM_POLY && !GEN && (T == 64 || 
 
 // DN: lean polynomial kernel for autosomal --denovo (instantiated separately so the common kernel carries
 // no de novo hoisting code or register pressure).
-template <int T, int S, int NUM, bool GEN, bool ES, bool DN = false>
+// PF: lean kernel whose items' genotype planes are prefetched into LDS (prefetch_planes); no other hoisting path.
+template <int T, int S, int NUM, bool GEN, bool ES, bool DN = false, bool PF = false>
 __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(DevArgs A, int list) {
   constexpr bool PROD = NUM != PM_NUM_EXACT;
   __shared__ double s_lk[256];
@@ -868,14 +947,17 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
   // XCD-aware item order: blocks are dealt round-robin to the 8 XCDs (separate L2s), so consecutive
   // items -- the 2-4 configurations of one site, which read the same PL block -- go to blocks of one XCD.
   const int vb = (gridDim.x % 8 == 0) ? (blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8 : blockIdx.x;
+  // lean kernel, one wave per item: the item's genotype planes arrive in LDS by prefetch (pf_npad > 0)
+  constexpr bool PFK = PF && NUM == PM_NUM_POLY && !GEN && !ES && !DN && T == 64;
+  extern __shared__ uint8_t s_pf[];
+  const bool pf = PFK && A.pf_npad > 0;
+  if (pf) prefetch_planes(A, items, vb, nItems, s_pf);
   for (int it = vb; it < nItems; it += gridDim.x) {
     const int item = items[it];
     const int site = item >> 3, cfg = item & 7;
     const int r = A.ref[site];
     ItemCtx I;
-    if (A.vcf) { I.a1 = r & 15; I.a2 = r >> 4; }
-    else if (cfg == 7) { I.a1 = A.res[site].allele1; I.a2 = A.res[site].allele2; }
-    else cfg_alleles(cfg, r, &I.a1, &I.a2);
+    item_alleles(A, site, cfg, r, &I.a1, &I.a2);
     I.g11 = d_gi(I.a1, I.a1); I.g12 = d_gi(I.a1, I.a2); I.g22 = d_gi(I.a2, I.a2);
     // the lean polynomial kernel also runs autosomal --denovo items (its hoisting has the de novo kid terms)
     I.denovo = (GEN || (POLYK && DN)) ? (A.denovo && cfg != 7) : 0;
@@ -896,7 +978,17 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
     unsigned live = 0;
     bool hoisted = false;
     if constexpr (POLY) {
-      if (A.max_nuc <= 4) {
+      if constexpr (PFK) {
+        if (pf) {
+          __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this item's planes have landed in LDS
+          hoist_poly4_lds<S, T>(A, s_pf, s_lk, cond, live);
+          __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): every read of the buffer is done ...
+          __builtin_amdgcn_sched_barrier(0);
+          prefetch_planes(A, items, it + gridDim.x, nItems, s_pf);   // ... before the next item's planes overwrite it
+          hoisted = true;
+        }
+      }
+      if (!PFK && !hoisted && A.max_nuc <= 4) {
         if constexpr (DN) hoist_poly4_dn<S, T>(A, I, pl, s_lk, s_M, cond, live);   // de novo and cfg-7 items
         else hoist_poly4<S, T>(A, I, pl, s_lk, cond, live);
         hoisted = true;
@@ -905,7 +997,7 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
 #pragma unroll
     for (int s = 0; s < S; s++) {
       fl[s] = 0;
-      if (hoisted) continue;
+      if (PFK || hoisted) continue;
       if constexpr (POLY) {
         const int4 u = A.units[s * T + threadIdx.x];   // L1/L2-resident; not kept in registers
         double c9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -916,6 +1008,25 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
       else if (GEN && unit[s].x == U_FP) fl[s] = hoist_fp(A, I, pl, s_lk, unit[s].z, unit[s].w & 0xFF, cond[s]);
     }
     double* raw = A.raw + (size_t)site * 8;
+#ifdef PM_EXP_HOIST_ONLY   // timing experiment: hoisting alone (results are a checksum, not likelihoods)
+    if constexpr (POLY) {
+      double cs = 0.0;
+#pragma unroll
+      for (int s2 = 0; s2 < S; s2++) cs += cond[s2][0] + cond[s2][4];
+      if (cs == 12345.0) raw[cfg] = cs;
+      if (threadIdx.x == 0) { raw[cfg] = -1.0; A.minv[site * 8 + cfg] = 0.5; A.evals[site * 8 + cfg] = 1; }
+      continue;
+    }
+#endif
+#ifdef PM_EXP_EVAL_ONLY   // timing experiment: evaluations on fixed synthetic coefficients (no PL loads)
+    if constexpr (POLY) {
+#pragma unroll
+      for (int s2 = 0; s2 < S; s2++) {
+        const double q = 1e-3 * (1 + ((threadIdx.x + s2 + site) & 7));
+        cond[s2][0] = q; cond[s2][1] = 0.5 * q; cond[s2][2] = 0.25 * q; cond[s2][3] = 2 * q; cond[s2][4] = 0.9;
+      }
+    }
+#endif
     double* wsl = ES ? A.ws + (size_t)blockIdx.x * A.ws_per_lane * T + threadIdx.x : nullptr;
     const bool single = !A.vcf && ((cfg == 0) || (A.single_nuclear && !A.unrelated));
     // One evaluation site for the objective: the three bracketing evaluations of OptimizeFrequency
@@ -2276,8 +2387,14 @@ static DevArgs make_args(pm_engine* E, int n, const uint8_t* pl, const uint32_t*
 typedef void (*BrentFn)(DevArgs, int);
 // numerics: PM_NUM_PRODUCT / PM_NUM_EXACT for every flavour; PM_NUM_POLY only for the lean kernel
 // (the generic and ES flavours fall back to PRODUCT numerics).
-static BrentFn brent_kernel(int T, int S, int num, bool gen, bool es, bool dn = false) {
+static BrentFn brent_kernel(int T, int S, int num, bool gen, bool es, bool dn = false, bool pf = false) {
   const int n = (num == PM_NUM_POLY && gen) ? PM_NUM_PRODUCT : num;
+  if (pf) {   // lean autosomal kernel with LDS plane prefetch
+#define PMKP(s) if (T == 64 && S == s) return k_brent<64, s, PM_NUM_POLY, false, false, false, true>;
+    PMKP(1) PMKP(2) PMKP(4) PMKP(8) PMKP(16)
+#undef PMKP
+    return nullptr;
+  }
   if (dn && !gen && !es && n == PM_NUM_POLY) {   // lean autosomal --denovo
 #define PMKD(t, s) if (T == t && S == s) return k_brent<t, s, PM_NUM_POLY, false, false, true>;
     PMKD(64, 1) PMKD(64, 2) PMKD(64, 4) PMKD(64, 8) PMKD(64, 16) PMKD(128, 8) PMKD(512, 4) PMKD(1024, 4) PMKD(1024, 8)
@@ -2315,13 +2432,22 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
     A.units = E->d_units_q; A.T = T = E->Tq; A.S = S = E->Sq; grid = E->grid_q;
     A.ext_count = nullptr; A.unrelated = 1; A.denovo = 0; gen = true;
   } else A.unrelated = 0;
-  BrentFn fn = brent_kernel(T, S, E->par.numerics, gen, !unrelated && n_ext > 0, A.denovo != 0);
+  // lean non-de-novo kernel at one wave per item: LDS-DMA plane prefetch when the planes are 16-B aligned
+  size_t shmem = 0;
+  A.pf_npad = 0;
+  if (!gen && !unrelated && n_ext == 0 && !A.denovo && T == 64 && E->par.numerics == PM_NUM_POLY && E->max_nuc <= 4 &&
+      E->n_person % 16 == 0 && E->n_person >= 16 && (E->n_person + 1023) / 1024 * 1024 * 3 <= 60 * 1024 &&
+      !getenv("PM_NO_PREFETCH")) {
+    A.pf_npad = (E->n_person + 1023) / 1024 * 1024;
+    shmem = (size_t)3 * A.pf_npad;
+  }
+  BrentFn fn = brent_kernel(T, S, E->par.numerics, gen, !unrelated && n_ext > 0, A.denovo != 0, A.pf_npad > 0);
   if (!fn) { pm_set_last_error("launch_brent: no kernel variant for the lane plan"); return PM_EINVAL; }
   hipEvent_t a, b;
   HIP_TRY(hipEventCreate(&a));
   HIP_TRY(hipEventCreate(&b));
   HIP_TRY(hipEventRecord(a, E->stream));
-  hipLaunchKernelGGL(fn, dim3(grid), dim3(T), 0, E->stream, A, list);
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(T), shmem, E->stream, A, list);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(b, E->stream));
   E->brent_events.push_back({a, b});

@@ -122,6 +122,27 @@ def test_synthetic_device_generator_and_parity(built, shape, nfam, nsites, tmp_p
 
 
 
+def test_plane_prefetch_bit_identical(built, tmp_path, monkeypatch):
+    """The lean kernel's LDS plane prefetch (taken when n_person % 16 == 0) gives bit-identical results to the
+    direct-load hoisting (PM_NO_PREFETCH=1), and both match the oracle."""
+    d = str(tmp_path / "pf")
+    pm.synth_write_dataset(d, "quad", 64, 500, 13)   # 256 persons: 16-B aligned planes
+    ped = pm.Pedigree(os.path.join(d, "test.dat"), os.path.join(d, "test.ped"))
+    label, pos, ref, pl, dm = _read_all(ped, d)[0]
+    params = pm.Params.defaults(numerics=pm.NUM_POLY)
+    outs = []
+    for nopf in ("", "1"):
+        if nopf:
+            monkeypatch.setenv("PM_NO_PREFETCH", nopf)
+        eng = pm.Engine(ped.view, params, max_batch=len(ref))
+        outs.append(eng.run(pl, dm, ref))
+        eng.close()
+    (a, ac), (b, bc) = outs
+    assert a.tobytes() == b.tobytes() and ac.tobytes() == bc.tobytes()
+    o, oc = Oracle(ped.view, params).run(pl, dm, ref)
+    assert compare_results(a, o, ac, oc, label="prefetch ")["called"] > 0
+
+
 @pytest.mark.parametrize("numerics", [pm.NUM_PRODUCT, pm.NUM_POLY])
 @pytest.mark.parametrize("shape", ["quad+dn", "trio+dn"])
 def test_denovo_planted_parity(built, tmp_path, numerics, shape):
