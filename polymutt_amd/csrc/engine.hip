@@ -562,11 +562,17 @@ __device__ __forceinline__ void fold_poly(const double* c, double* a) {
   a[4] = c[8];
 }
 
+// Lean kernels keep the lane plan in LDS, one int per (slot, lane): 0 = empty slot, else a nuclear family
+// as first person | persons << 24 (k_brent fills it once per block; no global round trip per item).
+__device__ __forceinline__ int unit_pack(const int4 u) { return u.x == U_NUC ? (u.z | (u.w << 24)) : 0; }
+__device__ __forceinline__ int unit_nn(int u) { return (int)((unsigned)u >> 24); }
+__device__ __forceinline__ int unit_first(int u) { return u & 0xFFFFFF; }
+
 // Chunked hoisting for the lean polynomial kernel when every nuclear family has <= 4 persons: the PL
 // bytes of 4 slots (4 x 12 loads) are issued before any of them is used, so the HBM round trips of a
 // chunk overlap instead of running slot after slot.  Arithmetic is hoist_nuc's, in the same order.
 template <int S, int T>
-__device__ __forceinline__ void hoist_poly4(const DevArgs& A, const ItemCtx& I, const uint8_t* pl, const double* lk,
+__device__ __forceinline__ void hoist_poly4(const DevArgs& A, const int* su, const ItemCtx& I, const uint8_t* pl, const double* lk,
                                             double (*a)[5], unsigned& live) {
   constexpr int C = S < PM_HOIST_CHUNK ? S : PM_HOIST_CHUNK;
   const size_t np = (size_t)A.n_person;
@@ -579,13 +585,13 @@ __device__ __forceinline__ void hoist_poly4(const DevArgs& A, const ItemCtx& I, 
     int nn[C];
 #pragma unroll
     for (int j = 0; j < C; j++) {
-      const int4 u = A.units[(c0 + j) * T + threadIdx.x];
-      const bool nuc = u.x == U_NUC;
-      nn[j] = nuc ? u.w : 0;
+      const int u = su[(c0 + j) * T + threadIdx.x];
+      const bool nuc = u != 0;
+      nn[j] = unit_nn(u);
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const bool ok = q < nn[j];
-        const int pp = u.z + (ok ? q : 0);
+        const int pp = unit_first(u) + (ok ? q : 0);
         by[j][3 * q + 0] = ok ? P11[pp] : 0;
         by[j][3 * q + 1] = ok ? P12[pp] : 0;
         by[j][3 * q + 2] = ok ? P22[pp] : 0;
@@ -652,21 +658,24 @@ __device__ __forceinline__ void prefetch_planes(const DevArgs& A, const int* ite
 }
 
 // hoist_poly4 reading the item's planes from the LDS buffer of prefetch_planes (same arithmetic and order).
+#ifndef PM_HOIST_CHUNK_LDS
+#define PM_HOIST_CHUNK_LDS 2
+#endif
 template <int S, int T>
-__device__ __forceinline__ void hoist_poly4_lds(const DevArgs& A, const uint8_t* buf, const double* lk, double (*a)[5],
-                                                unsigned& live) {
+__device__ __forceinline__ void hoist_poly4_lds(const DevArgs& A, const int* su, const uint8_t* buf, const double* lk,
+                                                double (*a)[5], unsigned& live) {
   const int npad = A.pf_npad;
-  constexpr int C = S < PM_HOIST_CHUNK ? S : PM_HOIST_CHUNK;
+  constexpr int C = S < PM_HOIST_CHUNK_LDS ? S : PM_HOIST_CHUNK_LDS;
 #pragma unroll
   for (int s = 0; s < S; s++) {
-    if (s % C == 0) __builtin_amdgcn_sched_barrier(0);   // chunks of C slots: bounded bytes in flight
-    const int4 u = A.units[s * T + threadIdx.x];
-    const int nn = u.x == U_NUC ? u.w : 0;
+    if (s % C == 0) __builtin_amdgcn_sched_barrier(0);   // chunks of C slots: bounded registers in flight
+    const int u = su[s * T + threadIdx.x];
+    const int nn = unit_nn(u);
     uint32_t by[12];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       const bool ok = q < nn;
-      const int pp = u.z + (ok ? q : 0);
+      const int pp = unit_first(u) + (ok ? q : 0);
       by[3 * q + 0] = ok ? buf[pp] : 0;
       by[3 * q + 1] = ok ? buf[npad + pp] : 0;
       by[3 * q + 2] = ok ? buf[2 * npad + pp] : 0;
@@ -704,7 +713,7 @@ __device__ __forceinline__ void hoist_poly4_lds(const DevArgs& A, const uint8_t*
 #define PM_HOIST_CHUNK_DN 2
 #endif
 template <int S, int T>
-__device__ __forceinline__ void hoist_poly4_dn(const DevArgs& A, const ItemCtx& I, const uint8_t* pl, const double* lk,
+__device__ __forceinline__ void hoist_poly4_dn(const DevArgs& A, const int* su, const ItemCtx& I, const uint8_t* pl, const double* lk,
                                                const double* M, double (*a)[5], unsigned& live) {
   constexpr int C = S < PM_HOIST_CHUNK_DN ? S : PM_HOIST_CHUNK_DN;
   const size_t np = (size_t)A.n_person;
@@ -718,13 +727,13 @@ __device__ __forceinline__ void hoist_poly4_dn(const DevArgs& A, const ItemCtx& 
     asm volatile("" : "+v"(r11), "+v"(r12), "+v"(r22));
 #pragma unroll
     for (int j = 0; j < C; j++) {
-      const int4 u = A.units[(c0 + j) * T + threadIdx.x];
-      const bool nuc = u.x == U_NUC;
-      nn[j] = nuc ? u.w : 0;
+      const int u = su[(c0 + j) * T + threadIdx.x];
+      const bool nuc = u != 0;
+      nn[j] = unit_nn(u);
 #pragma unroll
       for (int q = 0; q < 2; q++) {
         const bool ok = q < nn[j];
-        const uint8_t* R = pl + u.z + (ok ? q : 0);
+        const uint8_t* R = pl + unit_first(u) + (ok ? q : 0);
         par[j][3 * q + 0] = ok ? R[I.g11 * np] : 0;
         par[j][3 * q + 1] = ok ? R[I.g12 * np] : 0;
         par[j][3 * q + 2] = ok ? R[I.g22 * np] : 0;
@@ -732,7 +741,7 @@ __device__ __forceinline__ void hoist_poly4_dn(const DevArgs& A, const ItemCtx& 
 #pragma unroll
       for (int q = 0; q < 2; q++) {
         const bool ok = q + 2 < nn[j];
-        const uint8_t* R = pl + u.z + (ok ? q + 2 : 0);
+        const uint8_t* R = pl + unit_first(u) + (ok ? q + 2 : 0);
 #pragma unroll
         for (int g = 0; g < 10; g++) kid[j][q][g] = ok ? R[g * np] : 0;
       }
@@ -927,15 +936,20 @@ constexpr int brent_waves() { return (NUM == PM_NUM_POLY && !GEN && (T == 64 || 
 template <int T, int S, int NUM, bool GEN, bool ES, bool DN = false, bool PF = false>
 __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(DevArgs A, int list) {
   constexpr bool PROD = NUM != PM_NUM_EXACT;
+  constexpr bool POLYK = NUM == PM_NUM_POLY && !GEN;
   __shared__ double s_lk[256];
-  __shared__ double s_M[100];
-  __shared__ double s_red[96];
-  __shared__ int s_rede[32];
+  __shared__ double s_M[(GEN || DN) ? 100 : 1];
+  __shared__ double s_red[T > 64 ? 96 : 1];
+  __shared__ int s_rede[T > 64 ? 32 : 1];
+  __shared__ int s_u[POLYK ? S * T : 1];   // packed lane plan (unit_pack) of the lean kernels
   for (int i = threadIdx.x; i < 256; i += T) s_lk[i] = A.lktab[i];
-  for (int i = threadIdx.x; i < 100; i += T) s_M[i] = A.M[i];
+  if constexpr (GEN || DN)
+    for (int i = threadIdx.x; i < 100; i += T) s_M[i] = A.M[i];
+  if constexpr (POLYK)
+#pragma unroll
+    for (int s = 0; s < S; s++) s_u[s * T + threadIdx.x] = unit_pack(A.units[s * T + threadIdx.x]);
   __syncthreads();
   int4 unit[S];
-  constexpr bool POLYK = NUM == PM_NUM_POLY && !GEN;
   if constexpr (!POLYK) {
 #pragma unroll
     for (int s = 0; s < S; s++) unit[s] = A.units[s * T + threadIdx.x];
@@ -952,7 +966,15 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
   extern __shared__ uint8_t s_pf[];
   const bool pf = PFK && A.pf_npad > 0;
   if (pf) prefetch_planes(A, items, vb, nItems, s_pf);
+#ifdef PM_EXP_TIMING   // timing experiment: per-wave cycle split between hoisting, evaluations and the rest
+  long long tm_w = 0, tm_h = 0, tm_e = 0, tm_all = -(long long)wall_clock64(), tm_0 = 0, tm_1 = 0;
+  int tm_items = 0, tm_ev = 0;
+#endif
+  unsigned long long ev_acc = 0;   // evaluation count of this block's items: one atomic per block, at exit
   for (int it = vb; it < nItems; it += gridDim.x) {
+#ifdef PM_EXP_TIMING
+    tm_0 = wall_clock64(); tm_items++;
+#endif
     const int item = items[it];
     const int site = item >> 3, cfg = item & 7;
     const int r = A.ref[site];
@@ -981,7 +1003,10 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
       if constexpr (PFK) {
         if (pf) {
           __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this item's planes have landed in LDS
-          hoist_poly4_lds<S, T>(A, s_pf, s_lk, cond, live);
+#ifdef PM_EXP_TIMING
+          tm_w += wall_clock64() - tm_0;
+#endif
+          hoist_poly4_lds<S, T>(A, s_u, s_pf, s_lk, cond, live);
           __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): every read of the buffer is done ...
           __builtin_amdgcn_sched_barrier(0);
           prefetch_planes(A, items, it + gridDim.x, nItems, s_pf);   // ... before the next item's planes overwrite it
@@ -989,8 +1014,8 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
         }
       }
       if (!PFK && !hoisted && A.max_nuc <= 4) {
-        if constexpr (DN) hoist_poly4_dn<S, T>(A, I, pl, s_lk, s_M, cond, live);   // de novo and cfg-7 items
-        else hoist_poly4<S, T>(A, I, pl, s_lk, cond, live);
+        if constexpr (DN) hoist_poly4_dn<S, T>(A, s_u, I, pl, s_lk, s_M, cond, live);   // de novo and cfg-7 items
+        else hoist_poly4<S, T>(A, s_u, I, pl, s_lk, cond, live);
         hoisted = true;
       }
     }
@@ -1008,6 +1033,9 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
       else if (GEN && unit[s].x == U_FP) fl[s] = hoist_fp(A, I, pl, s_lk, unit[s].z, unit[s].w & 0xFF, cond[s]);
     }
     double* raw = A.raw + (size_t)site * 8;
+#ifdef PM_EXP_TIMING
+    tm_1 = wall_clock64(); tm_h += tm_1 - tm_0;
+#endif
 #ifdef PM_EXP_HOIST_ONLY   // timing experiment: hoisting alone (results are a checksum, not likelihoods)
     if constexpr (POLY) {
       double cs = 0.0;
@@ -1126,10 +1154,19 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
       raw[cfg] = -fmin;
       A.minv[site * 8 + cfg] = mn;
       A.evals[site * 8 + cfg] = nev;
-      if (!single) atomicAdd(A.eval_total, (unsigned long long)nev);
+      if (!single) ev_acc += nev;
       if (!ok) atomicExch(&A.counts[5], 1);
     }
+#ifdef PM_EXP_TIMING
+    tm_e += wall_clock64() - tm_1; tm_ev += nev;
+#endif
   }
+  if (threadIdx.x == 0 && ev_acc) atomicAdd(A.eval_total, ev_acc);
+#ifdef PM_EXP_TIMING
+  tm_all += wall_clock64();
+  if (threadIdx.x == 0 && (blockIdx.x % 97) == 0 && list == 0)
+    printf("TIMING blk %d items %d evals %d hoist %lld eval %lld all %lld wait %lld (x10ns)\n", blockIdx.x, tm_items, tm_ev, tm_h, tm_e, tm_all, tm_w);
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------
