@@ -568,6 +568,41 @@ __device__ __forceinline__ int unit_pack(const int4 u) { return u.x == U_NUC ? (
 __device__ __forceinline__ int unit_nn(int u) { return (int)((unsigned)u >> 24); }
 __device__ __forceinline__ int unit_first(int u) { return u & 0xFFFFFF; }
 
+#ifdef PM_EXP_LK_NOCONFLICT   // timing experiment: conflict-free table reads (wrong values)
+#define LKX(b) ((((b) & 1) | ((threadIdx.x & 63) << 1)) & 255)
+#else
+#define LKX(b) (b)
+#endif
+
+// One nuclear family's quartic coefficients from its PL bytes by[3q + {0,1,2}] = (g11, g12, g22) of person q
+// (father, mother, kids), nn persons (0 = empty slot -> the phantom family).  Branch-free: lanes whose
+// family has fewer persons multiply by exactly 1.0 and select, so no exec-masked regions (and no waits
+// per region) are generated; the arithmetic and its order are hoist_nuc's.
+__device__ __forceinline__ void fam_poly4(const uint32_t* by, int nn, const double* lk, double* a) {
+  double kids[9];
+#pragma unroll
+  for (int k = 0; k < 9; k++) kids[k] = 1.0;
+#pragma unroll
+  for (int q = 2; q < 4; q++) {
+    const double l11 = lk[LKX(by[3 * q])], l12 = lk[LKX(by[3 * q + 1])], l22 = lk[LKX(by[3 * q + 2])];
+    const bool kid = q < nn;
+#pragma unroll
+    for (int k = 0; k < 9; k++) kids[k] *= kid ? d_one_kid(k, PM_CHR_AUTO, 0, l11, l12, l22) : 1.0;
+  }
+  const double lF[3] = {lk[LKX(by[0])], lk[LKX(by[1])], lk[LKX(by[2])]};
+  const double lM[3] = {lk[LKX(by[3])], lk[LKX(by[4])], lk[LKX(by[5])]};
+  const bool fam = nn >= 2;
+  double c9[9];
+#pragma unroll
+  for (int x = 0; x < 3; x++)
+#pragma unroll
+    for (int y = 0; y < 3; y++) c9[3 * x + y] = fam ? kids[3 * x + y] * (lF[x] * lM[y]) : 0.0;
+  fold_poly(c9, a);
+  if (nn == 0) {   // empty slot: the phantom family (f + g)^4 (selects, not a branch)
+    a[0] = 1.0; a[1] = 4.0; a[2] = 6.0; a[3] = 4.0; a[4] = 1.0;
+  }
+}
+
 // Chunked hoisting for the lean polynomial kernel when every nuclear family has <= 4 persons: the PL
 // bytes of 4 slots (4 x 12 loads) are issued before any of them is used, so the HBM round trips of a
 // chunk overlap instead of running slot after slot.  Arithmetic is hoist_nuc's, in the same order.
@@ -590,38 +625,15 @@ __device__ __forceinline__ void hoist_poly4(const DevArgs& A, const int* su, con
       nn[j] = unit_nn(u);
 #pragma unroll
       for (int q = 0; q < 4; q++) {
-        const bool ok = q < nn[j];
-        const int pp = unit_first(u) + (ok ? q : 0);
-        by[j][3 * q + 0] = ok ? P11[pp] : 0;
-        by[j][3 * q + 1] = ok ? P12[pp] : 0;
-        by[j][3 * q + 2] = ok ? P22[pp] : 0;
+        const int pp = unit_first(u) + (q < nn[j] ? q : 0);   // in range for every lane: no branch around the load
+        by[j][3 * q + 0] = P11[pp];
+        by[j][3 * q + 1] = P12[pp];
+        by[j][3 * q + 2] = P22[pp];
       }
       if (nuc) live |= 1u << (c0 + j);
     }
 #pragma unroll
-    for (int j = 0; j < C; j++) {
-      double c9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-      if (nn[j] >= 2) {
-        double kids[9];
-#pragma unroll
-        for (int k = 0; k < 9; k++) kids[k] = 1.0;
-#pragma unroll
-        for (int q = 2; q < 4; q++)
-          if (q < nn[j]) {
-            const double l11 = lk[by[j][3 * q]], l12 = lk[by[j][3 * q + 1]], l22 = lk[by[j][3 * q + 2]];
-#pragma unroll
-            for (int k = 0; k < 9; k++) kids[k] *= d_one_kid(k, PM_CHR_AUTO, 0, l11, l12, l22);
-          }
-        const double lF[3] = {lk[by[j][0]], lk[by[j][1]], lk[by[j][2]]};
-        const double lM[3] = {lk[by[j][3]], lk[by[j][4]], lk[by[j][5]]};
-#pragma unroll
-        for (int x = 0; x < 3; x++)
-#pragma unroll
-          for (int y = 0; y < 3; y++) c9[3 * x + y] = kids[3 * x + y] * (lF[x] * lM[y]);
-      }
-      fold_poly(c9, a[c0 + j]);
-      if (nn[j] == 0) phantom_poly(a[c0 + j]);   // empty slot (lane_poly_r)
-    }
+    for (int j = 0; j < C; j++) fam_poly4(by[j], nn[j], lk, a[c0 + j]);
   }
 }
 
@@ -674,34 +686,13 @@ __device__ __forceinline__ void hoist_poly4_lds(const DevArgs& A, const int* su,
     uint32_t by[12];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-      const bool ok = q < nn;
-      const int pp = unit_first(u) + (ok ? q : 0);
-      by[3 * q + 0] = ok ? buf[pp] : 0;
-      by[3 * q + 1] = ok ? buf[npad + pp] : 0;
-      by[3 * q + 2] = ok ? buf[2 * npad + pp] : 0;
+      const int pp = unit_first(u) + (q < nn ? q : 0);   // in range for every lane: no branch around the read
+      by[3 * q + 0] = buf[pp];
+      by[3 * q + 1] = buf[npad + pp];
+      by[3 * q + 2] = buf[2 * npad + pp];
     }
     if (nn) live |= 1u << s;
-    double c9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    if (nn >= 2) {
-      double kids[9];
-#pragma unroll
-      for (int k = 0; k < 9; k++) kids[k] = 1.0;
-#pragma unroll
-      for (int q = 2; q < 4; q++)
-        if (q < nn) {
-          const double l11 = lk[by[3 * q]], l12 = lk[by[3 * q + 1]], l22 = lk[by[3 * q + 2]];
-#pragma unroll
-          for (int k = 0; k < 9; k++) kids[k] *= d_one_kid(k, PM_CHR_AUTO, 0, l11, l12, l22);
-        }
-      const double lF[3] = {lk[by[0]], lk[by[1]], lk[by[2]]};
-      const double lM[3] = {lk[by[3]], lk[by[4]], lk[by[5]]};
-#pragma unroll
-      for (int x = 0; x < 3; x++)
-#pragma unroll
-        for (int y = 0; y < 3; y++) c9[3 * x + y] = kids[3 * x + y] * (lF[x] * lM[y]);
-    }
-    fold_poly(c9, a[s]);
-    if (nn == 0) phantom_poly(a[s]);
+    fam_poly4(by, nn, lk, a[s]);
   }
 }
 
@@ -732,63 +723,62 @@ __device__ __forceinline__ void hoist_poly4_dn(const DevArgs& A, const int* su, 
       nn[j] = unit_nn(u);
 #pragma unroll
       for (int q = 0; q < 2; q++) {
-        const bool ok = q < nn[j];
-        const uint8_t* R = pl + unit_first(u) + (ok ? q : 0);
-        par[j][3 * q + 0] = ok ? R[I.g11 * np] : 0;
-        par[j][3 * q + 1] = ok ? R[I.g12 * np] : 0;
-        par[j][3 * q + 2] = ok ? R[I.g22 * np] : 0;
+        const uint8_t* R = pl + unit_first(u) + (q < nn[j] ? q : 0);   // in range: no branch around the loads
+        par[j][3 * q + 0] = R[I.g11 * np];
+        par[j][3 * q + 1] = R[I.g12 * np];
+        par[j][3 * q + 2] = R[I.g22 * np];
       }
 #pragma unroll
       for (int q = 0; q < 2; q++) {
-        const bool ok = q + 2 < nn[j];
-        const uint8_t* R = pl + unit_first(u) + (ok ? q + 2 : 0);
+        const uint8_t* R = pl + unit_first(u) + (q + 2 < nn[j] ? q + 2 : 0);
 #pragma unroll
-        for (int g = 0; g < 10; g++) kid[j][q][g] = ok ? R[g * np] : 0;
+        for (int g = 0; g < 10; g++) kid[j][q][g] = R[g * np];
       }
       if (nuc) live |= 1u << (c0 + j);
     }
 #pragma unroll
-    for (int j = 0; j < C; j++) {
-      double c9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-      if (nn[j] >= 2) {
-        double kids[9];
+    for (int j = 0; j < C; j++) {   // branch-free over the lanes' family sizes (see fam_poly4)
+      double kids[9];
 #pragma unroll
-        for (int k = 0; k < 9; k++) kids[k] = 1.0;
+      for (int k = 0; k < 9; k++) kids[k] = 1.0;
 #pragma unroll
-        for (int q = 0; q < 2; q++)
-          if (q + 2 < nn[j]) {
-            double D11 = 0.0, D12 = 0.0, D22 = 0.0;
-            if (I.denovo) {
+      for (int q = 0; q < 2; q++) {
+        double D11 = 0.0, D12 = 0.0, D22 = 0.0;
+        if (I.denovo) {   // uniform per item
 #pragma unroll
-              for (int g = 0; g < 10; g++) {
-                const double pg = lk[kid[j][q][g]];
-                // fused multiply-add: <= 1 ulp from the reference's mul + add (POLY numerics)
-                D11 = fma(M[r11 + g], pg, D11);
-                D12 = fma(M[r12 + g], pg, D12);
-                D22 = fma(M[r22 + g], pg, D22);
-              }
-            } else {   // cfg-7 items: likelihoodONEKid's autosomal terms are d_one_kid_dn's on (l11, l12, l22)
-              uint32_t b11 = 0, b12 = 0, b22 = 0;   // register selects (a dynamic index would go to scratch)
-#pragma unroll
-              for (int g = 0; g < 10; g++) {
-                b11 = g == I.g11 ? kid[j][q][g] : b11;
-                b12 = g == I.g12 ? kid[j][q][g] : b12;
-                b22 = g == I.g22 ? kid[j][q][g] : b22;
-              }
-              D11 = lk[b11]; D12 = lk[b12]; D22 = lk[b22];
-            }
-#pragma unroll
-            for (int k = 0; k < 9; k++) kids[k] *= d_one_kid_dn(k, D11, D12, D22);
+          for (int g = 0; g < 10; g++) {
+            const double pg = lk[kid[j][q][g]];
+            // fused multiply-add: <= 1 ulp from the reference's mul + add (POLY numerics)
+            D11 = fma(M[r11 + g], pg, D11);
+            D12 = fma(M[r12 + g], pg, D12);
+            D22 = fma(M[r22 + g], pg, D22);
           }
-        const double lF[3] = {lk[par[j][0]], lk[par[j][1]], lk[par[j][2]]};
-        const double lM[3] = {lk[par[j][3]], lk[par[j][4]], lk[par[j][5]]};
+        } else {   // cfg-7 items: likelihoodONEKid's autosomal terms are d_one_kid_dn's on (l11, l12, l22)
+          uint32_t b11 = 0, b12 = 0, b22 = 0;   // register selects (a dynamic index would go to scratch)
 #pragma unroll
-        for (int x = 0; x < 3; x++)
+          for (int g = 0; g < 10; g++) {
+            b11 = g == I.g11 ? kid[j][q][g] : b11;
+            b12 = g == I.g12 ? kid[j][q][g] : b12;
+            b22 = g == I.g22 ? kid[j][q][g] : b22;
+          }
+          D11 = lk[b11]; D12 = lk[b12]; D22 = lk[b22];
+        }
+        const bool isKid = q + 2 < nn[j];
 #pragma unroll
-          for (int y = 0; y < 3; y++) c9[3 * x + y] = kids[3 * x + y] * (lF[x] * lM[y]);
+        for (int k = 0; k < 9; k++) kids[k] *= isKid ? d_one_kid_dn(k, D11, D12, D22) : 1.0;
       }
+      const double lF[3] = {lk[par[j][0]], lk[par[j][1]], lk[par[j][2]]};
+      const double lM[3] = {lk[par[j][3]], lk[par[j][4]], lk[par[j][5]]};
+      const bool fam = nn[j] >= 2;
+      double c9[9];
+#pragma unroll
+      for (int x = 0; x < 3; x++)
+#pragma unroll
+        for (int y = 0; y < 3; y++) c9[3 * x + y] = fam ? kids[3 * x + y] * (lF[x] * lM[y]) : 0.0;
       fold_poly(c9, a[c0 + j]);
-      if (nn[j] == 0) phantom_poly(a[c0 + j]);   // empty slot (lane_poly_r)
+      if (nn[j] == 0) {   // empty slot: the phantom family (selects)
+        a[c0 + j][0] = 1.0; a[c0 + j][1] = 4.0; a[c0 + j][2] = 6.0; a[c0 + j][3] = 4.0; a[c0 + j][4] = 1.0;
+      }
     }
     __builtin_amdgcn_sched_barrier(0);   // keep the next chunk's loads from being hoisted above this one
   }
