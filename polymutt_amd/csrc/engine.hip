@@ -567,6 +567,22 @@ __device__ __forceinline__ void fold_poly(const double* c, double* a) {
 __device__ __forceinline__ int unit_pack(const int4 u) { return u.x == U_NUC ? (u.z | (u.w << 24)) : 0; }
 __device__ __forceinline__ int unit_nn(int u) { return (int)((unsigned)u >> 24); }
 __device__ __forceinline__ int unit_first(int u) { return u & 0xFFFFFF; }
+// The lane's S packed units, stored lane-major (s_u[lane * S + slot]) so they arrive in S/4 16-B LDS reads
+// at the start of the hoisting, before any coefficient register is live.
+template <int S>
+__device__ __forceinline__ void load_units(const int* su, int* uu) {
+  const int* p = su + threadIdx.x * S;
+  if constexpr (S % 4 == 0) {
+#pragma unroll
+    for (int s = 0; s < S; s += 4) {
+      const int4 v = *(const int4*)(p + s);
+      uu[s] = v.x; uu[s + 1] = v.y; uu[s + 2] = v.z; uu[s + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < S; s++) uu[s] = p[s];
+  }
+}
 
 #ifdef PM_EXP_LK_NOCONFLICT   // timing experiment: conflict-free table reads (wrong values)
 #define LKX(b) ((((b) & 1) | ((threadIdx.x & 63) << 1)) & 255)
@@ -614,13 +630,15 @@ __device__ __forceinline__ void hoist_poly4(const DevArgs& A, const int* su, con
   const uint8_t* P11 = pl + I.g11 * np;   // the three genotype planes of the item
   const uint8_t* P12 = pl + I.g12 * np;
   const uint8_t* P22 = pl + I.g22 * np;
+  int uu[S];
+  load_units<S>(su, uu);
 #pragma unroll
   for (int c0 = 0; c0 < S; c0 += C) {
     uint32_t by[C][12];
     int nn[C];
 #pragma unroll
     for (int j = 0; j < C; j++) {
-      const int u = su[(c0 + j) * T + threadIdx.x];
+      const int u = uu[c0 + j];
       const bool nuc = u != 0;
       nn[j] = unit_nn(u);
 #pragma unroll
@@ -678,10 +696,12 @@ __device__ __forceinline__ void hoist_poly4_lds(const DevArgs& A, const int* su,
                                                 double (*a)[5], unsigned& live) {
   const int npad = A.pf_npad;
   constexpr int C = S < PM_HOIST_CHUNK_LDS ? S : PM_HOIST_CHUNK_LDS;
+  int uu[S];
+  load_units<S>(su, uu);
 #pragma unroll
   for (int s = 0; s < S; s++) {
     if (s % C == 0) __builtin_amdgcn_sched_barrier(0);   // chunks of C slots: bounded registers in flight
-    const int u = su[s * T + threadIdx.x];
+    const int u = uu[s];
     const int nn = unit_nn(u);
     uint32_t by[12];
 #pragma unroll
@@ -708,6 +728,8 @@ __device__ __forceinline__ void hoist_poly4_dn(const DevArgs& A, const int* su, 
                                                const double* M, double (*a)[5], unsigned& live) {
   constexpr int C = S < PM_HOIST_CHUNK_DN ? S : PM_HOIST_CHUNK_DN;
   const size_t np = (size_t)A.n_person;
+  int uu[S];
+  load_units<S>(su, uu);
 #pragma unroll
   for (int c0 = 0; c0 < S; c0 += C) {
     uint32_t par[C][6], kid[C][2][10];
@@ -718,7 +740,7 @@ __device__ __forceinline__ void hoist_poly4_dn(const DevArgs& A, const int* su, 
     asm volatile("" : "+v"(r11), "+v"(r12), "+v"(r22));
 #pragma unroll
     for (int j = 0; j < C; j++) {
-      const int u = su[(c0 + j) * T + threadIdx.x];
+      const int u = uu[c0 + j];
       const bool nuc = u != 0;
       nn[j] = unit_nn(u);
 #pragma unroll
@@ -837,10 +859,9 @@ __device__ __forceinline__ void lane_poly_r(double r, double g4, const double (*
 #pragma unroll
   for (int w = 1; w < NA; w *= 2)
 #pragma unroll
-    for (int j = 0; j + w < NA; j += 2 * w) {
-      int x;
-      am[j] = frexp(am[j] * am[j + w], &x);
-      ae[j] += ae[j + w] + x;
+    for (int j = 0; j + w < NA; j += 2 * w) {   // 4 mantissas in [0.5, 1): product >= 1/16, renormalised in wave_prod
+      am[j] = am[j] * am[j + w];
+      ae[j] += ae[j + w];
     }
   m = am[0];
   e = ae[0];
@@ -856,9 +877,8 @@ __device__ __forceinline__ void dpp_prod_step(double& m, int& e) {
   const int olo = __builtin_amdgcn_update_dpp(0, lo, CTRL, ROWMASK, 0xF, false);
   const int ohi = __builtin_amdgcn_update_dpp(0x3FF00000, hi, CTRL, ROWMASK, 0xF, false);
   const int oe = __builtin_amdgcn_update_dpp(0, e, CTRL, ROWMASK, 0xF, false);
-  int ev;
-  m = frexp(m * __hiloint2double(ohi, olo), &ev);
-  e += oe + ev;
+  m = m * __hiloint2double(ohi, olo);   // no renormalisation: 64 factors in [1/16, 1) stay >= 2^-256
+  e += oe;
 }
 
 // Product of the 64 lanes' (m, e), in a fixed order: quad xor 1, quad xor 2, half-row mirror, row mirror
@@ -872,8 +892,9 @@ __device__ __forceinline__ void wave_prod(double& m, int& e) {
   dpp_prod_step<0x142, 0xA>(m, e);   // row_bcast:15 -> rows 1, 3
   dpp_prod_step<0x143, 0xC>(m, e);   // row_bcast:31 -> rows 2, 3
   const int lo = __builtin_amdgcn_readlane(__double2loint(m), 63), hi = __builtin_amdgcn_readlane(__double2hiint(m), 63);
-  m = __hiloint2double(hi, lo);
-  e = __builtin_amdgcn_readlane(e, 63);
+  int ev;
+  m = frexp(__hiloint2double(hi, lo), &ev);   // one normalisation (exact: the mantissa bits are those of the
+  e = __builtin_amdgcn_readlane(e, 63) + ev;  // step-wise normalised product, scalings by 2^k being exact)
 }
 
 // log10(m * 2^e) for a normalised mantissa m in [0.5, 1) (or 0): m is moved to [sqrt(1/2), sqrt(2)) (exact),
@@ -931,13 +952,13 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
   __shared__ double s_M[(GEN || DN) ? 100 : 1];
   __shared__ double s_red[T > 64 ? 96 : 1];
   __shared__ int s_rede[T > 64 ? 32 : 1];
-  __shared__ int s_u[POLYK ? S * T : 1];   // packed lane plan (unit_pack) of the lean kernels
+  __shared__ __attribute__((aligned(16))) int s_u[POLYK ? S * T : 4];   // packed lane plan (unit_pack, lane-major)
   for (int i = threadIdx.x; i < 256; i += T) s_lk[i] = A.lktab[i];
   if constexpr (GEN || DN)
     for (int i = threadIdx.x; i < 100; i += T) s_M[i] = A.M[i];
   if constexpr (POLYK)
 #pragma unroll
-    for (int s = 0; s < S; s++) s_u[s * T + threadIdx.x] = unit_pack(A.units[s * T + threadIdx.x]);
+    for (int s = 0; s < S; s++) s_u[threadIdx.x * S + s] = unit_pack(A.units[s * T + threadIdx.x]);
   __syncthreads();
   int4 unit[S];
   if constexpr (!POLYK) {
