@@ -3,8 +3,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <ctime>
 #include "glf.h"
+#include "ingest.h"
+#include <thread>
 #include "vcf.h"
 #include "vcf_input.h"
 
@@ -35,7 +38,7 @@ Options parse_command_line(int argc, char** argv) {
       {"pos", 's', &o.positionFile}, {"all_sites", 'b', &o.all_sites}, {"gl_off", 'b', &o.gl_off},
       {"quick_call", 'b', &o.quick_call},
       // engine options (not in the reference)
-      {"gpu", 'i', &o.device}, {"batch", 'i', &o.batch}, {"exact_log10", 'b', &o.exact_log10}, {"numerics", 's', &o.numerics},
+      {"gpu", 'i', &o.device}, {"batch", 'i', &o.batch}, {"io_threads", 'i', &o.io_threads}, {"exact_log10", 'b', &o.exact_log10}, {"numerics", 's', &o.numerics},
   };
   auto assign = [](Flag& f, const char* v) {
     switch (f.kind) {
@@ -82,6 +85,8 @@ Options parse_command_line(int argc, char** argv) {
 }
 
 namespace {
+
+double now_s() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 
 void print_status(const Options& o) {   // abbreviated ParameterList::Status banner
   printf("\nThe following parameters are in effect:\n");
@@ -137,8 +142,12 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval) {
   std::map<std::string, int> positionMap;
   if (!opt.positionFile.empty()) positionMap = load_positions(opt.positionFile);
 
-  SiteSource src;
-  src.open(ped, opt.glfListFile);
+  ParallelSiteSource src;   // PedigreeGLF with parallel decode (ingest.h)
+  {
+    int io = opt.io_threads;
+    if (io <= 0) io = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+    src.open(ped, opt.glfListFile, io);
+  }
   FILE* vcf = fopen(opt.vcfOutFile.c_str(), "w");
   if (!vcf) throw FatalError("vcfOutFile can not be opened for output!\n");
 
@@ -167,11 +176,18 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval) {
   B.init(opt.batch > 0 ? opt.batch : 4096, np);
   int out_cnt = 0;
   size_t chrDone = 0;
+  double t_ingest = 0, t_eval = 0, t_out = 0;   // PM_TIMING=1: host-side breakdown on stderr
+  struct TimingReport {
+    double &a, &b, &c;
+    ~TimingReport() {
+      if (getenv("PM_TIMING")) fprintf(stderr, "PM_TIMING ingest %.3f s, engine %.3f s, vcf %.3f s\n", a, b, c);
+    }
+  } timing_report{t_ingest, t_eval, t_out};
 
   while (src.nextSection()) {
     if (!chrSel.empty() && chrDone >= chrSelCount) break;
     const std::string label = src.label();
-    if (!chrSel.empty() && chrSel[label] < 1) { while (src.nextBaseEntry()) {} continue; }
+    if (!chrSel.empty() && chrSel[label] < 1) continue;   // the next section's skip consumes this one
     int chrom = label == opt.chrX ? PM_CHR_X : label == opt.chrY ? PM_CHR_Y : label == opt.MT ? PM_CHR_MT : PM_CHR_AUTO;
     eval.begin_section(chrom);
     W.chrom = chrom;
@@ -182,7 +198,10 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval) {
     auto flush = [&]() {
       if (B.n == 0) return;
       int rows = 0;
+      const double t0 = now_s();
       eval.run(B.n, B.pl.data(), B.dm.data(), B.ref.data(), B.res.data(), B.calls.data(), &rows);
+      const double t1 = now_s();
+      t_eval += t1 - t0;
       for (int i = 0; i < B.n && !stop; i++) {
         const pm_site_result& r = B.res[i];
         if (!r.emit) continue;
@@ -192,20 +211,31 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval) {
         if (opt.force_call && out_cnt >= (int)positionMap.size()) stop = true;   // main.cpp:593 returns without a summary
       }
       B.n = 0;
+      t_out += now_s() - t1;
     };
 
-    while (src.nextBaseEntry()) {
-      if (entries == 0) entries = src.maxPosition();
-      if (!opt.positionFile.empty()) {
-        std::string key = label + ":" + std::to_string(src.currentPos + 1);
-        if (!positionMap.count(key)) continue;
+    std::vector<int> wpos(src.window()), rowOf(src.window());
+    std::vector<uint8_t> wref(src.window());
+    for (;;) {   // windows of Move2NextBaseEntry calls, merged serially, decoded and filled in parallel
+      const int want = std::min(src.window(), B.cap - B.n);
+      const double ti = now_s();
+      const int got = src.nextSites(want, wpos.data(), wref.data());
+      if (got > 0 && entries == 0) entries = src.maxPosition();
+      for (int s = 0; s < got; s++) {
+        rowOf[s] = -1;
+        if (!opt.positionFile.empty()) {
+          std::string key = label + ":" + std::to_string(wpos[s] + 1);
+          if (!positionMap.count(key)) continue;
+        }
+        const int i = B.n++;
+        B.pos[i] = wpos[s] + 1;
+        B.ref[i] = wref[s];
+        rowOf[s] = i;
       }
-      int i = B.n++;
-      B.pos[i] = src.currentPos + 1;
-      B.ref[i] = (uint8_t)src.refBase;
-      src.fill(B.pl.data() + (size_t)i * np * 10, B.dm.data() + (size_t)i * np);
+      src.fill(rowOf.data(), B.pl.data(), B.dm.data());
+      t_ingest += now_s() - ti;
       if (B.n == B.cap) flush();
-      if (stop) break;
+      if (stop || got < want) break;
     }
     flush();
     if (stop) { fflush(vcf); return 0; }

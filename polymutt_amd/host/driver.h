@@ -19,6 +19,7 @@ struct Options {
   std::string numerics = "poly";
   double denovo_rate = 1.5e-08, denovo_tstv = 2.0, denovo_llr = 0.01;
   int device = 0, batch = 4096;
+  int io_threads = 0;   // GLF decode threads (0: min(16, hardware threads))
   std::string cmd;
   pm_params params() const;
 };

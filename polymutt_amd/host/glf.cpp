@@ -126,7 +126,7 @@ bool GlfFile::nextBaseEntry() {   // :195-204
 }
 
 // ---------------------------------------------------------------------------------------------
-static std::map<std::string, std::string> readIndex(const std::string& path) {
+std::map<std::string, std::string> read_glf_index(const std::string& path) {
   // readGLFannoFile, src/main.cpp:15-37: "key filename" per line, lines with <2 tokens skipped
   std::map<std::string, std::string> m;
   gzFile fh = gzopen(path.c_str(), "rb");
@@ -155,7 +155,7 @@ static std::map<std::string, std::string> readIndex(const std::string& path) {
 }
 
 void SiteSource::open(const Pedigree& ped, const std::string& glfIndexFile) {
-  auto index = readIndex(glfIndexFile);
+  auto index = read_glf_index(glfIndexFile);
   const int n = (int)ped.column_pid.size();
   files_ = std::vector<GlfFile>(n);
   has_.assign(n, 0);

@@ -46,6 +46,9 @@ class GlfFile {
   bool zeof_ = false;
 };
 
+// readGLFannoFile (src/main.cpp:15-37): GLF index file -> {key: file name}
+std::map<std::string, std::string> read_glf_index(const std::string& path);
+
 class SiteSource {
  public:
   // Opens every person's GLF (key = (int)GLF_Index looked up in the index file).

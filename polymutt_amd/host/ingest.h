@@ -1,0 +1,107 @@
+// ingest.h -- parallel GLF ingest.
+//
+// ParallelSiteSource produces exactly the site stream of SiteSource (PedigreeGLF::Move2NextSection /
+// Move2NextBaseEntry, src/PedigreeGLF.cpp:197-324), but splits the work the reference does serially per site:
+//
+//   1. decode  (parallel over persons): every person's GLF is inflated and parsed ahead into a queue of
+//      GlfState -- the state glfHandler holds after each NextBaseEntry call (core/glfHandler.cpp:195-261).
+//      A person's state sequence depends on its own file only, so the queues fill independently.
+//   2. merge   (serial, integer only): Move2NextBaseEntry restated over the queue heads -- the end-of-section
+//      check, the advance of the persons sitting at currentPos, and the min-position scan whose refBase is
+//      taken from the first person holding the minimum.  One fused pass per site.
+//   3. fill    (parallel over persons): each person replays the same advance rule over the merged positions
+//      and writes its PL / depth|mapQ columns of the dense block rows.
+//
+// Memory: n_person x (window + 1) x 20 B of decoded states (82 MB for 4000 persons at the default window).
+#pragma once
+#include <condition_variable>
+#include <cstdint>
+#include <functional>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+#include "glf.h"
+#include "pedigree.h"
+
+namespace pmhost {
+
+// glfHandler's per-record state after a NextBaseEntry call.
+struct GlfState {
+  int32_t pos;
+  uint32_t dm;       // depth (24 b) | mapQuality << 24
+  uint8_t lk[10];
+  uint8_t ref;       // translated refBase 0..4
+  uint8_t rt;        // recordType (0 = end of section)
+};
+
+// Minimal fork-join pool: run(n, fn) calls fn(i) for i in [0, n) on the pool's threads and the caller.
+class TaskPool {
+ public:
+  explicit TaskPool(int threads);
+  ~TaskPool();
+  void run(int n, const std::function<void(int)>& fn);
+  int threads() const { return (int)workers_.size() + 1; }
+
+ private:
+  void work();
+  std::vector<std::thread> workers_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(int)>* fn_ = nullptr;
+  int n_ = 0, next_ = 0, active_ = 0;
+  long gen_ = 0;
+  bool stop_ = false;
+};
+
+class ParallelSiteSource {
+ public:
+  ParallelSiteSource() = default;
+  ParallelSiteSource(const ParallelSiteSource&) = delete;
+  ParallelSiteSource& operator=(const ParallelSiteSource&) = delete;
+  ~ParallelSiteSource();
+  // threads: decode/fill workers (the caller counts as one).  window: sites merged per nextSites call at most.
+  void open(const Pedigree& ped, const std::string& glfIndexFile, int threads, int window = 1024);
+  bool nextSection();   // PedigreeGLF::Move2NextSection (the files skip to their next section in parallel)
+  const std::string& label() const { return files_[nonNull_].label; }
+  int maxPosition() const { return files_[nonNull_].maxPosition; }
+  int nPerson() const { return (int)files_.size(); }
+  int window() const { return window_; }
+
+  // Advances up to maxSites (<= window) sites of the current section, as that many Move2NextBaseEntry calls
+  // would: pos[i] (0-based currentPos) and ref[i] (refBase) of each site.  Returns the count; fewer than
+  // maxSites means the section has ended.
+  int nextSites(int maxSites, int* pos, uint8_t* ref);
+  // Writes the block rows of the sites of the last nextSites call: site i goes to row rowOf[i] of pl
+  // ([row][n_person][10]) and dm ([row][n_person]); rowOf[i] < 0 skips the site (--pos filtering).
+  void fill(const int* rowOf, uint8_t* pl, uint32_t* dm);
+
+ private:
+  struct Queue {
+    std::vector<GlfState> q;
+    int head = -1;          // -1: before the section's first call (the state at position 0)
+    int tail = 0;
+    bool terminal = false;  // q[tail - 1] is the end-of-section state, which repeats forever
+  };
+  void refill(int j, int need);
+  const GlfState& state(int j, int k) const { return k < 0 ? virtual_ : qs_[j].q[k]; }
+  int next(int j, int k) const { return (k + 1 < qs_[j].tail) ? k + 1 : k; }
+  template <class F> void forChunks(F f);
+
+  std::vector<GlfFile> files_;
+  std::vector<Queue> qs_;
+  std::vector<int> active_;   // persons with a GLF handle (handle != NULL), ascending; active_[0] == nonNull_
+  std::vector<char> has_;
+  std::vector<std::string> pids_;
+  int nonNull_ = -1;
+  int window_ = 1024;
+  TaskPool* pool_ = nullptr;
+  GlfState virtual_{};
+  int currentPos_ = 0;
+  bool ended_ = false;
+  // the last nextSites call: currentPos and queue heads before it, and the merged positions
+  int prevPos_ = 0, nLast_ = 0;
+  std::vector<int> headAtStart_, lastPos_;
+};
+
+}  // namespace pmhost

@@ -1,6 +1,7 @@
 // vcf.cpp -- see vcf.h.
 #include "vcf.h"
 #include <ctime>
+#include "vcf_fmt.h"
 
 namespace pmhost {
 
@@ -49,7 +50,7 @@ void VcfWriter::output(const std::string& label, int pos1, int refBase, const pm
   const bool refIsA1 = refBase == r.allele1;
   char info[512];
   std::string alt;
-  auto label_of = [&](const pm_geno_call& c) -> std::string {
+  auto label_of = [&](const pm_geno_call& c) -> const char* {
     switch (c.label) {
       case PM_LBL_DOT: return ".";
       case PM_LBL_GENO10: return kGeno10[c.best];
@@ -81,15 +82,26 @@ void VcfWriter::output(const std::string& label, int pos1, int refBase, const pm
     fprintf(fh, "%s\t%d\t%s\t%c\t%s\t%d\t%s\t%s\t%s", label.c_str(), pos1, ".", kBases[refBase], alt.c_str(), int(r.poly_qual + 0.5), ".",
             INFO.c_str(), gl_off ? "GT:GQ:DP:DS" : "GT:GQ:DP:DS:PL");
     const int g11 = GI(r.allele1, r.allele1), g12 = GI(r.allele1, r.allele2), g22 = GI(r.allele2, r.allele2);
+    std::string& L = line_;   // "\t%s:%d:%d:%.2f[:%u,%u,%u]" per person, formatted without stdio
+    L.clear();
     for (int p = 0; p < n; p++) {
       const pm_geno_call& c = calls[p];
-      fprintf(fh, "\t%s:", label_of(c).c_str());
-      fprintf(fh, "%d:", (int)c.gq);
-      fprintf(fh, "%d:", (int)(dm[p] & 0xFFFFFF));
-      fprintf(fh, "%.2f", c.dosage);
-      if (!gl_off) fprintf(fh, ":%u,%u,%u", (unsigned)pl[p * 10 + g11], (unsigned)pl[p * 10 + g12], (unsigned)pl[p * 10 + g22]);
+      L.push_back('\t');
+      L += label_of(c);
+      L.push_back(':');
+      fmt_int(L, (int)c.gq);
+      L.push_back(':');
+      fmt_int(L, (int)(dm[p] & 0xFFFFFF));
+      L.push_back(':');
+      fmt_fixed(L, c.dosage, 2);
+      if (!gl_off) {
+        L.push_back(':'); fmt_uint(L, pl[p * 10 + g11]);
+        L.push_back(','); fmt_uint(L, pl[p * 10 + g12]);
+        L.push_back(','); fmt_uint(L, pl[p * 10 + g22]);
+      }
     }
-    fprintf(fh, "\n");
+    L.push_back('\n');
+    fwrite(L.data(), 1, L.size(), fh);
     fflush(fh);
   } else {
     const int a2 = r.denovo_mono ? r.allele1 : r.allele2;
@@ -103,18 +115,24 @@ void VcfWriter::output(const std::string& label, int pos1, int refBase, const pm
     else alt = std::string(1, kBases[r.allele1]) + "," + kBases[a2];
     fprintf(fh, "%s\t%d\t%s\t%c\t%s\t%d\t%s\t%s\t%s", label.c_str(), pos1, ".", kBases[refBase], alt.c_str(), int(r.poly_qual + 0.5), ".", info,
             gl_off ? "GT:GQ:DP" : "GT:GQ:DP:PL");
+    std::string& L = line_;
+    L.clear();
     for (int p = 0; p < n; p++) {
       const pm_geno_call& c = calls[p];
-      fprintf(fh, "\t%s:", label_of(c).c_str());
-      fprintf(fh, "%d:", (int)c.gq);
-      fprintf(fh, "%d", (int)(dm[p] & 0xFFFFFF));
+      L.push_back('\t');
+      L += label_of(c);
+      L.push_back(':');
+      fmt_int(L, (int)c.gq);
+      L.push_back(':');
+      fmt_int(L, (int)(dm[p] & 0xFFFFFF));
       if (!gl_off) {
-        fprintf(fh, ":");
-        for (int g = 0; g < 9; g++) fprintf(fh, "%d,", (int)pl[p * 10 + g]);
-        fprintf(fh, "%d", (int)pl[p * 10 + 9]);
+        L.push_back(':');
+        for (int g = 0; g < 9; g++) { fmt_uint(L, pl[p * 10 + g]); L.push_back(','); }
+        fmt_uint(L, pl[p * 10 + 9]);
       }
     }
-    fprintf(fh, "\n");
+    L.push_back('\n');
+    fwrite(L.data(), 1, L.size(), fh);
     fflush(fh);
   }
 }

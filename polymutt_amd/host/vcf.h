@@ -26,6 +26,7 @@ struct VcfWriter {
  private:
   void header();
   bool singleNuclear() const;
+  std::string line_;   // genotype columns of the record being written (reused)
 };
 
 }  // namespace pmhost

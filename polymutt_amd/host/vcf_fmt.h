@@ -1,0 +1,67 @@
+// vcf_fmt.h -- allocation-free text formatting for the per-genotype VCF columns.
+//
+// OutputVCF (src/NucFamGenotypeLikelihood.cpp:1751-1915) prints every genotype column with fprintf
+// ("%s:%d:%d:%.2f:%d,%d,%d"); with thousands of persons per record that is most of the CLI's host time.
+// These helpers append the same characters to a buffer: integers in decimal, and fixed-point values
+// rounded exactly as glibc's printf does (the exact binary value rounded to `prec` decimals, ties to even).
+#pragma once
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+namespace pmhost {
+
+inline void fmt_uint(std::string& out, uint64_t v) {
+  char b[24];
+  int n = 0;
+  do { b[n++] = char('0' + v % 10); v /= 10; } while (v);
+  while (n) out.push_back(b[--n]);
+}
+
+inline void fmt_int(std::string& out, int64_t v) {
+  if (v < 0) { out.push_back('-'); fmt_uint(out, (uint64_t)(-(v + 1)) + 1); }
+  else fmt_uint(out, (uint64_t)v);
+}
+
+// printf("%.<prec>f", v) for prec in 0..6.  v = m * 2^e exactly (m < 2^53); m * 10^prec * 2^e is split into
+// an integer part and an exact remainder with 128-bit arithmetic, then rounded half-to-even.
+inline void fmt_fixed(std::string& out, double v, int prec) {
+  static const uint64_t kPow10[7] = {1, 10, 100, 1000, 10000, 100000, 1000000};
+  if (!std::isfinite(v) || std::fabs(v) >= 1e12 || prec < 0 || prec > 6) {
+    char b[64];
+    snprintf(b, sizeof(b), "%.*f", prec, v);
+    out += b;
+    return;
+  }
+  const bool neg = std::signbit(v);
+  const double a = std::fabs(v);
+  uint64_t q = 0;
+  if (a != 0.0) {
+    int e;
+    const double fr = std::frexp(a, &e);                       // a = fr * 2^e, fr in [0.5, 1)
+    const uint64_t m = (uint64_t)std::ldexp(fr, 53);           // exact: a = m * 2^(e - 53)
+    e -= 53;
+    const unsigned __int128 scaled = (unsigned __int128)m * kPow10[prec];
+    if (e >= 0) q = (uint64_t)(scaled << e);
+    else if (-e < 127) {
+      const int sh = -e;
+      const unsigned __int128 one = 1;
+      const unsigned __int128 mask = (one << sh) - 1, half = one << (sh - 1);
+      q = (uint64_t)(scaled >> sh);
+      const unsigned __int128 rem = scaled & mask;
+      if (rem > half || (rem == half && (q & 1))) q++;
+    }
+  }
+  if (neg) out.push_back('-');
+  fmt_uint(out, q / kPow10[prec]);
+  if (prec) {
+    out.push_back('.');
+    uint64_t f = q % kPow10[prec];
+    char b[8];
+    for (int i = prec - 1; i >= 0; i--) { b[i] = char('0' + f % 10); f /= 10; }
+    out.append(b, prec);
+  }
+}
+
+}  // namespace pmhost

@@ -78,3 +78,31 @@ def test_cpu_driver_reproduces_vcf_input_golden(cpu_driver, tmp_path):
     assert "Total samples in both VCF and PED files: 12" in r.stdout
     exp = gzip.open(os.path.join(EXAMPLE, "testvcf.out.vcf.body.gz"), "rt").read().splitlines()
     assert _body(out) == exp
+
+
+INGEST = os.path.join(os.path.dirname(EXAMPLE), "ingest")
+
+
+@pytest.mark.parametrize("io_threads", [1, 4])
+def test_cpu_driver_ragged_glf_matches_reference(cpu_driver, tmp_path, io_threads):
+    """Parallel GLF ingest (host/ingest.cpp) on ragged GLFs -- per-person position sets, offset-0 repeats,
+    indel records, an early section end, a person without a GLF key, two sections -- reproduces the VCF the
+    reference wrote for the same files (tests/golden/ingest, tools/make_ingest_golden.py), for any thread
+    count."""
+    out = tmp_path / "out.vcf"
+    r = subprocess.run([cpu_driver, "-p", "test.ped", "-d", "test.dat", "-g", "test.gif", "--all_sites",
+                        "--io_threads", str(io_threads), "--out_vcf", str(out)], cwd=INGEST, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:]
+    exp = [l for l in gzip.open(os.path.join(INGEST, "ref.vcf.body.gz"), "rt").read().splitlines() if l]
+    assert _body(out) == exp
+
+
+def test_vcf_fixed_point_formatting_matches_printf(tmp_path):
+    """host/vcf_fmt.h (the allocation-free DS/GQ/DP/PL column formatter) prints exactly what glibc's printf
+    prints: random dosages, exact decimal ties and their neighbours, signed zeros, subnormals."""
+    exe = str(tmp_path / "fmt_check")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-o", exe, os.path.join(os.path.dirname(__file__), "native", "fmt_check.cpp")],
+                   check=True)
+    r = subprocess.run([exe, "300000"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout[-2000:]

@@ -163,3 +163,18 @@ def test_denovo_planted_parity(built, tmp_path, numerics, shape):
     assert (o["emit"] == 1).sum() > 0 and (o["emit"] == 2).sum() > 0, np.unique(o["emit"], return_counts=True)
     assert ((e["call_row"] >= 0) == (o["emit"] == 1)).all()
     assert st["called"] > 0
+
+
+@pytest.mark.parametrize("io_threads", [1, 6])
+def test_cli_ragged_glf_matches_reference(built, tmp_path, io_threads):
+    """The product CLI (parallel GLF ingest + HIP engine) on ragged GLFs reproduces the reference's VCF."""
+    import gzip
+    ingest = os.path.join(os.path.dirname(EXAMPLE), "ingest")
+    out = tmp_path / "out.vcf"
+    r = subprocess.run([pm.BIN_PATH, "-p", "test.ped", "-d", "test.dat", "-g", "test.gif", "--all_sites",
+                        "--io_threads", str(io_threads), "--out_vcf", str(out)], cwd=ingest, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    got = [l for l in out.read_text().splitlines() if not l.startswith("##")]
+    exp = [l for l in gzip.open(os.path.join(ingest, "ref.vcf.body.gz"), "rt").read().splitlines() if l]
+    assert got == exp
