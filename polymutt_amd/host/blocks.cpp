@@ -1,0 +1,193 @@
+// blocks.cpp -- see blocks.h.
+#include "blocks.h"
+#include <algorithm>
+#include <cstring>
+
+namespace pmhost {
+
+BlockWriter::~BlockWriter() { if (fh_) fclose(fh_); }
+
+void BlockWriter::put(const void* p, size_t n) {
+  if (n && fwrite(p, 1, n, fh_) != n) throw FatalError("write to " + path_ + " failed\n");
+  off_ += n;
+}
+
+void BlockWriter::open(const std::string& path, int n_person, int block_sites) {
+  path_ = path;
+  fh_ = fopen(path.c_str(), "wb");
+  if (!fh_) throw FatalError("block file " + path + " can not be opened for output!\n");
+  np_ = n_person; bs_ = block_sites;
+  const uint32_t h[3] = {(uint32_t)n_person, (uint32_t)block_sites, 0};
+  put("PMB1", 4);
+  put(h, sizeof(h));
+}
+
+void BlockWriter::beginSection(const std::string& label, int maxPosition) {
+  if (inSection_) endSection();
+  const int32_t mp = maxPosition;
+  const uint32_t len = (uint32_t)label.size();
+  put("SECT", 4); put(&mp, 4); put(&len, 4); put(label.data(), len);
+  inSection_ = true;
+  sectionSites_ = 0;
+}
+
+void BlockWriter::block(int n, const int* pos, const uint8_t* ref, const uint8_t* pl, const uint32_t* dm) {
+  if (n <= 0) return;
+  index_.push_back({section_, (uint32_t)n, pos[0], pos[n - 1], off_});
+  const uint32_t un = (uint32_t)n;
+  put("BLK1", 4); put(&un, 4);
+  put(pos, sizeof(int) * n);
+  put(ref, n);
+  put(pl, (size_t)n * np_ * 10);
+  put(dm, (size_t)n * np_ * 4);
+  sectionSites_ += n;
+}
+
+void BlockWriter::endSection() {
+  if (!inSection_) return;
+  put("SEND", 4); put(&sectionSites_, 8);
+  inSection_ = false;
+  section_++;
+}
+
+void BlockWriter::close() {
+  if (!fh_) return;
+  endSection();
+  const uint64_t at = off_;
+  const uint32_t nb = (uint32_t)index_.size();
+  put("PIDX", 4); put(&nb, 4);
+  for (const auto& e : index_) { put(&e.section, 4); put(&e.n, 4); put(&e.first_pos, 4); put(&e.last_pos, 4); put(&e.offset, 8); }
+  put(&at, 8); put("PMBE", 4);
+  if (fclose(fh_) != 0) throw FatalError("write to " + path_ + " failed\n");
+  fh_ = nullptr;
+}
+
+// ---------------------------------------------------------------------------------------------
+BlockSiteSource::~BlockSiteSource() { if (fh_) fclose(fh_); }
+
+void BlockSiteSource::get(void* p, size_t n) {
+  if (n && fread(p, 1, n, fh_) != n) throw FatalError("block file " + path_ + " is truncated\n");
+}
+
+void BlockSiteSource::open(const std::string& path, int n_person) {
+  path_ = path;
+  fh_ = fopen(path.c_str(), "rb");
+  if (!fh_) throw FatalError("block file " + path + " can not be opened!\n");
+  char magic[4];
+  uint32_t h[3];
+  get(magic, 4); get(h, sizeof(h));
+  if (memcmp(magic, "PMB1", 4) != 0) throw FatalError(path + " is not a polymutt block file\n");
+  if ((int)h[0] != n_person)
+    throw FatalError(path + ": block file has " + std::to_string(h[0]) + " persons, the pedigree " + std::to_string(n_person) + "\n");
+  np_ = n_person;
+  // index (trailer: u64 index_offset "PMBE")
+  const long here = ftell(fh_);
+  if (fseek(fh_, -12, SEEK_END) == 0) {
+    uint64_t at = 0;
+    char end[4];
+    get(&at, 8); get(end, 4);
+    if (memcmp(end, "PMBE", 4) == 0 && fseek(fh_, (long)at, SEEK_SET) == 0) {
+      char tag[4];
+      uint32_t nb = 0;
+      get(tag, 4); get(&nb, 4);
+      if (memcmp(tag, "PIDX", 4) == 0) {
+        index_.resize(nb);
+        for (auto& e : index_) { get(&e.section, 4); get(&e.n, 4); get(&e.first_pos, 4); get(&e.last_pos, 4); get(&e.offset, 8); }
+      }
+    }
+  }
+  fseek(fh_, here, SEEK_SET);
+}
+
+bool BlockSiteSource::nextSection() {
+  // skip what is left of the current section (the reference's NextSection skips the rest of the records)
+  while (inSection_) loadBlock();
+  char tag[4];
+  if (fread(tag, 1, 4, fh_) != 4 || memcmp(tag, "SECT", 4) != 0) return false;   // "PIDX": no more sections
+  int32_t mp;
+  uint32_t len;
+  get(&mp, 4); get(&len, 4);
+  label_.assign(len, '\0');
+  get(&label_[0], len);
+  maxPos_ = mp;
+  inSection_ = true;
+  ended_ = false;
+  n_ = cur_ = lastBegin_ = 0;
+  return true;
+}
+
+bool BlockSiteSource::loadBlock() {
+  char tag[4];
+  get(tag, 4);
+  if (memcmp(tag, "SEND", 4) == 0) {
+    uint64_t cnt;
+    get(&cnt, 8);
+    inSection_ = false;
+    n_ = cur_ = lastBegin_ = 0;
+    return false;
+  }
+  if (memcmp(tag, "BLK1", 4) != 0) throw FatalError(path_ + ": corrupt block\n");
+  uint32_t n;
+  get(&n, 4);
+  n_ = (int)n;
+  pos_.resize(n); ref_.resize(n); pl_.resize((size_t)n * np_ * 10); dm_.resize((size_t)n * np_);
+  get(pos_.data(), 4 * (size_t)n);
+  get(ref_.data(), n);
+  get(pl_.data(), pl_.size());
+  get(dm_.data(), dm_.size() * 4);
+  cur_ = lastBegin_ = 0;
+  return true;
+}
+
+int BlockSiteSource::nextSites(int maxSites, int* pos, uint8_t* ref) {
+  lastBegin_ = cur_;
+  if (ended_) return 0;
+  if (cur_ == n_ && !loadBlock()) { ended_ = true; return 0; }
+  const int k = std::min(maxSites, n_ - cur_);
+  for (int i = 0; i < k; i++) { pos[i] = pos_[cur_ + i]; ref[i] = ref_[cur_ + i]; }
+  cur_ += k;
+  return k;
+}
+
+void BlockSiteSource::fill(const int* rowOf, uint8_t* pl, uint32_t* dm) {
+  for (int i = 0; i < cur_ - lastBegin_; i++) {
+    const int r = rowOf[i];
+    if (r < 0) continue;
+    const int s = lastBegin_ + i;
+    memcpy(pl + (size_t)r * np_ * 10, pl_.data() + (size_t)s * np_ * 10, (size_t)np_ * 10);
+    memcpy(dm + (size_t)r * np_, dm_.data() + (size_t)s * np_, (size_t)np_ * 4);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+long convert_glf_to_blocks(const Pedigree& ped, const std::string& glfIndexFile, const std::string& out, int io_threads,
+                           int block_sites) {
+  ParallelSiteSource src;
+  src.open(ped, glfIndexFile, io_threads);
+  const int np = (int)ped.column_pid.size();
+  const int bs = std::max(1, block_sites);
+  BlockWriter w;
+  w.open(out, np, bs);
+  std::vector<int> pos(bs), rowOf(src.window());
+  std::vector<uint8_t> ref(bs), pl((size_t)bs * np * 10);
+  std::vector<uint32_t> dm((size_t)bs * np);
+  std::vector<int> wpos(src.window());
+  std::vector<uint8_t> wref(src.window());
+  long total = 0;
+  while (src.nextSection()) {
+    w.beginSection(src.label(), src.maxPosition());
+    int n = 0;
+    while (!src.ended()) {
+      const int got = src.nextSites(std::min(src.window(), bs - n), wpos.data(), wref.data());
+      for (int i = 0; i < got; i++) { rowOf[i] = n + i; pos[n + i] = wpos[i]; ref[n + i] = wref[i]; }
+      src.fill(rowOf.data(), pl.data(), dm.data());
+      n += got;
+      if (n == bs || (src.ended() && n > 0)) { w.block(n, pos.data(), ref.data(), pl.data(), dm.data()); total += n; n = 0; }
+    }
+    w.endSection();
+  }
+  w.close();
+  return total;
+}
+
+}  // namespace pmhost

@@ -1,0 +1,86 @@
+// blocks.h -- the dense indexed site-block format.
+//
+// A .pmb file holds the site stream PedigreeGLF produces from a pedigree's GLF files (the sections, and per
+// site the position, refBase and every person's 10 PL bytes + depth|mapQ), already merged and densified,
+// so a run reads blocks straight into the engine's input layout instead of inflating and merging
+// n_person GLF files per site.  `polymutt --glf2blocks OUT.pmb` writes one; `--in_blocks FILE` reads it in
+// place of `-g` and gives byte-identical VCFs.
+//
+// Layout (little-endian):
+//   header   "PMB1" u32 n_person u32 block_sites u32 0
+//   section  "SECT" i32 maxPosition u32 label_len label[label_len]
+//     block  "BLK1" u32 n  i32 pos[n] (0-based)  u8 ref[n]  u8 pl[n][n_person][10]  u32 dm[n][n_person]
+//   end      "SEND" u64 sites_in_section
+//   index    "PIDX" u32 n_blocks, per block {u32 section, u32 n, i32 first_pos, i32 last_pos, u64 offset}
+//   trailer  u64 index_offset "PMBE"
+// The index gives random access to any block (e.g. one shard of a section per GPU).
+#pragma once
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+#include "ingest.h"
+
+namespace pmhost {
+
+struct BlockIndexEntry {
+  uint32_t section, n;
+  int32_t first_pos, last_pos;
+  uint64_t offset;
+};
+
+class BlockWriter {
+ public:
+  void open(const std::string& path, int n_person, int block_sites);
+  void beginSection(const std::string& label, int maxPosition);
+  void block(int n, const int* pos, const uint8_t* ref, const uint8_t* pl, const uint32_t* dm);
+  void endSection();
+  void close();   // writes the index and the trailer
+  ~BlockWriter();
+
+ private:
+  void put(const void* p, size_t n);
+  FILE* fh_ = nullptr;
+  std::string path_;
+  int np_ = 0, bs_ = 0;
+  uint32_t section_ = 0;
+  uint64_t sectionSites_ = 0, off_ = 0;
+  bool inSection_ = false;
+  std::vector<BlockIndexEntry> index_;
+};
+
+class BlockSiteSource : public SiteStream {
+ public:
+  void open(const std::string& path, int n_person);
+  ~BlockSiteSource();
+  bool nextSection() override;
+  const std::string& label() const override { return label_; }
+  int maxPosition() const override { return maxPos_; }
+  int window() const override { return 1024; }
+  int nextSites(int maxSites, int* pos, uint8_t* ref) override;
+  bool ended() const override { return ended_; }
+  void fill(const int* rowOf, uint8_t* pl, uint32_t* dm) override;
+  const std::vector<BlockIndexEntry>& index() const { return index_; }
+
+ private:
+  bool loadBlock();   // false at the section end marker
+  void get(void* p, size_t n);
+  FILE* fh_ = nullptr;
+  std::string path_;
+  int np_ = 0;
+  std::string label_;
+  int maxPos_ = 0;
+  bool inSection_ = false, ended_ = true;
+  // the loaded block and the cursor into it; the last nextSites call covered [lastBegin_, cur_)
+  std::vector<int> pos_;
+  std::vector<uint8_t> ref_, pl_;
+  std::vector<uint32_t> dm_;
+  int n_ = 0, cur_ = 0, lastBegin_ = 0;
+  std::vector<BlockIndexEntry> index_;
+};
+
+// Converts the GLF site stream of `ped` (index file glfIndexFile) into a .pmb file; returns the site count.
+long convert_glf_to_blocks(const Pedigree& ped, const std::string& glfIndexFile, const std::string& out, int io_threads,
+                           int block_sites);
+
+}  // namespace pmhost

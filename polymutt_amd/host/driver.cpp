@@ -7,6 +7,8 @@
 #include <ctime>
 #include "glf.h"
 #include "ingest.h"
+#include "blocks.h"
+#include <memory>
 #include <thread>
 #include "vcf.h"
 #include "vcf_input.h"
@@ -38,7 +40,8 @@ Options parse_command_line(int argc, char** argv) {
       {"pos", 's', &o.positionFile}, {"all_sites", 'b', &o.all_sites}, {"gl_off", 'b', &o.gl_off},
       {"quick_call", 'b', &o.quick_call},
       // engine options (not in the reference)
-      {"gpu", 'i', &o.device}, {"batch", 'i', &o.batch}, {"io_threads", 'i', &o.io_threads}, {"exact_log10", 'b', &o.exact_log10}, {"numerics", 's', &o.numerics},
+      {"gpu", 'i', &o.device}, {"batch", 'i', &o.batch}, {"io_threads", 'i', &o.io_threads},
+      {"in_blocks", 's', &o.blocksIn}, {"glf2blocks", 's', &o.blocksOut}, {"block_sites", 'i', &o.blockSites}, {"exact_log10", 'b', &o.exact_log10}, {"numerics", 's', &o.numerics},
   };
   auto assign = [](Flag& f, const char* v) {
     switch (f.kind) {
@@ -82,6 +85,14 @@ Options parse_command_line(int argc, char** argv) {
   if (!o.positionFile.empty()) { o.force_call = true; o.quick_call = false; o.all_sites = false; }   // main.cpp:151
   if (o.all_sites) o.quick_call = false;                                                            // main.cpp:153
   return o;
+}
+
+namespace {
+
+}  // namespace
+
+int default_io_threads(const Options& opt) {
+  return opt.io_threads > 0 ? opt.io_threads : std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
 }
 
 namespace {
@@ -134,7 +145,8 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval) {
   print_status(opt);
   if (opt.vcfInFile == opt.vcfOutFile) throw FatalError("Input and output VCF files are the same!\n");
   if (opt.pedFile.empty()) throw FatalError("pedFile not provided for input!\n");
-  if (opt.glfListFile.empty() && opt.vcfInFile.empty()) throw FatalError("glfListFile or input VCF file not provided for input!\n");
+  if (opt.glfListFile.empty() && opt.vcfInFile.empty() && opt.blocksIn.empty())
+    throw FatalError("glfListFile or input VCF file not provided for input!\n");
   if (opt.vcfOutFile.empty()) throw FatalError("vcfOutFile not provided for output!\n");
   if (!opt.vcfInFile.empty()) return run_polymutt_vcf(opt, ped, eval);   // main.cpp:238-246
   if (opt.denovo && opt.denovo_llr < 0) throw FatalError("denovo_min_LLR can only be greater than 0 !\n");
@@ -142,12 +154,17 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval) {
   std::map<std::string, int> positionMap;
   if (!opt.positionFile.empty()) positionMap = load_positions(opt.positionFile);
 
-  ParallelSiteSource src;   // PedigreeGLF with parallel decode (ingest.h)
-  {
-    int io = opt.io_threads;
-    if (io <= 0) io = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
-    src.open(ped, opt.glfListFile, io);
+  std::unique_ptr<SiteStream> srcp;
+  if (!opt.blocksIn.empty()) {   // dense indexed blocks (blocks.h)
+    auto* b = new BlockSiteSource;
+    srcp.reset(b);
+    b->open(opt.blocksIn, (int)ped.column_pid.size());
+  } else {   // PedigreeGLF with parallel decode (ingest.h)
+    auto* g = new ParallelSiteSource;
+    srcp.reset(g);
+    g->open(ped, opt.glfListFile, default_io_threads(opt));
   }
+  SiteStream& src = *srcp;
   FILE* vcf = fopen(opt.vcfOutFile.c_str(), "w");
   if (!vcf) throw FatalError("vcfOutFile can not be opened for output!\n");
 
@@ -235,7 +252,7 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval) {
       src.fill(rowOf.data(), B.pl.data(), B.dm.data());
       t_ingest += now_s() - ti;
       if (B.n == B.cap) flush();
-      if (stop || got < want) break;
+      if (stop || src.ended()) break;
     }
     flush();
     if (stop) { fflush(vcf); return 0; }

@@ -20,6 +20,8 @@ struct Options {
   double denovo_rate = 1.5e-08, denovo_tstv = 2.0, denovo_llr = 0.01;
   int device = 0, batch = 4096;
   int io_threads = 0;   // GLF decode threads (0: min(16, hardware threads))
+  std::string blocksIn, blocksOut;   // --in_blocks FILE (.pmb input in place of -g), --glf2blocks FILE (convert)
+  int blockSites = 4096;
   std::string cmd;
   pm_params params() const;
 };
@@ -37,6 +39,8 @@ class SiteEvaluator {
                    int* n_rows) = 0;
   virtual void counters(pm_counters* out) = 0;
 };
+
+int default_io_threads(const Options& opt);
 
 // Runs the whole analysis; returns the process exit code.
 int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval);

@@ -54,7 +54,22 @@ class TaskPool {
   bool stop_ = false;
 };
 
-class ParallelSiteSource {
+// The driver's view of a site source: sections, then windows of sites and their dense block rows.
+class SiteStream {
+ public:
+  virtual ~SiteStream() {}
+  virtual bool nextSection() = 0;
+  virtual const std::string& label() const = 0;
+  virtual int maxPosition() const = 0;
+  virtual int window() const = 0;
+  // Up to maxSites (<= window) sites of the current section: pos[i] (0-based) and ref[i] (refBase).
+  virtual int nextSites(int maxSites, int* pos, uint8_t* ref) = 0;
+  virtual bool ended() const = 0;   // the current section has no more sites
+  // Rows of the sites of the last nextSites call: site i -> row rowOf[i] (< 0: skipped).
+  virtual void fill(const int* rowOf, uint8_t* pl, uint32_t* dm) = 0;
+};
+
+class ParallelSiteSource : public SiteStream {
  public:
   ParallelSiteSource() = default;
   ParallelSiteSource(const ParallelSiteSource&) = delete;
@@ -62,19 +77,20 @@ class ParallelSiteSource {
   ~ParallelSiteSource();
   // threads: decode/fill workers (the caller counts as one).  window: sites merged per nextSites call at most.
   void open(const Pedigree& ped, const std::string& glfIndexFile, int threads, int window = 1024);
-  bool nextSection();   // PedigreeGLF::Move2NextSection (the files skip to their next section in parallel)
-  const std::string& label() const { return files_[nonNull_].label; }
-  int maxPosition() const { return files_[nonNull_].maxPosition; }
+  bool nextSection() override;   // PedigreeGLF::Move2NextSection (the files skip to their next section in parallel)
+  const std::string& label() const override { return files_[nonNull_].label; }
+  int maxPosition() const override { return files_[nonNull_].maxPosition; }
   int nPerson() const { return (int)files_.size(); }
-  int window() const { return window_; }
+  int window() const override { return window_; }
+  bool ended() const override { return ended_; }
 
   // Advances up to maxSites (<= window) sites of the current section, as that many Move2NextBaseEntry calls
   // would: pos[i] (0-based currentPos) and ref[i] (refBase) of each site.  Returns the count; fewer than
   // maxSites means the section has ended.
-  int nextSites(int maxSites, int* pos, uint8_t* ref);
+  int nextSites(int maxSites, int* pos, uint8_t* ref) override;
   // Writes the block rows of the sites of the last nextSites call: site i goes to row rowOf[i] of pl
   // ([row][n_person][10]) and dm ([row][n_person]); rowOf[i] < 0 skips the site (--pos filtering).
-  void fill(const int* rowOf, uint8_t* pl, uint32_t* dm);
+  void fill(const int* rowOf, uint8_t* pl, uint32_t* dm) override;
 
  private:
   struct Queue {

@@ -4,6 +4,7 @@
 #include <cstdio>
 #include <vector>
 #include "../../include/polymutt_engine.h"
+#include "blocks.h"
 #include "driver.h"
 
 using namespace pmhost;
@@ -34,6 +35,12 @@ int main(int argc, char** argv) {
     Options opt = parse_command_line(argc, argv);
     Pedigree ped;
     ped.load(opt.datFile, opt.pedFile);
+    if (!opt.blocksOut.empty()) {   // --glf2blocks: GLF site stream -> dense indexed blocks, no engine
+      if (opt.glfListFile.empty()) throw FatalError("--glf2blocks needs the GLF index file (-g)\n");
+      const long n = convert_glf_to_blocks(ped, opt.glfListFile, opt.blocksOut, default_io_threads(opt), opt.blockSites);
+      printf("%ld sites written to %s\n", n, opt.blocksOut.c_str());
+      return 0;
+    }
     pm_pedigree v = ped.view();
     pm_params par = opt.params();
     EngineEvaluator ev(v, par, opt.device, opt.batch);

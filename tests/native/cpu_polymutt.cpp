@@ -5,6 +5,7 @@
 // reference's committed goldens.  Never shipped.
 #include <cstdio>
 #include <vector>
+#include "../../polymutt_amd/host/blocks.h"
 #include "../../polymutt_amd/host/driver.h"
 #include "../../oracle/pm_oracle.h"
 
@@ -37,6 +38,10 @@ int main(int argc, char** argv) {
     Options opt = parse_command_line(argc, argv);
     Pedigree ped;
     ped.load(opt.datFile, opt.pedFile);
+    if (!opt.blocksOut.empty()) {
+      printf("%ld sites written\n", convert_glf_to_blocks(ped, opt.glfListFile, opt.blocksOut, default_io_threads(opt), opt.blockSites));
+      return 0;
+    }
     pm_pedigree v = ped.view();
     pm_params par = opt.params();
     OracleEvaluator ev(v, par);

@@ -106,3 +106,41 @@ def test_vcf_fixed_point_formatting_matches_printf(tmp_path):
                    check=True)
     r = subprocess.run([exe, "300000"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout[-2000:]
+
+
+@pytest.mark.parametrize("args,golden", EXAMPLE_RUNS[:1] + EXAMPLE_RUNS[2:], ids=["default_filters", "denovo"])
+def test_cpu_driver_block_format_round_trip(cpu_driver, tmp_path, args, golden):
+    """GLF -> dense indexed blocks (--glf2blocks) -> analysis (--in_blocks) reproduces the reference golden;
+    the block index (polymutt_amd/blocks.py) addresses every block and matches the GLF site stream."""
+    from polymutt_amd import blocks
+    pmb = str(tmp_path / "example.pmb")
+    r = subprocess.run([cpu_driver, "-p", "test.ped", "-d", "test.dat", "-g", "test.gif", "--glf2blocks", pmb,
+                        "--block_sites", "5000"], cwd=EXAMPLE, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:]
+    idx = blocks.read_index(pmb)
+    secs = blocks.read_sections(pmb)
+    assert sum(e["n"] for e in idx) == 81016 and len(secs) >= 1
+    ped = pm.Pedigree(os.path.join(EXAMPLE, "test.dat"), os.path.join(EXAMPLE, "test.ped"))
+    cwd = os.getcwd()
+    os.chdir(EXAMPLE)
+    try:
+        rd = pm.GlfReader(ped, "test.gif")
+        parts = [rd.read(200000) for _ in rd.sections()]
+    finally:
+        os.chdir(cwd)
+    pos, ref, pl, dm = (np.concatenate([p[k].reshape(len(p[1]), -1) if k >= 2 else p[k] for p in parts]) for k in range(4))
+    got = [blocks.read_block(pmb, e) for e in idx]
+    assert np.array_equal(np.concatenate([g[0] for g in got]) + 1, pos)
+    assert np.array_equal(np.concatenate([g[1] for g in got]), ref)
+    assert np.array_equal(np.concatenate([g[2] for g in got]), pl.reshape(len(ref), -1, 10))
+    assert np.array_equal(np.concatenate([g[3] for g in got]), dm.reshape(len(ref), -1))
+    out = tmp_path / "out.vcf"
+    blk_args = [a for a in args]
+    i = blk_args.index("-g")
+    blk_args[i:i + 2] = ["--in_blocks", pmb]
+    r = subprocess.run([cpu_driver] + blk_args + ["--out_vcf", str(out)], cwd=EXAMPLE, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:]
+    p = os.path.join(EXAMPLE, golden)
+    exp = gzip.open(p, "rt").read().splitlines() if p.endswith(".gz") else _body(p)
+    assert _body(out) == exp

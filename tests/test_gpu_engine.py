@@ -178,3 +178,18 @@ def test_cli_ragged_glf_matches_reference(built, tmp_path, io_threads):
     got = [l for l in out.read_text().splitlines() if not l.startswith("##")]
     exp = [l for l in gzip.open(os.path.join(ingest, "ref.vcf.body.gz"), "rt").read().splitlines() if l]
     assert got == exp
+
+
+def test_cli_block_input_reproduces_golden(built, tmp_path):
+    """--glf2blocks then --in_blocks through the product CLI (engine on the GPU) gives the reference golden."""
+    import gzip
+    pmb = str(tmp_path / "example.pmb")
+    r = subprocess.run([pm.BIN_PATH, "-p", "test.ped", "-d", "test.dat", "-g", "test.gif", "--glf2blocks", pmb], cwd=EXAMPLE,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    out = tmp_path / "out.vcf"
+    r = subprocess.run([pm.BIN_PATH, "-p", "test.ped", "-d", "test.dat", "--in_blocks", pmb, "-c", "0.9", "--minDepth", "150",
+                        "--maxDepth", "200", "--out_vcf", str(out)], cwd=EXAMPLE, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    got = [l for l in out.read_text().splitlines() if not l.startswith("##")]
+    assert got == gzip.open(os.path.join(EXAMPLE, "test.out.vcf.body.gz"), "rt").read().splitlines()
