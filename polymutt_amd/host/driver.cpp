@@ -8,7 +8,12 @@
 #include "glf.h"
 #include "ingest.h"
 #include "blocks.h"
+#include <atomic>
 #include <memory>
+#include <condition_variable>
+#include <deque>
+#include <exception>
+#include <mutex>
 #include <thread>
 #include "vcf.h"
 #include "vcf_input.h"
@@ -125,6 +130,50 @@ std::map<std::string, int> load_positions(const std::string& file) {   // LoadPo
   return m;
 }
 
+void print_summary(const std::string& label, int entries, const pm_counters& C, time_t t0) {   // main.cpp:596-620
+  long total = 0;
+  for (int k = 0; k < 5; k++) total += C.ref_base_counts[k];
+  long other = C.tstvs1 + C.tstvs2 + C.tvs1tvs2;
+  printf("Summary of reference -- %s\n", label.c_str());
+  printf("Total Entry Count: %9d\n", entries);
+  printf("Total Base Cout: %9ld\n", total);
+  printf("Non-Polymorphic Count: %9ld\n", (long)C.homo_ref);
+  printf("Transition Count: %9ld\n", (long)C.transitions);
+  printf("Transversion Count: %9ld\n", (long)C.transversions);
+  printf("Other Polymorphism Count: %9ld\n", other);
+  printf("Filter counts:\n");
+  printf("\tminMapQual %u\n", (unsigned)C.min_map_qual_filter);
+  printf("\tminTotalDepth %u\n", (unsigned)C.min_total_depth_filter);
+  printf("\tmaxTotalDepth %u\n", (unsigned)C.max_total_depth_filter);
+  printf("Hard to call: %9ld\n", (long)C.nocall);
+  printf("Skipped bases: %u\n", (unsigned)(entries - C.homo_ref - C.transitions - C.transversions - other));
+  time_t t1; time(&t1);
+  printf("Analysis ended on %s\n", ctime(&t1));
+  printf("Running time is %u seconds\n\n", (unsigned)(t1 - t0));
+}
+
+// A closable blocking FIFO between the pipeline stages.
+template <class T>
+class Channel {
+ public:
+  void push(T v) {
+    { std::lock_guard<std::mutex> l(mu_); q_.push_back(std::move(v)); }
+    cv_.notify_one();
+  }
+  T pop() {
+    std::unique_lock<std::mutex> l(mu_);
+    cv_.wait(l, [&] { return !q_.empty(); });
+    T v = std::move(q_.front());
+    q_.pop_front();
+    return v;
+  }
+
+ private:
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<T> q_;
+};
+
 struct Batch {
   int n = 0, cap = 0, np = 0;
   std::vector<uint8_t> pl, ref;
@@ -154,6 +203,7 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval) {
   std::map<std::string, int> positionMap;
   if (!opt.positionFile.empty()) positionMap = load_positions(opt.positionFile);
 
+  const double t_open0 = now_s();
   std::unique_ptr<SiteStream> srcp;
   if (!opt.blocksIn.empty()) {   // dense indexed blocks (blocks.h)
     auto* b = new BlockSiteSource;
@@ -165,6 +215,7 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval) {
     g->open(ped, opt.glfListFile, default_io_threads(opt));
   }
   SiteStream& src = *srcp;
+  if (getenv("PM_TIMING")) fprintf(stderr, "PM_TIMING open inputs %.3f s\n", now_s() - t_open0);
   FILE* vcf = fopen(opt.vcfOutFile.c_str(), "w");
   if (!vcf) throw FatalError("vcfOutFile can not be opened for output!\n");
 
@@ -201,11 +252,142 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval) {
     }
   } timing_report{t_ingest, t_eval, t_out};
 
+  auto chrom_of = [&](const std::string& label) {
+    return label == opt.chrX ? PM_CHR_X : label == opt.chrY ? PM_CHR_Y : label == opt.MT ? PM_CHR_MT : PM_CHR_AUTO;
+  };
+  if (!opt.force_call && !getenv("PM_SERIAL")) {
+    // Three stages: ingest (producer thread: GLF decode + merge, or block reads, into
+    // batch buffers) -> engine (this thread: one pm_engine_run per batch, in order) -> VCF writer thread
+    // (the batch's records, then the section summary).  Three batch buffers rotate, so the ingest of batch
+    // k+1 and the formatting of batch k-1 overlap the engine on batch k.  Output order is the serial one.
+    // (--pos runs stop after the listed sites, main.cpp:593; they take the serial loop below.)
+    enum { M_SECTION, M_BATCH, M_END, M_DONE };
+    struct Msg { int kind; Batch* b; std::string label; int chrom; int entries; pm_counters C; };
+    const int cap = B.cap;
+    std::vector<std::unique_ptr<Batch>> pool;
+    Channel<Batch*> freeq;
+    for (int i = 0; i < 3; i++) {
+      pool.emplace_back(new Batch);
+      pool.back()->init(cap, np);
+      freeq.push(pool.back().get());
+    }
+    B = Batch();   // the serial path's buffer is not used
+    Channel<Msg> toEngine, toWriter;
+    std::atomic<bool> abort{false};
+    std::exception_ptr perr, eerr, werr;
+    std::thread producer([&] {
+      try {
+        size_t done = 0;
+        std::vector<int> wpos(src.window()), rowOf(src.window());
+        std::vector<uint8_t> wref(src.window());
+        while (!abort && src.nextSection()) {
+          if (!chrSel.empty() && done >= chrSelCount) break;
+          const std::string label = src.label();
+          if (!chrSel.empty() && chrSel[label] < 1) continue;   // the next section's skip consumes this one
+          const int chrom = chrom_of(label);
+          done++;
+          toEngine.push({M_SECTION, nullptr, label, chrom, 0, {}});
+          int entries = 0;
+          Batch* b = freeq.pop();
+          b->n = 0;
+          while (!abort) {
+            const double ti = now_s();
+            const int want = std::min(src.window(), b->cap - b->n);
+            const int got = src.nextSites(want, wpos.data(), wref.data());
+            if (got > 0 && entries == 0) entries = src.maxPosition();
+            for (int k = 0; k < got; k++) {
+              const int i = b->n++;
+              b->pos[i] = wpos[k] + 1;
+              b->ref[i] = wref[k];
+              rowOf[k] = i;
+            }
+            src.fill(rowOf.data(), b->pl.data(), b->dm.data());
+            t_ingest += now_s() - ti;
+            if (b->n == b->cap) {
+              toEngine.push({M_BATCH, b, label, chrom, 0, {}});
+              b = freeq.pop();
+              b->n = 0;
+            }
+            if (src.ended()) break;
+          }
+          if (b->n > 0) toEngine.push({M_BATCH, b, label, chrom, 0, {}});
+          else freeq.push(b);
+          toEngine.push({M_END, nullptr, label, chrom, entries, {}});
+        }
+      } catch (...) {
+        perr = std::current_exception();
+      }
+      toEngine.push({M_DONE, nullptr, "", 0, 0, {}});
+    });
+    std::thread writer([&] {
+      for (;;) {
+        Msg m = toWriter.pop();
+        if (m.kind == M_DONE) break;
+        try {
+          if (m.kind == M_BATCH && !werr) {
+            const double t1 = now_s();
+            W.chrom = m.chrom;
+            const Batch& b = *m.b;
+            for (int i = 0; i < b.n; i++) {
+              const pm_site_result& r = b.res[i];
+              if (!r.emit) continue;
+              W.output(m.label, b.pos[i], b.ref[i], r, r.call_row >= 0 ? b.calls.data() + (size_t)r.call_row * np : nullptr,
+                       b.pl.data() + (size_t)i * np * 10, b.dm.data() + (size_t)i * np);
+            }
+            t_out += now_s() - t1;
+          } else if (m.kind == M_END && !werr) {
+            print_summary(m.label, m.entries, m.C, t0);
+            fflush(vcf);
+          }
+        } catch (...) {
+          werr = std::current_exception();
+          abort = true;
+        }
+        if (m.kind == M_BATCH) freeq.push(m.b);
+      }
+    });
+    for (;;) {   // engine stage
+      Msg m = toEngine.pop();
+      if (m.kind == M_DONE) {
+        toWriter.push(m);
+        break;
+      }
+      if (eerr) {   // draining after an engine error
+        if (m.kind == M_BATCH) freeq.push(m.b);
+        continue;
+      }
+      try {
+        if (m.kind == M_SECTION) eval.begin_section(m.chrom);
+        else if (m.kind == M_BATCH) {
+          int rows = 0;
+          const double te = now_s();
+          Batch& b = *m.b;
+          eval.run(b.n, b.pl.data(), b.dm.data(), b.ref.data(), b.res.data(), b.calls.data(), &rows);
+          t_eval += now_s() - te;
+          toWriter.push(m);
+        } else if (m.kind == M_END) {
+          eval.counters(&m.C);
+          toWriter.push(m);
+        }
+      } catch (...) {
+        eerr = std::current_exception();
+        abort = true;
+        if (m.kind == M_BATCH) freeq.push(m.b);
+      }
+    }
+    producer.join();
+    writer.join();
+    for (auto* e : {&eerr, &perr, &werr})
+      if (*e) std::rethrow_exception(*e);
+    fclose(vcf);
+    return 0;
+  }
+
   while (src.nextSection()) {
     if (!chrSel.empty() && chrDone >= chrSelCount) break;
     const std::string label = src.label();
     if (!chrSel.empty() && chrSel[label] < 1) continue;   // the next section's skip consumes this one
-    int chrom = label == opt.chrX ? PM_CHR_X : label == opt.chrY ? PM_CHR_Y : label == opt.MT ? PM_CHR_MT : PM_CHR_AUTO;
+    const int chrom = chrom_of(label);
     eval.begin_section(chrom);
     W.chrom = chrom;
     chrDone++;
@@ -259,25 +441,7 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval) {
 
     pm_counters C;
     eval.counters(&C);
-    long total = 0;
-    for (int k = 0; k < 5; k++) total += C.ref_base_counts[k];
-    long other = C.tstvs1 + C.tstvs2 + C.tvs1tvs2;
-    printf("Summary of reference -- %s\n", label.c_str());
-    printf("Total Entry Count: %9d\n", entries);
-    printf("Total Base Cout: %9ld\n", total);
-    printf("Non-Polymorphic Count: %9ld\n", (long)C.homo_ref);
-    printf("Transition Count: %9ld\n", (long)C.transitions);
-    printf("Transversion Count: %9ld\n", (long)C.transversions);
-    printf("Other Polymorphism Count: %9ld\n", other);
-    printf("Filter counts:\n");
-    printf("\tminMapQual %u\n", (unsigned)C.min_map_qual_filter);
-    printf("\tminTotalDepth %u\n", (unsigned)C.min_total_depth_filter);
-    printf("\tmaxTotalDepth %u\n", (unsigned)C.max_total_depth_filter);
-    printf("Hard to call: %9ld\n", (long)C.nocall);
-    printf("Skipped bases: %u\n", (unsigned)(entries - C.homo_ref - C.transitions - C.transversions - other));
-    time_t t1; time(&t1);
-    printf("Analysis ended on %s\n", ctime(&t1));
-    printf("Running time is %u seconds\n\n", (unsigned)(t1 - t0));
+    print_summary(label, entries, C, t0);
     fflush(vcf);
   }
   fclose(vcf);

@@ -66,18 +66,30 @@ void ParallelSiteSource::open(const Pedigree& ped, const std::string& glfIndexFi
   qs_ = std::vector<Queue>(n);
   pids_ = ped.column_pid;
   has_.assign(n, 0);
-  for (size_t f = 0; f < ped.families.size(); f++) {   // PedigreeGLF::SetPedGLF, src/PedigreeGLF.cpp:117-163
+  window_ = std::max(1, window);
+  pool_ = new TaskPool(std::max(1, threads));
+  // PedigreeGLF::SetPedGLF (src/PedigreeGLF.cpp:117-163): the file opens (inflate state + header) run in
+  // parallel; warnings and the first open failure are then reported in person order, as the serial loop does
+  std::vector<std::string> path(n), missing(n);
+  for (int j = 0; j < n; j++) {
+    const int idx = ped.column_glf[j];
+    if (idx == 0) continue;
+    const std::string key = std::to_string(idx);
+    auto it = index.find(key);
+    if (it == index.end()) missing[j] = key;
+    else path[j] = it->second;
+  }
+  std::vector<char> ok(n, 0);
+  pool_->run((n + 31) / 32, [&](int c) {
+    for (int j = c * 32; j < std::min(n, (c + 1) * 32); j++)
+      if (!path[j].empty()) ok[j] = files_[j].open(path[j]);
+  });
+  for (size_t f = 0; f < ped.families.size(); f++) {
     int valid = 0;
     for (int j = ped.fam_start[f]; j < ped.fam_start[f + 1]; j++) {
-      const int idx = ped.column_glf[j];
-      if (idx == 0) continue;
-      const std::string key = std::to_string(idx);
-      auto it = index.find(key);
-      if (it == index.end()) {
-        printf("\n\aWARNING - \nNo entry found for the glf with the key [%s]\n\n", key.c_str());
-        continue;
-      }
-      if (!files_[j].open(it->second)) throw FatalError("GLF file " + it->second + " can  not be opened!\n");
+      if (!missing[j].empty()) printf("\n\aWARNING - \nNo entry found for the glf with the key [%s]\n\n", missing[j].c_str());
+      if (path[j].empty()) continue;
+      if (!ok[j]) throw FatalError("GLF file " + path[j] + " can  not be opened!\n");
       has_[j] = 1;
       if (nonNull_ < 0) nonNull_ = j;
       valid++;
@@ -87,8 +99,6 @@ void ParallelSiteSource::open(const Pedigree& ped, const std::string& glfIndexFi
   if (nonNull_ < 0) throw FatalError("No GLF file could be opened\n");
   for (int j = 0; j < n; j++)
     if (has_[j]) active_.push_back(j);
-  window_ = std::max(1, window);
-  pool_ = new TaskPool(std::max(1, threads));
   headAtStart_.assign(n, -1);
   lastPos_.assign(window_, 0);
   virtual_.pos = 0;

@@ -1,7 +1,9 @@
 // main.cpp -- the `polymutt` command line (src/main.cpp:57-627 surface) on the MI355X engine.
 // The site loop body runs on the GPU through the C ABI (include/polymutt_engine.h); there is no CPU
 // fallback: without a usable HIP device the program exits with an error.
+#include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 #include "../../include/polymutt_engine.h"
 #include "blocks.h"
@@ -43,7 +45,11 @@ int main(int argc, char** argv) {
     }
     pm_pedigree v = ped.view();
     pm_params par = opt.params();
+    const auto t0 = std::chrono::steady_clock::now();
     EngineEvaluator ev(v, par, opt.device, opt.batch);
+    if (getenv("PM_TIMING"))
+      fprintf(stderr, "PM_TIMING engine create %.3f s\n",
+              std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
     return run_polymutt(opt, ped, ev);
   } catch (const FatalError& e) {
     printf("\nFATAL ERROR - \n%s\n\n", e.what());
