@@ -737,7 +737,7 @@ __device__ __forceinline__ void hoist_poly4_dn(const DevArgs& A, const int* su, 
     // mutation-matrix rows: laundered per chunk so the compiler re-reads them from LDS instead of keeping
     // all 30 doubles live across the whole hoisting phase (which spills the 5 x S coefficients)
     int r11 = I.g11 * 10, r12 = I.g12 * 10, r22 = I.g22 * 10;
-    asm volatile("" : "+v"(r11), "+v"(r12), "+v"(r22));
+    asm volatile("" : "+v"(r11), "+v"(r12), "+v"(r22));   // (scalar loads from global memory instead: slower)
 #pragma unroll
     for (int j = 0; j < C; j++) {
       const int u = uu[c0 + j];

@@ -13,7 +13,7 @@ cd "$D"
 GPU=""
 for io in $IOS; do
   t0=$(date +%s.%N)
-  timeout -k 10 600 "$R/polymutt_amd/bin/polymutt" -p test.ped -d test.dat -g test.gif --out_vcf gpu.vcf --io_threads $io > gpu.log
+  PM_TIMING=1 timeout -k 10 600 "$R/polymutt_amd/bin/polymutt" -p test.ped -d test.dat -g test.gif --out_vcf gpu.vcf --io_threads $io > gpu.log 2> gpu_$io.err; cat gpu_$io.err >&2
   t1=$(date +%s.%N)
   GPU="$GPU\"io_threads_$io\": $(python3 -c "print(round($t1 - $t0, 3))"), "
 done
