@@ -852,9 +852,15 @@ __device__ __forceinline__ void lane_poly_r(double r, double g4, const double (*
 #pragma unroll
   for (int s = 0; s < S; s++) {
     const double h = fma(r, fma(r, fma(r, fma(r, a[s][0], a[s][1]), a[s][2]), a[s][3]), a[s][4]) * g4;
-    int x;
-    am[s % NA] = frexp(am[s % NA] * h, &x);
-    ae[s % NA] += x;
+    am[s % NA] = am[s % NA] * h;
+    // renormalise after every second factor of an accumulator (and after the last): a nuclear family's
+    // likelihood is >= ~1e-118 (PL <= 255 per person, HWE prior >= 1e-16), so two factors on a mantissa in
+    // [0.5, 1) stay >= 1e-237, clear of underflow; the mantissa bits are those of step-wise renormalisation
+    if ((s / NA) % 2 == 1 || s + NA >= S) {
+      int x;
+      am[s % NA] = frexp(am[s % NA], &x);
+      ae[s % NA] += x;
+    }
   }
 #pragma unroll
   for (int w = 1; w < NA; w *= 2)
