@@ -92,6 +92,7 @@ struct DevArgs {
   const double* T10dn;     // FamilyLikelihoodES::transmission_denovo [10][10][10]
   double* ws;              // peeling workspace, lane-interleaved
   int ws_per_lane;         // doubles per lane (max over ES families of n*ns + couples*ns*ns)
+  int ws_lds;              // ES workspace in dynamic LDS (lane-interleaved) instead of HBM
   int unrelated;           // --quick_call MakeUnrelated(): every family is all-founder
   double theta_one;        // 1.0 (opaque to the compiler; timing experiments only)
   int vcf;                 // vcf_mode: one (ref, alt) Brent per site, FamilyLikelihoodSeq_VCF family rules
@@ -1072,7 +1073,10 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
       }
     }
 #endif
+    // ES workspace: lane-interleaved, in LDS when it fits the block's share (ws_lds), else in HBM (L2-resident)
+    // (two pointers, so each inlined peel keeps a known address space: ds_* or global_* accesses, no flat)
     double* wsl = ES ? A.ws + (size_t)blockIdx.x * A.ws_per_lane * T + threadIdx.x : nullptr;
+    double* wsl_lds = ES ? (double*)s_pf + threadIdx.x : nullptr;
     const bool single = !A.vcf && ((cfg == 0) || (A.single_nuclear && !A.unrelated));
     // One evaluation site for the objective: the three bracketing evaluations of OptimizeFrequency
     // (:432-444) and every Brent step (core/MathGold.cpp:81-177) run through the same loop body.
@@ -1103,8 +1107,9 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
         if (ES && A.ext_count)   // extended families of this lane: Elston-Stewart peeling per evaluation
           for (int q = 0; q < A.ext_count[threadIdx.x]; q++) {
             const int f = A.ext_fam[q * T + threadIdx.x];
-            const double v = I.denovo ? d_es_lk<10>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, x, -1, -1, wsl, T)
-                                      : d_es_lk<3>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, x, -1, -1, wsl, T);
+            const double v = I.denovo  ? d_es_lk<10>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, x, -1, -1, wsl, T)
+                             : A.ws_lds ? d_es_lk<3>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, x, -1, -1, wsl_lds, T)
+                                        : d_es_lk<3>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, x, -1, -1, wsl, T);
             int e1, e2;
             const double mv = frexp(v, &e1);
             m = frexp(m * mv, &e2);
@@ -1116,8 +1121,9 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
         if (ES && A.ext_count)
           for (int q = 0; q < A.ext_count[threadIdx.x]; q++) {
             const int f = A.ext_fam[q * T + threadIdx.x];
-            part += log10(I.denovo ? d_es_lk<10>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, x, -1, -1, wsl, T)
-                                   : d_es_lk<3>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, x, -1, -1, wsl, T));
+            part += log10(I.denovo  ? d_es_lk<10>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, x, -1, -1, wsl, T)
+                          : A.ws_lds ? d_es_lk<3>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, x, -1, -1, wsl_lds, T)
+                                     : d_es_lk<3>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, x, -1, -1, wsl, T));
           }
         tot = block_sum<T>(part, s_red, par);
       }
@@ -2497,6 +2503,19 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
   }
   BrentFn fn = brent_kernel(T, S, E->par.numerics, gen, !unrelated && n_ext > 0, A.denovo != 0, A.pf_npad > 0);
   if (!fn) { pm_set_last_error("launch_brent: no kernel variant for the lane plan"); return PM_EINVAL; }
+  // Elston-Stewart workspace in LDS: every partial / marriage-partial access of the peel becomes an LDS round
+  // trip instead of an L2 one.  Blocks per CU follow from the LDS budget (160 KB per CU).
+  A.ws_lds = 0;
+  if (!unrelated && n_ext > 0 && !E->par.denovo && !getenv("PM_ES_HBM")) {   // BA peels (the 10-state one is too big)
+    const size_t need = (size_t)E->ws_per_lane * T * sizeof(double);
+    if (need > 0 && need <= 150 * 1024) {
+      if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)need) == hipSuccess) {
+        A.ws_lds = 1;
+        shmem = need;
+        grid = E->n_cu * std::max(1, std::min(1024 / T, (int)((160 * 1024) / (need + 8 * 1024))));
+      } else (void)hipGetLastError();
+    }
+  }
   hipEvent_t a, b;
   HIP_TRY(hipEventCreate(&a));
   HIP_TRY(hipEventCreate(&b));
