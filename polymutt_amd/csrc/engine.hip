@@ -381,39 +381,53 @@ __device__ __forceinline__ double d_es_lk(const DevArgs& A, int f, const uint8_t
         for (int x = 0; x < NS; x++)
           for (int y = 0; y < NS; y++) MPP(slot, x, y) = 1.0;
       const int csex = A.sex[p0 + off];
+      double pk[NS];   // the offspring's partial, read once (the workspace may alias: keep it out of the loops)
+#pragma unroll
+      for (int k = 0; k < NS; k++) pk[k] = PP(off, k);
       for (int i = 0; i < NS; i++)
         for (int j = 0; j < NS; j++) {
           double sum = 0;
+#pragma unroll
           for (int k = 0; k < NS; k++) {
             const double t = (NS == 3) ? d_tba(i, j, k, chrom, csex) : A.T10dn[(i * 10 + j) * 10 + k];
-            sum += t * PP(off, k);
+            sum += t * pk[k];
           }
           MPP(slot, i, j) *= sum;
         }
     } else if (type == 2) {   // spouse -> spouse
       const int sf = from0, stt = to0;
+      double ps[NS];
+#pragma unroll
+      for (int j = 0; j < NS; j++) ps[j] = PP(sf, j);
       for (int i = 0; i < NS; i++) {
         double sum = 0.0;
-        if (slot == 255) for (int j = 0; j < NS; j++) sum += PP(sf, j);
-        else if (fa2mo) for (int j = 0; j < NS; j++) sum += PP(sf, j) * MPP(slot, j, i);
-        else for (int j = 0; j < NS; j++) sum += PP(sf, j) * MPP(slot, i, j);
+        if (slot == 255) for (int j = 0; j < NS; j++) sum += ps[j];
+        else if (fa2mo) for (int j = 0; j < NS; j++) sum += ps[j] * MPP(slot, j, i);
+        else for (int j = 0; j < NS; j++) sum += ps[j] * MPP(slot, i, j);
         PP(stt, i) *= sum;
       }
     } else {   // parents -> only offspring
       const int fa = from0, mo = from1, off = to0;
       const int csex = A.sex[p0 + off];
-      for (int k = 0; k < NS; k++) {
-        double sum = 0.0;
-        for (int i = 0; i < NS; i++)
-          for (int j = 0; j < NS; j++) {
+      // loop order (i, j) outer, k inner with NS accumulators: each sum[k] still adds its (i, j) terms in the
+      // reference's order, and every term keeps its association ((fa * m) * mo) * t -- identical results,
+      // with each workspace value read once instead of NS times
+      double pf[NS], pm[NS], sum[NS];
+#pragma unroll
+      for (int k = 0; k < NS; k++) { pf[k] = PP(fa, k); pm[k] = PP(mo, k); sum[k] = 0.0; }
+      for (int i = 0; i < NS; i++)
+        for (int j = 0; j < NS; j++) {
+          const double w = (slot == 255) ? pf[i] * pm[j] : pf[i] * MPP(slot, i, j) * pm[j];
+#pragma unroll
+          for (int k = 0; k < NS; k++) {
             double t;
             if (NS == 3) t = d_tba(i, j, k, chrom, csex);
             else t = (slot == 255) ? A.T10dn[(i * 10 + j) * 10 + k] : A.T10[(i * 10 + j) * 10 + k];   // quirk :1391
-            if (slot == 255) sum += PP(fa, i) * PP(mo, j) * t;
-            else sum += PP(fa, i) * MPP(slot, i, j) * PP(mo, j) * t;
+            sum[k] += w * t;
           }
-        PP(off, k) *= sum;
-      }
+        }
+#pragma unroll
+      for (int k = 0; k < NS; k++) PP(off, k) *= sum[k];
     }
   }
   const int fin = (A.steps[s1 - 1].x >> 24) & 255;
