@@ -1769,6 +1769,43 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
           const int best = d_best3(q11, q12, q22);
           const int8_t lab = dn ? (int8_t)PM_LBL_ALLELES : ((chrom == PM_CHR_Y && sx == FEMALE) ? (int8_t)PM_LBL_DOT : d_vcf_label(chrom, sx));
           d_emit_call(out + p, post, best, lab, post[1] + post[2] * 2);
+        } else if (!dn && chrom == PM_CHR_AUTO && n <= 4) {   // KidJointGenoLikelihood :798-835, autosomal, <= 2 kids
+          // d_kid_geno's autosomal branches with every kid's three likelihoods loaded once and k unrolled; the
+          // products run over the kids in the same order from 1.0, so the values are d_kid_geno's bit for bit
+          double kl[2][3];
+#pragma unroll
+          for (int i = 0; i < 2; i++) {
+            const int pi = p0 + 2 + (2 + i < n ? i : 0);
+            kl[i][0] = s_lk[PLB(pl, np, pi, g11)]; kl[i][1] = s_lk[PLB(pl, np, pi, g12)]; kl[i][2] = s_lk[PLB(pl, np, pi, g22)];
+          }
+          double g[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+          for (int k = 0; k < 9; k++) {
+            double G[3] = {1.0, 1.0, 1.0};
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+              if (2 + i >= n) break;
+              const double l11 = kl[i][0], l12 = kl[i][1], l22 = kl[i][2];
+              double l, q11, q12, q22;
+              switch (k) {
+                case 0: l = l11; q11 = l11; q12 = q22 = 0; break;
+                case 1: case 3: l = 0.5 * (l11 + l12); q11 = l11 * 0.5; q12 = l12 * 0.5; q22 = 0; break;
+                case 2: case 6: l = l12; q11 = 0; q12 = l12; q22 = 0; break;
+                case 4: l = 0.25 * l11 + 0.5 * l12 + 0.25 * l22; q11 = l11 * 0.25; q12 = l12 * 0.5; q22 = l22 * 0.25; break;
+                case 5: case 7: l = 0.5 * (l12 + l22); q11 = 0; q12 = l12 * 0.5; q22 = l22 * 0.5; break;
+                default: l = l22; q11 = 0; q12 = 0; q22 = l22; break;
+              }
+              if (2 + i != j) { G[0] *= l; G[1] *= l; G[2] *= l; }
+              else { G[0] *= q11; G[1] *= q12; G[2] *= q22; }
+            }
+            const double w = pg[k] * pp[k];
+#pragma unroll
+            for (int t = 0; t < 3; t++) g[t] = (k == 0) ? G[t] * w : g[t] + G[t] * w;   // J[0] + J[1] + ... + J[8]
+          }
+          const double sum = g[0] + g[1] + g[2];
+          double post[3] = {0, 0, 0};
+          if (sum != 0.0) { post[0] = g[0] / sum; post[1] = g[1] / sum; post[2] = g[2] / sum; }
+          d_emit_call(out + p, post, d_best3(post[0], post[1], post[2]), d_vcf_label(chrom, sx), post[1] + post[2] * 2);
         } else if (!dn) {   // KidJointGenoLikelihood :798-835
           double J[9][3];
           for (int k = 0; k < 9; k++) {
