@@ -1650,7 +1650,9 @@ __device__ void d_kid_geno(int chrom, const uint8_t* pl, int np, const double* l
   out[0] = G11; out[1] = G12; out[2] = G22;
 }
 
-template <bool DN, bool ES>
+// LEAN: autosome, no extended family, nuclear families of <= 4 persons (the common case): the chrX/Y/MT
+// branches fold away and the generic kid path is not compiled, so the kernel runs at a higher occupancy.
+template <bool DN, bool ES, bool LEAN = false>
 __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
   __shared__ double s_lk[256];
   __shared__ double s_M[100];
@@ -1660,8 +1662,10 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
   const long long work = (long long)A.counts[3] * A.n_fam;
   const size_t gid_base = (size_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (size_t)gridDim.x * blockDim.x;
   for (long long gid = (long long)gid_base; gid < work; gid += (long long)stride) {
-    const int row = (int)(gid / A.n_fam);
-    const int f = (int)(gid % A.n_fam);
+    // 32-bit division when the work index fits (a 64-bit divide is a long software sequence on the GPU)
+    int row, f;
+    if (work < 0xFFFFFFFFll) { const unsigned u = (unsigned)gid, nf = (unsigned)A.n_fam; row = (int)(u / nf); f = (int)(u - (unsigned)row * nf); }
+    else { row = (int)(gid / A.n_fam); f = (int)(gid % A.n_fam); }
     const int site = A.row_site[row];
     const pm_site_result* R = A.res + site;
     const int np = A.n_person;
@@ -1669,7 +1673,7 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
     pm_geno_call* out = A.calls + (size_t)row * np;
     const int a1 = R->allele1, a2 = R->allele2;
     const int g11 = d_gi(a1, a1), g12 = d_gi(a1, a2), g22 = d_gi(a2, a2);
-    const int chrom = A.chrom;
+    const int chrom = LEAN ? (int)PM_CHR_AUTO : A.chrom;
     constexpr int dn = DN ? 1 : 0;
     // CalcPostProb freq (main.cpp:576-587)
     const double freq = (R->maxidx == 0) ? (dn ? 1.0 : 1 - A.theta) : R->af;
@@ -1754,8 +1758,8 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
         const double lF[3] = {F11, F12, F22}, lM[3] = {M11, M12, M22};
         for (int x = 0; x < 3; x++) for (int y = 0; y < 3; y++) pg[3 * x + y] = lF[x] * lM[y];
       }
-      double m[9];
-      for (int k = 0; k < 9; k++) m[k] = cond[k] * pp[k];
+      double m[9], wk[9];   // wk: the kid weights pg[k] * pp[k] of KidJointGenoLikelihood (cond, pg, pp die here)
+      for (int k = 0; k < 9; k++) { m[k] = cond[k] * pp[k]; wk[k] = pg[k] * pp[k]; }
       for (int j = 0; j < n; j++) {
         const int p = p0 + j;
         const int sx = A.sex[p];
@@ -1798,7 +1802,7 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
               if (2 + i != j) { G[0] *= l; G[1] *= l; G[2] *= l; }
               else { G[0] *= q11; G[1] *= q12; G[2] *= q22; }
             }
-            const double w = pg[k] * pp[k];
+            const double w = wk[k];
 #pragma unroll
             for (int t = 0; t < 3; t++) g[t] = (k == 0) ? G[t] * w : g[t] + G[t] * w;   // J[0] + J[1] + ... + J[8]
           }
@@ -1806,6 +1810,7 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
           double post[3] = {0, 0, 0};
           if (sum != 0.0) { post[0] = g[0] / sum; post[1] = g[1] / sum; post[2] = g[2] / sum; }
           d_emit_call(out + p, post, d_best3(post[0], post[1], post[2]), d_vcf_label(chrom, sx), post[1] + post[2] * 2);
+        } else if (LEAN) {   // (every nuclear family has <= 4 persons: the branch above took them)
         } else if (!dn) {   // KidJointGenoLikelihood :798-835
           double J[9][3];
           for (int k = 0; k < 9; k++) {
@@ -2630,8 +2635,9 @@ static int run_pipeline(pm_engine* E, int n, const uint8_t* pl, const uint32_t* 
   HIP_TRY(hipGetLastError());
   {
     const bool es = (E->use_plan1 ? E->n_ext1 : E->n_ext) > 0;
+    const bool lean = !E->par.denovo && !es && E->chrom == PM_CHR_AUTO && E->max_nuc <= 4 && !E->use_plan1;
     void (*post)(DevArgs) = E->par.denovo ? (es ? k_posterior<true, true> : k_posterior<true, false>)
-                                          : (es ? k_posterior<false, true> : k_posterior<false, false>);
+                          : es ? k_posterior<false, true> : lean ? k_posterior<false, false, true> : k_posterior<false, false>;
     hipLaunchKernelGGL(post, dim3(E->grid_post), dim3(256), 0, E->stream, A);
   }
   HIP_TRY(hipGetLastError());
