@@ -99,6 +99,7 @@ struct DevArgs {
   int nuc_es;              // nuclear families are peeled (vcf_mode plan 1)
   int mono_dn;             // k_prep computes the de novo monomorphism item (cfg 0) itself (lean --denovo)
   int pf_npad;             // lean kernel: > 0 = the item's 3 genotype planes are prefetched into LDS (stride)
+  int dn_pf;               // lean --denovo kernel: PL windows staged through LDS by LDS-DMA (hoist_poly4_dn_pf)
   // tables
   const double* lktab;     // [256]
   const double* M;         // [100] genotype mutation matrix
@@ -821,6 +822,111 @@ __device__ __forceinline__ void hoist_poly4_dn(const DevArgs& A, const int* su, 
   }
 }
 
+// hoist_poly4_dn with the PL bytes staged through LDS by LDS-DMA (A.dn_pf): the lean plan deals families
+// round-robin, so the 64 families of one wave in one slot row are consecutive and their persons form one
+// window of <= 256 bytes per genotype plane.  A chunk of DN_PF_C slots needs 10 planes x DN_PF_C windows
+// (272 B each: the 16-B aligned start plus slack), fetched with global_load_lds_dwordx4 into this wave's
+// half of a double buffer while the previous chunk is hoisted; every byte is then an LDS read.  Needs
+// n_person % 16 == 0 (16-B aligned planes).  Arithmetic and order are hoist_poly4_dn's.
+#define DN_PF_C 2
+#define DN_PF_WIN 272
+#define DN_PF_BUF 6144   // per wave per chunk: 10 x DN_PF_C x 272 = 5440 B, issued as 6 x 1 KB
+__device__ __forceinline__ void dn_pf_issue(const DevArgs& A, const uint8_t* pl, const int* start_al, uint8_t* dst) {
+  const int lane = threadIdx.x & 63, np = A.n_person;
+#pragma unroll
+  for (int i = 0; i < DN_PF_BUF / 1024; i++) {
+    int P = i * 1024 + lane * 16;
+    if (P >= 10 * DN_PF_C * DN_PF_WIN) P = 10 * DN_PF_C * DN_PF_WIN - 16;   // tail lanes: any valid source
+    const int w = P / DN_PF_WIN, j = w / 10, g = w - 10 * j, off = P - w * DN_PF_WIN;
+    const int src = min(start_al[j] + off, np - 16);
+    __builtin_amdgcn_global_load_lds((const void*)(pl + (size_t)g * np + src), (void*)(dst + i * 1024), 16, 0, 0);
+  }
+}
+
+template <int S, int T>
+__device__ __forceinline__ void hoist_poly4_dn_pf(const DevArgs& A, const int* su, const ItemCtx& I, const uint8_t* pl,
+                                                  const double* lk, const double* M, double (*a)[5], unsigned& live,
+                                                  uint8_t* wbuf) {
+  static_assert(S % DN_PF_C == 0, "chunking");
+  constexpr int C = DN_PF_C;
+  const int wv = threadIdx.x >> 6;
+  int uu[S];
+  load_units<S>(su, uu);
+  // window start per slot: the first person of this wave's lane-0 family (uniform), aligned down to 16 B
+  int start_al[S];
+#pragma unroll
+  for (int s = 0; s < S; s++) start_al[s] = __builtin_amdgcn_readfirstlane(unit_first(su[(wv * 64) * S + s]) & ~15);
+  __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the previous item's reads of this wave's buffers are done
+  __builtin_amdgcn_sched_barrier(0);
+  dn_pf_issue(A, pl, start_al, wbuf);
+#pragma unroll
+  for (int c0 = 0; c0 < S; c0 += C) {
+    uint8_t* cur = wbuf + ((c0 / C) & 1) * DN_PF_BUF;
+    if (c0 + C < S) {
+      __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the reads of the buffer about to be refilled are done
+      __builtin_amdgcn_sched_barrier(0);
+      dn_pf_issue(A, pl, start_al + c0 + C, wbuf + (((c0 / C) + 1) & 1) * DN_PF_BUF);
+      __builtin_amdgcn_s_waitcnt(0x0F76);   // vmcnt(6): this chunk's 6 DMA instructions have landed
+    } else {
+      __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    int r11 = I.g11 * 10, r12 = I.g12 * 10, r22 = I.g22 * 10;
+    asm volatile("" : "+v"(r11), "+v"(r12), "+v"(r22));
+#pragma unroll
+    for (int j = 0; j < C; j++) {
+      const int u = uu[c0 + j];
+      const int nn = unit_nn(u);
+      if (u != 0) live |= 1u << (c0 + j);
+      const uint8_t* W = cur + j * 10 * DN_PF_WIN;   // plane g of this slot at W[g * DN_PF_WIN + person - start]
+      const int rel = u ? unit_first(u) - start_al[c0 + j] : 0;
+      uint32_t par[6];
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const int pp = rel + (q < nn ? q : 0);
+        par[3 * q + 0] = W[I.g11 * DN_PF_WIN + pp];
+        par[3 * q + 1] = W[I.g12 * DN_PF_WIN + pp];
+        par[3 * q + 2] = W[I.g22 * DN_PF_WIN + pp];
+      }
+      double kids[9];
+#pragma unroll
+      for (int k = 0; k < 9; k++) kids[k] = 1.0;
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const int pk = rel + (q + 2 < nn ? q + 2 : 0);
+        double D11 = 0.0, D12 = 0.0, D22 = 0.0;
+        if (I.denovo) {   // uniform per item
+#pragma unroll
+          for (int g = 0; g < 10; g++) {
+            const double pg = lk[W[g * DN_PF_WIN + pk]];
+            D11 = fma(M[r11 + g], pg, D11);
+            D12 = fma(M[r12 + g], pg, D12);
+            D22 = fma(M[r22 + g], pg, D22);
+          }
+        } else {   // cfg-7 items: likelihoodONEKid's autosomal terms
+          D11 = lk[W[I.g11 * DN_PF_WIN + pk]]; D12 = lk[W[I.g12 * DN_PF_WIN + pk]]; D22 = lk[W[I.g22 * DN_PF_WIN + pk]];
+        }
+        const bool isKid = q + 2 < nn;
+#pragma unroll
+        for (int k = 0; k < 9; k++) kids[k] *= isKid ? d_one_kid_dn(k, D11, D12, D22) : 1.0;
+      }
+      const double lF[3] = {lk[par[0]], lk[par[1]], lk[par[2]]};
+      const double lM[3] = {lk[par[3]], lk[par[4]], lk[par[5]]};
+      const bool fam = nn >= 2;
+      double c9[9];
+#pragma unroll
+      for (int x = 0; x < 3; x++)
+#pragma unroll
+        for (int y = 0; y < 3; y++) c9[3 * x + y] = fam ? kids[3 * x + y] * (lF[x] * lM[y]) : 0.0;
+      fold_poly(c9, a[c0 + j]);
+      if (nn == 0) {
+        a[c0 + j][0] = 1.0; a[c0 + j][1] = 4.0; a[c0 + j][2] = 6.0; a[c0 + j][3] = 4.0; a[c0 + j][4] = 1.0;
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // Four interleaved (mantissa, exponent) accumulators: short dependency chains, few live registers.
 // Slots below `full` are occupied on every lane (families are dealt round-robin); only the slot rows at
 // or above it can be empty and are masked (h = 1).  LO selects the Horner direction (t = f / (1 - f) or
@@ -1046,7 +1152,12 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
         }
       }
       if (!PFK && !hoisted && A.max_nuc <= 4) {
-        if constexpr (DN) hoist_poly4_dn<S, T>(A, s_u, I, pl, s_lk, s_M, cond, live);   // de novo and cfg-7 items
+        if constexpr (DN) {   // de novo and cfg-7 items
+          if constexpr (S % DN_PF_C == 0) {
+            if (A.dn_pf) hoist_poly4_dn_pf<S, T>(A, s_u, I, pl, s_lk, s_M, cond, live, s_pf + (threadIdx.x >> 6) * 2 * DN_PF_BUF);
+            else hoist_poly4_dn<S, T>(A, s_u, I, pl, s_lk, s_M, cond, live);
+          } else hoist_poly4_dn<S, T>(A, s_u, I, pl, s_lk, s_M, cond, live);
+        }
         else hoist_poly4<S, T>(A, s_u, I, pl, s_lk, cond, live);
         hoisted = true;
       }
@@ -2556,6 +2667,13 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
       !getenv("PM_NO_PREFETCH")) {
     A.pf_npad = (E->n_person + 1023) / 1024 * 1024;
     shmem = (size_t)3 * A.pf_npad;
+  }
+  // lean --denovo kernel: LDS-DMA staging of the PL windows (double buffer per wave)
+  A.dn_pf = 0;
+  if (!gen && !unrelated && n_ext == 0 && A.denovo && E->par.numerics == PM_NUM_POLY && E->max_nuc <= 4 && S % DN_PF_C == 0 &&
+      E->n_person % 16 == 0 && E->n_person >= 16 && !getenv("PM_NO_PREFETCH")) {
+    A.dn_pf = 1;
+    shmem = (size_t)(T / 64) * 2 * DN_PF_BUF;
   }
   BrentFn fn = brent_kernel(T, S, E->par.numerics, gen, !unrelated && n_ext > 0, A.denovo != 0, A.pf_npad > 0);
   if (!fn) { pm_set_last_error("launch_brent: no kernel variant for the lane plan"); return PM_EINVAL; }

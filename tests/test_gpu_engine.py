@@ -122,14 +122,16 @@ def test_synthetic_device_generator_and_parity(built, shape, nfam, nsites, tmp_p
 
 
 
-def test_plane_prefetch_bit_identical(built, tmp_path, monkeypatch):
-    """The lean kernel's LDS plane prefetch (taken when n_person % 16 == 0) gives bit-identical results to the
-    direct-load hoisting (PM_NO_PREFETCH=1), and both match the oracle."""
+@pytest.mark.parametrize("shape,nfam,denovo", [("quad", 64, 0), ("quad+dn", 64, 1), ("trio+dn", 64, 1), ("quad+dn", 300, 1)])
+def test_plane_prefetch_bit_identical(built, tmp_path, monkeypatch, shape, nfam, denovo):
+    """The lean kernels' LDS staging of the PL bytes (plain: the item's 3 planes; --denovo: per-wave windows of
+    all 10 planes, double-buffered by LDS-DMA), taken when n_person % 16 == 0, gives bit-identical results to
+    the direct-load hoisting (PM_NO_PREFETCH=1), and both match the oracle."""
     d = str(tmp_path / "pf")
-    pm.synth_write_dataset(d, "quad", 64, 500, 13)   # 256 persons: 16-B aligned planes
+    pm.synth_write_dataset(d, shape, nfam, 500, 13)   # 256 / 192 / 1200 persons: 16-B aligned planes
     ped = pm.Pedigree(os.path.join(d, "test.dat"), os.path.join(d, "test.ped"))
     label, pos, ref, pl, dm = _read_all(ped, d)[0]
-    params = pm.Params.defaults(numerics=pm.NUM_POLY)
+    params = pm.Params.defaults(numerics=pm.NUM_POLY, denovo=denovo, denovo_mut_rate=1e-5 if denovo else 1.5e-8)
     outs = []
     for nopf in ("", "1"):
         if nopf:
