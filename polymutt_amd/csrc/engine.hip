@@ -98,6 +98,7 @@ struct DevArgs {
   int vcf;                 // vcf_mode: one (ref, alt) Brent per site, FamilyLikelihoodSeq_VCF family rules
   int nuc_es;              // nuclear families are peeled (vcf_mode plan 1)
   int mono_dn;             // k_prep computes the de novo monomorphism item (cfg 0) itself (lean --denovo)
+  int* row_blk;            // k_rows_count / k_rows: written records per 1024-site block
   int pf_npad;             // lean kernel: > 0 = the item's 3 genotype planes are prefetched into LDS (stride)
   int dn_pf;               // lean --denovo kernel: PL windows staged through LDS by LDS-DMA (hoist_poly4_dn_pf)
   // tables
@@ -2025,33 +2026,48 @@ __global__ void __launch_bounds__(256) k_ab(DevArgs A) {
   }
 }
 
-__global__ void k_rows(DevArgs A) {
-  // written records -> rows, in site order (single block scan; batches are <= a few million sites)
-  __shared__ int s_base;
-  if (threadIdx.x == 0) s_base = 0;
+// Written records -> genotype rows, in site order, as a two-pass multi-block scan over 1024-site blocks
+// (the single-block loop it replaces read the 240-B results at a 240-B stride, 64 sequential rounds per
+// 65 536 sites).  Rows exist only for written records: an OutputVCF_denovo call that returns before the
+// record (emit 2, NucFamGenotypeLikelihood.cpp:1868) has no observable genotype output.
+__device__ __forceinline__ int block_excl_scan_1024(int e, int* s_w, int& total) {
+  const unsigned long long bal = __ballot(e);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) s_w[wv] = __popcll(bal);
   __syncthreads();
-  for (int base = 0; base < A.n; base += blockDim.x) {
-    const int site = base + threadIdx.x;
-    // rows only for written records: an OutputVCF_denovo call that returns before the record (emit 2,
-    // NucFamGenotypeLikelihood.cpp:1868) has no observable genotype output, so its posteriors are skipped
-    const int em = site < A.n ? A.res[site].emit : 0;
-    const int e = em == 1 ? 1 : 0;
-    if (em == 2) A.res[site].call_row = -1;
-    // wave-level exclusive scan via ballot
-    const unsigned long long bal = __ballot(e);
-    const int lane = threadIdx.x & 63;
-    const int wpre = __popcll(bal & ((1ull << lane) - 1ull));
-    __shared__ int s_w[16];
-    if (lane == 0) s_w[threadIdx.x >> 6] = __popcll(bal);
-    __syncthreads();
-    int off = s_base;
-    for (int w = 0; w < (int)(threadIdx.x >> 6); w++) off += s_w[w];
-    if (e) { const int row = off + wpre; A.res[site].call_row = row; A.row_site[row] = site; }
-    __syncthreads();
-    if (threadIdx.x == 0) { int t = 0; for (int w = 0; w < (int)(blockDim.x >> 6); w++) t += s_w[w]; s_base += t; }
-    __syncthreads();
+  int off = 0, t = 0;
+  for (int w = 0; w < (int)(blockDim.x >> 6); w++) { if (w < wv) off += s_w[w]; t += s_w[w]; }
+  total = t;
+  return off + __popcll(bal & ((1ull << lane) - 1ull));
+}
+
+__global__ void __launch_bounds__(1024) k_rows_count(DevArgs A) {
+  __shared__ int s_w[16];
+  const int site = blockIdx.x * 1024 + threadIdx.x;
+  const int e = (site < A.n && A.res[site].emit == 1) ? 1 : 0;
+  int total;
+  (void)block_excl_scan_1024(e, s_w, total);
+  if (threadIdx.x == 0) A.row_blk[blockIdx.x] = total;
+}
+
+__global__ void __launch_bounds__(1024) k_rows(DevArgs A) {
+  __shared__ int s_w[16];
+  __shared__ int s_base;
+  if (threadIdx.x < 64) {   // rows of the blocks before this one
+    int b = 0;
+    for (int i = threadIdx.x; i < (int)blockIdx.x; i += 64) b += A.row_blk[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) b += __shfl_xor(b, o, 64);
+    if (threadIdx.x == 0) s_base = b;
   }
-  if (threadIdx.x == 0) A.counts[3] = s_base;
+  const int site = blockIdx.x * 1024 + threadIdx.x;
+  const int em = site < A.n ? A.res[site].emit : 0;
+  const int e = em == 1 ? 1 : 0;
+  if (em == 2) A.res[site].call_row = -1;
+  int total;
+  const int pre = block_excl_scan_1024(e, s_w, total);   // (its __syncthreads also publishes s_base)
+  if (e) { const int row = s_base + pre; A.res[site].call_row = row; A.row_site[row] = site; }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) A.counts[3] = s_base + total;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2137,6 +2153,7 @@ struct pm_engine {
   int* d_counts = nullptr;
   unsigned long long* d_eval_total = nullptr;
   int* d_row_site = nullptr;
+  int* d_row_blk = nullptr;   // k_rows_count: written records per 1024-site block
   unsigned long long* d_counters = nullptr;
   double M_h[100];
   // stats
@@ -2291,7 +2308,7 @@ void pm_engine_destroy(pm_engine* E) {
                   E->d_fam_start, E->d_fam_kind, E->d_fa, E->d_mo, E->d_sex, E->d_units, E->d_lktab, E->d_M, E->d_syn,
                   E->d_pl, E->d_stage, E->d_ref, E->d_dm, E->d_res, E->d_calls, E->d_raw, E->d_minv, E->d_mono, E->d_evals,
                   E->d_item_sex, E->d_items[0], E->d_items[1], E->d_items[2], E->d_counts, E->d_eval_total, E->d_row_site,
-                  E->d_counters};
+                  E->d_counters, E->d_row_blk};
   for (void* b : bufs) if (b) hipFree(b);
   for (auto& pr : E->brent_events) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
   if (E->ev0) hipEventDestroy(E->ev0);
@@ -2531,6 +2548,7 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
   DALLOC(E->d_counts, 16);
   DALLOC(E->d_eval_total, 1);
   DALLOC(E->d_row_site, nb);
+  DALLOC(E->d_row_blk, nb / 1024 + 2);
   DALLOC(E->d_counters, 16);
   HIP_TRY(hipMemset(E->d_counters, 0, 16 * sizeof(unsigned long long)));
   HIP_TRY(hipMemset(E->d_eval_total, 0, sizeof(unsigned long long)));
@@ -2605,7 +2623,7 @@ static DevArgs make_args(pm_engine* E, int n, const uint8_t* pl, const uint32_t*
   A.n = n; A.pl = pl; A.dm = dm; A.ref = ref; A.res = res; A.calls = calls;
   A.raw = E->d_raw; A.minv = E->d_minv; A.evals = E->d_evals; A.mono_plain = E->d_mono; A.item_sex = E->d_item_sex;
   for (int l = 0; l < N_LISTS; l++) A.items[l] = E->d_items[l];
-  A.counts = E->d_counts; A.eval_total = E->d_eval_total; A.row_site = E->d_row_site; A.counters = E->d_counters;
+  A.counts = E->d_counts; A.eval_total = E->d_eval_total; A.row_site = E->d_row_site; A.row_blk = E->d_row_blk; A.counters = E->d_counters;
   A.carry_postprob = E->carry_postprob ? 1 : 0;
   A.mono_dn = mono_dn_in_prep(E) ? 1 : 0;
   return A;
@@ -2749,7 +2767,11 @@ static int run_pipeline(pm_engine* E, int n, const uint8_t* pl, const uint32_t* 
     hipLaunchKernelGGL(k_final_dn, dim3(gb), dim3(tb), 0, E->stream, A);
     HIP_TRY(hipGetLastError());
   }
-  hipLaunchKernelGGL(k_rows, dim3(1), dim3(1024), 0, E->stream, A);
+  {
+    const int nb = std::max(1, (n + 1023) / 1024);
+    hipLaunchKernelGGL(k_rows_count, dim3(nb), dim3(1024), 0, E->stream, A);
+    hipLaunchKernelGGL(k_rows, dim3(nb), dim3(1024), 0, E->stream, A);
+  }
   HIP_TRY(hipGetLastError());
   {
     const bool es = (E->use_plan1 ? E->n_ext1 : E->n_ext) > 0;
