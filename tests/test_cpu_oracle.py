@@ -144,3 +144,21 @@ def test_cpu_driver_block_format_round_trip(cpu_driver, tmp_path, args, golden):
     p = os.path.join(EXAMPLE, golden)
     exp = gzip.open(p, "rt").read().splitlines() if p.endswith(".gz") else _body(p)
     assert _body(out) == exp
+
+
+def test_block_file_rejects_mismatched_or_truncated_input(cpu_driver, tmp_path):
+    """--in_blocks fails loudly (reference-style FATAL ERROR, exit 1) on a block file written for another
+    pedigree size or cut short, instead of analysing garbage."""
+    pmb = str(tmp_path / "ragged.pmb")
+    r = subprocess.run([cpu_driver, "-p", "test.ped", "-d", "test.dat", "-g", "test.gif", "--glf2blocks", pmb],
+                       cwd=INGEST, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:]
+    raw = open(pmb, "rb").read()
+    cut = str(tmp_path / "cut.pmb")
+    open(cut, "wb").write(raw[: len(raw) // 2])
+    r = subprocess.run([cpu_driver, "-p", "test.ped", "-d", "test.dat", "--in_blocks", cut, "--out_vcf", str(tmp_path / "o.vcf")],
+                       cwd=INGEST, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 1 and "FATAL ERROR" in r.stdout and "truncated" in r.stdout
+    r = subprocess.run([cpu_driver, "-p", os.path.join(EXAMPLE, "test.ped"), "-d", os.path.join(EXAMPLE, "test.dat"),
+                        "--in_blocks", pmb, "--out_vcf", str(tmp_path / "o2.vcf")], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 1 and "persons" in r.stdout
