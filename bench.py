@@ -4,7 +4,7 @@
 Metric (BASELINE.json): sites/s for the whole node, 1000 nuclear quad families, synthetic GLF-shaped sites
 (SURVEY.md 8(d) recipe, generated on the device), plus achieved HBM GB/s.  Default workload = BASELINE config 3,
 the configuration the metric is quoted on: 1000 nuclear quads x 10M sites with the --denovo MutationModel
-(160 steps x 65 536 sites = 10.5M sites per GPU); --no-denovo gives the plain quad model.  A "step" = one pass of the
+(40 steps x 262 144 sites = 10.5M sites per GPU); --no-denovo gives the plain quad model.  A "step" = one pass of the
 full per-site path (read stats, filters, monomorphism, 3(+3) Brent-optimised allele configurations, model
 selection, de novo LR with --denovo, genotype posteriors, allele balance) over one batch of sites already
 resident in HBM.
@@ -45,7 +45,7 @@ FP64_NONFMA_TOPS = 39.3       # mul/add issue rate = half the FMA-counted peak (
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=160)
+    ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--families", type=int, default=1000)
     ap.add_argument("--shape", choices=["quad", "trio", "ext10", "mixed"], default="quad",
@@ -55,7 +55,7 @@ def parse():
     ap.add_argument("--denovo", dest="denovo", action="store_true", default=True,
                     help="BASELINE config 3: --denovo MutationModel (default)")
     ap.add_argument("--no-denovo", dest="denovo", action="store_false", help="plain (non-de-novo) quad model")
-    ap.add_argument("--batch", type=int, default=65536, help="sites per step per GPU")
+    ap.add_argument("--batch", type=int, default=262144, help="sites per step per GPU (40 x 262 144 = 10.5 M sites)")
     ap.add_argument("--pool", type=int, default=4, help="distinct resident batches cycled by the steps")
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--cpu-sites", type=int, default=1500)
