@@ -122,13 +122,14 @@ def test_synthetic_device_generator_and_parity(built, shape, nfam, nsites, tmp_p
 
 
 
-@pytest.mark.parametrize("shape,nfam,denovo", [("quad", 64, 0), ("quad+dn", 64, 1), ("trio+dn", 64, 1), ("quad+dn", 300, 1)])
-def test_plane_prefetch_bit_identical(built, tmp_path, monkeypatch, shape, nfam, denovo):
+@pytest.mark.parametrize("shape,nfam,denovo,nsites", [("quad", 64, 0, 500), ("quad+dn", 64, 1, 500), ("trio+dn", 64, 1, 500),
+                                                     ("quad+dn", 300, 1, 300), ("quad+dn", 600, 1, 150), ("trio+dn", 528, 1, 150)])
+def test_plane_prefetch_bit_identical(built, tmp_path, monkeypatch, shape, nfam, denovo, nsites):
     """The lean kernels' LDS staging of the PL bytes (plain: the item's 3 planes; --denovo: per-wave windows of
     all 10 planes, double-buffered by LDS-DMA), taken when n_person % 16 == 0, gives bit-identical results to
     the direct-load hoisting (PM_NO_PREFETCH=1), and both match the oracle."""
     d = str(tmp_path / "pf")
-    pm.synth_write_dataset(d, shape, nfam, 500, 13)   # 256 / 192 / 1200 persons: 16-B aligned planes
+    pm.synth_write_dataset(d, shape, nfam, nsites, 13)   # n_person % 16 == 0; > 512 families: the 2-wave (128 x 8) plan
     ped = pm.Pedigree(os.path.join(d, "test.dat"), os.path.join(d, "test.ped"))
     label, pos, ref, pl, dm = _read_all(ped, d)[0]
     params = pm.Params.defaults(numerics=pm.NUM_POLY, denovo=denovo, denovo_mut_rate=1e-5 if denovo else 1.5e-8)
