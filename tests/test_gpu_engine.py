@@ -196,3 +196,22 @@ def test_cli_block_input_reproduces_golden(built, tmp_path):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     got = [l for l in out.read_text().splitlines() if not l.startswith("##")]
     assert got == gzip.open(os.path.join(EXAMPLE, "test.out.vcf.body.gz"), "rt").read().splitlines()
+
+
+@pytest.mark.parametrize("denovo", [0, 1])
+def test_headline_config_parity(built, denovo):
+    """The bench's own workload (BASELINE config 3: 1000 nuclear quads, the bench pedigree and site generator,
+    the geometry and kernels the bench runs -- 2-wave de novo plan with LDS-staged PL windows, or the 1-wave
+    plain plan with plane prefetch) against the CPU oracle on the first 1024 sites."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    ped = bench.nuclear_pedigree(pm, 1000, 2)
+    pl, dm, ref = pm.synth_block_host(ped, 1024, 7)
+    params = pm.Params.defaults(denovo=denovo)
+    eng = pm.Engine(ped, params, max_batch=1024)
+    e, ec = eng.run(pl, dm, ref)
+    eng.close()
+    o, oc = Oracle(ped, params).run(pl, dm, ref)
+    st = compare_results(e, o, ec, oc, label="headline ")
+    assert st["sites"] == 1024 and st["called"] > 0
