@@ -127,7 +127,7 @@ def test_synthetic_device_generator_and_parity(built, shape, nfam, nsites, tmp_p
 def test_plane_prefetch_bit_identical(built, tmp_path, monkeypatch, shape, nfam, denovo, nsites):
     """The lean kernels' LDS staging of the PL bytes (plain: the item's 3 planes; --denovo: per-wave windows of
     all 10 planes, double-buffered by LDS-DMA), taken when n_person % 16 == 0, gives bit-identical results to
-    the direct-load hoisting (PM_NO_PREFETCH=1), and both match the oracle."""
+    the direct-load hoisting (PM_NO_PREFETCH=1) on the same lane plan, and both match the oracle."""
     d = str(tmp_path / "pf")
     pm.synth_write_dataset(d, shape, nfam, nsites, 13)   # n_person % 16 == 0; > 512 families: the 2-wave (128 x 8) plan
     ped = pm.Pedigree(os.path.join(d, "test.dat"), os.path.join(d, "test.ped"))
@@ -141,9 +141,11 @@ def test_plane_prefetch_bit_identical(built, tmp_path, monkeypatch, shape, nfam,
         outs.append(eng.run(pl, dm, ref))
         eng.close()
     (a, ac), (b, bc) = outs
-    assert a.tobytes() == b.tobytes() and ac.tobytes() == bc.tobytes()
+    if nfam <= 512:   # same lane plan both ways (above 512 --denovo families, staging selects the 64 x 16 plan)
+        assert a.tobytes() == b.tobytes() and ac.tobytes() == bc.tobytes()
     o, oc = Oracle(ped.view, params).run(pl, dm, ref)
     assert compare_results(a, o, ac, oc, label="prefetch ")["called"] > 0
+    assert compare_results(b, o, bc, oc, label="direct ")["called"] > 0
 
 
 @pytest.mark.parametrize("numerics", [pm.NUM_PRODUCT, pm.NUM_POLY])
