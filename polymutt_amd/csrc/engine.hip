@@ -829,9 +829,11 @@ __device__ __forceinline__ void hoist_poly4_dn(const DevArgs& A, const int* su, 
 // (272 B each: the 16-B aligned start plus slack), fetched with global_load_lds_dwordx4 into this wave's
 // half of a double buffer while the previous chunk is hoisted; every byte is then an LDS read.  Needs
 // n_person % 16 == 0 (16-B aligned planes).  Arithmetic and order are hoist_poly4_dn's.
-#define DN_PF_C 2
+#ifndef DN_PF_C
+#define DN_PF_C 1
+#endif
 #define DN_PF_WIN 272
-#define DN_PF_BUF 6144   // per wave per chunk: 10 x DN_PF_C x 272 = 5440 B, issued as 6 x 1 KB
+#define DN_PF_BUF ((10 * DN_PF_C * DN_PF_WIN + 1023) / 1024 * 1024)   // per wave per chunk (C = 1: 2720 B as 3 x 1 KB)
 __device__ __forceinline__ void dn_pf_issue(const DevArgs& A, const uint8_t* pl, const int* start_al, uint8_t* dst) {
   const int lane = threadIdx.x & 63, np = A.n_person;
 #pragma unroll
@@ -867,7 +869,8 @@ __device__ __forceinline__ void hoist_poly4_dn_pf(const DevArgs& A, const int* s
       __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the reads of the buffer about to be refilled are done
       __builtin_amdgcn_sched_barrier(0);
       dn_pf_issue(A, pl, start_al + c0 + C, wbuf + (((c0 / C) + 1) & 1) * DN_PF_BUF);
-      __builtin_amdgcn_s_waitcnt(0x0F76);   // vmcnt(6): this chunk's 6 DMA instructions have landed
+      static_assert(DN_PF_BUF / 1024 <= 15, "vmcnt field");
+      __builtin_amdgcn_s_waitcnt(0x0F70 | (DN_PF_BUF / 1024));   // vmcnt(#DMA of the next chunk): this chunk's have landed
     } else {
       __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
     }
