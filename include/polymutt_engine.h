@@ -98,6 +98,13 @@ typedef struct {
                                   no filters; res.varllk[0] = mono, varllk[1] = poly (no priors), af = minimiser */
 } pm_params;
 
+/* Diagnostic environment variables read by pm_engine_create / pm_engine_run (tests and tools only; results
+ * never depend on them beyond the documented bit-identical alternatives):
+ *   PM_NO_PREFETCH=1  the lean kernels hoist from direct HBM loads instead of LDS-staged PL bytes (tests
+ *                     compare the two paths bit for bit);
+ *   PM_BRENT_TS=T,S   force the Brent lane plan to T threads x S slots when it holds the pedigree
+ *                     (tools/brent_sweep.py geometry sweeps). */
+
 /* Objective-evaluation numerics.  All three compute CalcAllFamLogLikelihood; they differ in rounding only.
  *   PM_NUM_PRODUCT: each family's likelihood exactly as the reference forms it (same operations, same order),
  *                   families combined as a normalised product, one log10 per evaluation;
@@ -166,6 +173,10 @@ typedef struct pm_engine pm_engine;
  * with respect to each other).  max_batch bounds the sites per pm_engine_run call. */
 int pm_engine_create(const pm_pedigree *ped, const pm_params *par, int device, int max_batch, pm_engine **out);
 void pm_engine_destroy(pm_engine *eng);
+
+/* The lane plan pm_engine_create chose for the Brent kernel: threads per item (one wave = 64) and
+ * family slots per lane.  Diagnostics and tests only (no reference counterpart). */
+int pm_engine_plan(pm_engine *eng, int32_t *threads, int32_t *slots);
 
 /* Start a GLF section: sets the chromosome class, recomputes the polymorphism prior
  * (GetPolyPrior, NucFamGenotypeLikelihood.cpp:295-304) and zeroes the section counters. */

@@ -601,11 +601,6 @@ __device__ __forceinline__ void load_units(const int* su, int* uu) {
   }
 }
 
-#ifdef PM_EXP_LK_NOCONFLICT   // timing experiment: conflict-free table reads (wrong values)
-#define LKX(b) ((((b) & 1) | ((threadIdx.x & 63) << 1)) & 255)
-#else
-#define LKX(b) (b)
-#endif
 
 // One nuclear family's quartic coefficients from its PL bytes by[3q + {0,1,2}] = (g11, g12, g22) of person q
 // (father, mother, kids), nn persons (0 = empty slot -> the phantom family).  Branch-free: lanes whose
@@ -617,13 +612,13 @@ __device__ __forceinline__ void fam_poly4(const uint32_t* by, int nn, const doub
   for (int k = 0; k < 9; k++) kids[k] = 1.0;
 #pragma unroll
   for (int q = 2; q < 4; q++) {
-    const double l11 = lk[LKX(by[3 * q])], l12 = lk[LKX(by[3 * q + 1])], l22 = lk[LKX(by[3 * q + 2])];
+    const double l11 = lk[by[3 * q]], l12 = lk[by[3 * q + 1]], l22 = lk[by[3 * q + 2]];
     const bool kid = q < nn;
 #pragma unroll
     for (int k = 0; k < 9; k++) kids[k] *= kid ? d_one_kid(k, PM_CHR_AUTO, 0, l11, l12, l22) : 1.0;
   }
-  const double lF[3] = {lk[LKX(by[0])], lk[LKX(by[1])], lk[LKX(by[2])]};
-  const double lM[3] = {lk[LKX(by[3])], lk[LKX(by[4])], lk[LKX(by[5])]};
+  const double lF[3] = {lk[by[0]], lk[by[1]], lk[by[2]]};
+  const double lM[3] = {lk[by[3]], lk[by[4]], lk[by[5]]};
   const bool fam = nn >= 2;
   double c9[9];
 #pragma unroll
@@ -1111,15 +1106,8 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
   extern __shared__ uint8_t s_pf[];
   const bool pf = PFK && A.pf_npad > 0;
   if (pf) prefetch_planes(A, items, vb, nItems, s_pf);
-#ifdef PM_EXP_TIMING   // timing experiment: per-wave cycle split between hoisting, evaluations and the rest
-  long long tm_w = 0, tm_h = 0, tm_e = 0, tm_all = -(long long)wall_clock64(), tm_0 = 0, tm_1 = 0;
-  int tm_items = 0, tm_ev = 0;
-#endif
   unsigned long long ev_acc = 0;   // evaluation count of this block's items: one atomic per block, at exit
   for (int it = vb; it < nItems; it += gridDim.x) {
-#ifdef PM_EXP_TIMING
-    tm_0 = wall_clock64(); tm_items++;
-#endif
     const int item = items[it];
     const int site = item >> 3, cfg = item & 7;
     const int r = A.ref[site];
@@ -1148,9 +1136,6 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
       if constexpr (PFK) {
         if (pf) {
           __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this item's planes have landed in LDS
-#ifdef PM_EXP_TIMING
-          tm_w += wall_clock64() - tm_0;
-#endif
           hoist_poly4_lds<S, T>(A, s_u, s_pf, s_lk, cond, live);
           __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): every read of the buffer is done ...
           __builtin_amdgcn_sched_barrier(0);
@@ -1184,28 +1169,6 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
       else if (GEN && unit[s].x == U_FP) fl[s] = hoist_fp(A, I, pl, s_lk, unit[s].z, unit[s].w & 0xFF, cond[s]);
     }
     double* raw = A.raw + (size_t)site * 8;
-#ifdef PM_EXP_TIMING
-    tm_1 = wall_clock64(); tm_h += tm_1 - tm_0;
-#endif
-#ifdef PM_EXP_HOIST_ONLY   // timing experiment: hoisting alone (results are a checksum, not likelihoods)
-    if constexpr (POLY) {
-      double cs = 0.0;
-#pragma unroll
-      for (int s2 = 0; s2 < S; s2++) cs += cond[s2][0] + cond[s2][4];
-      if (cs == 12345.0) raw[cfg] = cs;
-      if (threadIdx.x == 0) { raw[cfg] = -1.0; A.minv[site * 8 + cfg] = 0.5; A.evals[site * 8 + cfg] = 1; }
-      continue;
-    }
-#endif
-#ifdef PM_EXP_EVAL_ONLY   // timing experiment: evaluations on fixed synthetic coefficients (no PL loads)
-    if constexpr (POLY) {
-#pragma unroll
-      for (int s2 = 0; s2 < S; s2++) {
-        const double q = 1e-3 * (1 + ((threadIdx.x + s2 + site) & 7));
-        cond[s2][0] = q; cond[s2][1] = 0.5 * q; cond[s2][2] = 0.25 * q; cond[s2][3] = 2 * q; cond[s2][4] = 0.9;
-      }
-    }
-#endif
     // ES workspace: lane-interleaved, in LDS when it fits the block's share (ws_lds), else in HBM (L2-resident)
     // (two pointers, so each inlined peel keeps a known address space: ds_* or global_* accesses, no flat)
     double* wsl = ES ? A.ws + (size_t)blockIdx.x * A.ws_per_lane * T + threadIdx.x : nullptr;
@@ -1314,16 +1277,8 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
       if (!single) ev_acc += nev;
       if (!ok) atomicExch(&A.counts[5], 1);
     }
-#ifdef PM_EXP_TIMING
-    tm_e += wall_clock64() - tm_1; tm_ev += nev;
-#endif
   }
   if (threadIdx.x == 0 && ev_acc) atomicAdd(A.eval_total, ev_acc);
-#ifdef PM_EXP_TIMING
-  tm_all += wall_clock64();
-  if (threadIdx.x == 0 && (blockIdx.x % 97) == 0 && list == 0)
-    printf("TIMING blk %d items %d evals %d hoist %lld eval %lld all %lld wait %lld (x10ns)\n", blockIdx.x, tm_items, tm_ev, tm_h, tm_e, tm_all, tm_w);
-#endif
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2571,6 +2526,13 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
   return PM_OK;
 }
 
+int pm_engine_plan(pm_engine* E, int32_t* threads, int32_t* slots) {
+  if (!E || !threads || !slots) { pm_set_last_error("pm_engine_plan: invalid arguments"); return PM_EINVAL; }
+  *threads = E->T;
+  *slots = E->S;
+  return PM_OK;
+}
+
 int pm_engine_begin_section(pm_engine* E, int32_t chrom) {
   if (!E || chrom < 0 || chrom > 3) { pm_set_last_error("pm_engine_begin_section: invalid arguments"); return PM_EINVAL; }
   E->chrom = chrom;
@@ -2710,10 +2672,20 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
   }
   BrentFn fn = brent_kernel(T, S, E->par.numerics, gen, !unrelated && n_ext > 0, A.denovo != 0, A.pf_npad > 0 || A.dn_pf);
   if (!fn) { pm_set_last_error("launch_brent: no kernel variant for the lane plan"); return PM_EINVAL; }
+  // multi-wave de novo plans (T = 512 / 1024: more than 1024 families) stage 2 buffers per wave: above the
+  // default 64 KB dynamic-LDS limit the kernel must opt in, and the block (plus its static LDS: lane plan,
+  // tables) must fit one CU's 160 KB; otherwise the same kernel hoists from direct loads
+  if (A.dn_pf && !(T == 64 && S == 16)) {
+    const size_t stat = (size_t)S * T * 4 + 256 * 8 + 100 * 8 + 96 * 8 + 32 * 4;
+    bool ok = shmem + stat <= 160 * 1024;
+    if (ok && shmem > 64 * 1024)
+      ok = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem) == hipSuccess;
+    if (!ok) { (void)hipGetLastError(); A.dn_pf = 0; shmem = 0; }
+  }
   // Elston-Stewart workspace in LDS: every partial / marriage-partial access of the peel becomes an LDS round
   // trip instead of an L2 one.  Blocks per CU follow from the LDS budget (160 KB per CU).
   A.ws_lds = 0;
-  if (!unrelated && n_ext > 0 && !E->par.denovo && !getenv("PM_ES_HBM")) {   // BA peels (the 10-state one is too big)
+  if (!unrelated && n_ext > 0 && !E->par.denovo) {   // BA peels (the 10-state one is too big)
     const size_t need = (size_t)E->ws_per_lane * T * sizeof(double);
     if (need > 0 && need <= 150 * 1024) {
       if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)need) == hipSuccess) {
@@ -2746,7 +2718,6 @@ static int run_pipeline(pm_engine* E, int n, const uint8_t* pl, const uint32_t* 
   {   // persons per lane of k_prep: vector loads when n_person allows; the reference's serial mono order in EXACT
     const int np = E->n_person;
     int vmax = 8;   // measured best on 1000 quads (16 and 4 within 1%)
-    if (const char* ev = getenv("PM_PREP_VEC")) vmax = atoi(ev);   // geometry experiments
     void (*prep)(DevArgs) = E->par.numerics == PM_NUM_EXACT ? k_prep<1, true>
                           : (np % 16 == 0 && vmax >= 16) ? k_prep<16, false> : (np % 8 == 0 && vmax >= 8) ? k_prep<8, false>
                           : (np % 4 == 0 && vmax >= 4) ? k_prep<4, false> : k_prep<1, false>;

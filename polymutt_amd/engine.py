@@ -94,6 +94,7 @@ EXPORTS = {
     # include/polymutt_engine.h
     "pm_engine_create": (i32, [P(PedigreeStruct), P(Params), i32, i32, P(C.c_void_p)]),
     "pm_engine_destroy": (None, [C.c_void_p]),
+    "pm_engine_plan": (i32, [C.c_void_p, P(i32), P(i32)]),
     "pm_engine_begin_section": (i32, [C.c_void_p, i32]),
     "pm_engine_run": (i32, [C.c_void_p, i32, C.c_void_p, C.c_void_p, C.c_void_p, i32, C.c_void_p, C.c_void_p, P(i32)]),
     "pm_engine_run_device": (i32, [C.c_void_p, i32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
@@ -283,6 +284,12 @@ class Engine:
 
     def synth(self, n, seed, site_offset, d_pl, d_dm, d_ref):
         self._check(self.lib.pm_engine_synth(self.h, n, seed, site_offset, d_pl, d_dm, d_ref))
+
+    def plan(self):
+        """(threads per Brent item, family slots per lane) of the engine's lane plan."""
+        t, s = i32(0), i32(0)
+        self._check(self.lib.pm_engine_plan(self.h, C.byref(t), C.byref(s)))
+        return t.value, s.value
 
     def kernel_stats(self, reset=False):
         s = KernelStats()

@@ -65,6 +65,9 @@ bool synth_shape(const std::string& shape, int fam, std::vector<SynthMember>& ou
     return true;
   }
   if (shape == "single") { add(-1, -1, 1 + fam % 2, 1); return true; }
+  // quads with an ext10 pedigree at families 256, 513, ...: a few extended families next to hundreds of
+  // nuclear ones (the lane plan must pair nuclear slots with per-lane extended lists)
+  if (shape == "quadext") return synth_shape(fam % 257 == 256 ? "ext10" : "quad", fam, out);
   return false;
 }
 

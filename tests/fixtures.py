@@ -34,8 +34,8 @@ def read_dataset(directory):
         rd = pm.GlfReader(ped, "test.gif")
         secs = []
         h = hashlib.sha256()
-        for label, _ in rd.sections():
-            pos, ref, pl, dm = rd.read(1 << 22)
+        for label, maxpos in rd.sections():   # synthetic sections: one record per position
+            pos, ref, pl, dm = rd.read(maxpos + 16)
             for a in (pos, ref, pl, dm):
                 h.update(np.ascontiguousarray(a).tobytes())
             secs.append((label, pos, ref, pl, dm))
@@ -122,12 +122,12 @@ def compare_to_dump(res, dump, label=""):
         if (rel > LLK_RTOL).any():
             i = int(np.argmax(rel))
             problems.append(f"{label}varllk[{k}] rel err {rel[i]:.3g} ({e[i]!r} vs reference {o[i]!r})")
-        if k > 0:   # see tests/parity.py: divergences on flat objectives are allowed, others bounded
+        if k > 0:   # see tests/parity.py: divergences on flat objectives are allowed, no others
             d = np.abs(res["varfreq"][m, k] - dump["varfreq"][m, k]) > FREQ_ATOL
             flat += int((d & (rel <= FLAT_RTOL)).sum())
             nonflat += int((d & (rel > FLAT_RTOL)).sum())
             runs += int(m.sum())
-    if nonflat > max(2, 1e-3 * runs):
+    if nonflat:
         problems.append(f"{label}{nonflat} minimiser divergences on non-flat objectives in {runs} Brent runs")
     d = np.abs(res["var_post_prob"][called] - dump["var_post_prob"][called])
     if d.size and d.max() > 1e-9:

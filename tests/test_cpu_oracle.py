@@ -162,3 +162,16 @@ def test_block_file_rejects_mismatched_or_truncated_input(cpu_driver, tmp_path):
     r = subprocess.run([cpu_driver, "-p", os.path.join(EXAMPLE, "test.ped"), "-d", os.path.join(EXAMPLE, "test.dat"),
                         "--in_blocks", pmb, "--out_vcf", str(tmp_path / "o2.vcf")], capture_output=True, text=True, timeout=300)
     assert r.returncode == 1 and "persons" in r.stdout
+
+
+def test_cpu_driver_vcf_input_record_kinds(cpu_driver, tmp_path):
+    """--in_vcf with multi-allelic, REF == ALT, indel and lower-case records (tests/vcf_edits.py) through the
+    product host driver on the CPU oracle: drop rules, indel alleles and QUAL pinned against the golden."""
+    from vcf_edits import check_edited_output, write_edited_vcf
+    src = str(tmp_path / "in.vcf")
+    write_edited_vcf(src)
+    out = tmp_path / "out.vcf"
+    r = subprocess.run([cpu_driver, "-p", "test.ped", "-d", "test.dat", "--in_vcf", src, "--out_vcf", str(out)],
+                       cwd=EXAMPLE, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    check_edited_output([l for l in out.read_text().splitlines() if not l.startswith("#")])

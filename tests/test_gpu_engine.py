@@ -123,13 +123,14 @@ def test_synthetic_device_generator_and_parity(built, shape, nfam, nsites, tmp_p
 
 
 @pytest.mark.parametrize("shape,nfam,denovo,nsites", [("quad", 64, 0, 500), ("quad+dn", 64, 1, 500), ("trio+dn", 64, 1, 500),
-                                                     ("quad+dn", 300, 1, 300), ("quad+dn", 600, 1, 150), ("trio+dn", 528, 1, 150)])
+                                                     ("quad+dn", 300, 1, 300), ("quad+dn", 600, 1, 150), ("trio+dn", 528, 1, 150),
+                                                     ("quad+dn", 1200, 1, 96), ("quad+dn", 2100, 1, 64)])
 def test_plane_prefetch_bit_identical(built, tmp_path, monkeypatch, shape, nfam, denovo, nsites):
     """The lean kernels' LDS staging of the PL bytes (plain: the item's 3 planes; --denovo: per-wave windows of
     all 10 planes, double-buffered by LDS-DMA), taken when n_person % 16 == 0, gives bit-identical results to
     the direct-load hoisting (PM_NO_PREFETCH=1) on the same lane plan, and both match the oracle."""
     d = str(tmp_path / "pf")
-    pm.synth_write_dataset(d, shape, nfam, nsites, 13)   # n_person % 16 == 0; > 512 families: the 2-wave (128 x 8) plan
+    pm.synth_write_dataset(d, shape, nfam, nsites, 13)   # n_person % 16 == 0
     ped = pm.Pedigree(os.path.join(d, "test.dat"), os.path.join(d, "test.ped"))
     label, pos, ref, pl, dm = _read_all(ped, d)[0]
     params = pm.Params.defaults(numerics=pm.NUM_POLY, denovo=denovo, denovo_mut_rate=1e-5 if denovo else 1.5e-8)
@@ -141,7 +142,9 @@ def test_plane_prefetch_bit_identical(built, tmp_path, monkeypatch, shape, nfam,
         outs.append(eng.run(pl, dm, ref))
         eng.close()
     (a, ac), (b, bc) = outs
-    if nfam <= 512:   # same lane plan both ways (above 512 --denovo families, staging selects the 64 x 16 plan)
+    # same lane plan both ways, except for 513-1024 --denovo families (staging selects the 64 x 16 plan there);
+    # above 1024 families both take the multi-wave plans (512 x 4, 1024 x 4: 48 / 96 KB of staging buffers)
+    if nfam <= 512 or nfam > 1024:
         assert a.tobytes() == b.tobytes() and ac.tobytes() == bc.tobytes()
     o, oc = Oracle(ped.view, params).run(pl, dm, ref)
     assert compare_results(a, o, ac, oc, label="prefetch ")["called"] > 0
@@ -203,8 +206,9 @@ def test_cli_block_input_reproduces_golden(built, tmp_path):
 @pytest.mark.parametrize("denovo", [0, 1])
 def test_headline_config_parity(built, denovo):
     """The bench's own workload (BASELINE config 3: 1000 nuclear quads, the bench pedigree and site generator,
-    the geometry and kernels the bench runs -- 2-wave de novo plan with LDS-staged PL windows, or the 1-wave
-    plain plan with plane prefetch) against the CPU oracle on the first 1024 sites."""
+    the geometry and kernels the bench runs -- one wave per item with 16 family slots per lane: the de novo
+    kernel that compiles only the LDS-staged hoisting, or the plain kernel with plane prefetch) against the
+    CPU oracle on the first 1024 sites.  The plan is asserted so a geometry change fails loudly here."""
     import sys
     sys.path.insert(0, ROOT)
     import bench
@@ -212,6 +216,7 @@ def test_headline_config_parity(built, denovo):
     pl, dm, ref = pm.synth_block_host(ped, 1024, 7)
     params = pm.Params.defaults(denovo=denovo)
     eng = pm.Engine(ped, params, max_batch=1024)
+    assert eng.plan() == (64, 16)
     e, ec = eng.run(pl, dm, ref)
     eng.close()
     o, oc = Oracle(ped, params).run(pl, dm, ref)

@@ -39,6 +39,45 @@ def test_cli_reproduces_vcf_input_golden(built, tmp_path, numerics):
     assert not diff, f"{len(diff)} lines differ; first:\n{got[diff[0]][:300]}\n{exp[diff[0]][:300]}"
 
 
+@pytest.mark.parametrize("numerics", ["product", "poly"])
+def test_cli_vcf_input_record_kinds(built, cpu_driver, tmp_path, numerics):
+    """--in_vcf with multi-allelic, REF == ALT, indel and lower-case records (tests/vcf_edits.py): the GPU CLI
+    obeys the reference's drop rules and indel alleles (checked against the golden) and writes the same
+    bytes as the product host driver on the CPU oracle."""
+    from vcf_edits import check_edited_output, write_edited_vcf
+    src = str(tmp_path / "in.vcf")
+    write_edited_vcf(src)
+    outs = []
+    for exe, extra in ((pm.BIN_PATH, ["--numerics", numerics]), (cpu_driver, [])):
+        out = tmp_path / f"out{len(outs)}.vcf"
+        r = subprocess.run([exe, "-p", "test.ped", "-d", "test.dat", "--in_vcf", src, "--out_vcf", str(out)] + extra,
+                           cwd=EXAMPLE, capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        outs.append([l for l in out.read_text().splitlines() if not l.startswith("##")])
+    check_edited_output(outs[0][1:])
+    assert outs[0] == outs[1]
+
+
+@pytest.mark.parametrize("numerics", [pm.NUM_POLY, pm.NUM_EXACT])
+def test_engine_vcf_mode_config5_geometry(built, tmp_path, numerics):
+    """BASELINE config 5's shape: 2000 mixed trio/quad families in vcf_mode (one (ref, alt) Brent per site,
+    every site emitted), 512 sites in 2 batches, against the oracle's VCF restatement."""
+    pm.synth_write_dataset(str(tmp_path), "mixed", 2000, 512, 37)
+    ped, secs, _ = read_dataset(str(tmp_path))
+    (label, pos, ref, pl, dm), = secs
+    refalt = _vcf_block(pl, ref, 9)
+    par = pm.Params.defaults(vcf_mode=1, numerics=numerics)
+    eng = pm.Engine(ped.view, par, max_batch=256)
+    ora = Oracle(ped.view, par)
+    zeros = np.zeros_like(dm)
+    for s in range(0, len(ref), 256):
+        e, ec = eng.run(pl[s:s + 256], zeros[s:s + 256], refalt[s:s + 256])
+        o, oc = ora.run(pl[s:s + 256], zeros[s:s + 256], refalt[s:s + 256])
+        st = compare_results(e, o, ec, oc, label=f"cfg5[{s}] ")
+        assert st["emitted"] == st["called"] == len(e)
+    eng.close()
+
+
 def _vcf_block(pl, ref, seed):
     """Biallelic (ref, alt) per site: alt = transition, or a transversion on a third of the sites."""
     rng = np.random.default_rng(seed)

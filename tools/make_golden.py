@@ -54,6 +54,17 @@ CASES = {
                                            "--minPercSampleWithData", "99.5"]),
     "quad_allsites": ("quad", 10, 300, 61, ["--all_sites"]),
     "quad_prec": ("quad", 30, 400, 67, ["--prec", "1e-6", "--theta", "0.01", "--poly_tstv", "1.5"]),
+    # ES type-3 peels (parents -> only child) under the 10-state de novo model and on chrX
+    "roof_denovo": ("roof+dn", 12, 300, 83, ["--denovo", "--rate_denovo", "1e-6"]),
+    "roof_chrX": ("roof", 12, 300, 89, ["--chrX", "1"]),
+    # BASELINE.json config geometries (the lane plans and kernels the bench selects for them)
+    "big_trio_1000": ("trio", 1000, 256, 11, []),
+    "big_quad_1000_denovo": ("quad", 1000, 256, 7, ["--denovo"]),
+    "big_ext10_200": ("ext10", 200, 256, 17, []),
+    "big_ext10_200_denovo": ("ext10+dn", 200, 256, 29, ["--denovo", "--rate_denovo", "1e-6"]),
+    # a few extended pedigrees next to > 512 nuclear families
+    "big_quadext_600": ("quadext", 600, 256, 97, []),
+    "big_quadext_600_denovo": ("quadext", 600, 200, 101, ["--denovo", "--rate_denovo", "1e-6"]),
 }
 
 SITE_DUMP = np.dtype([("pos", "<i4"), ("ref", "<i4"), ("status", "<i4"), ("total_depth", "<i4"),
@@ -73,8 +84,8 @@ def block_sha256(directory):
     try:
         rd = pm.GlfReader(ped, "test.gif")
         h = hashlib.sha256()
-        for label, _ in rd.sections():
-            pos, ref, pl, dm = rd.read(1 << 22)
+        for label, maxpos in rd.sections():   # synthetic sections: one record per position
+            pos, ref, pl, dm = rd.read(maxpos + 16)
             for a in (pos, ref, pl, dm):
                 h.update(np.ascontiguousarray(a).tobytes())
         return h.hexdigest()
@@ -119,8 +130,8 @@ def main():
     for n in names:
         meta[n] = make_case(n)
         print(n, meta[n]["dumped_sites"], "sites,", meta[n]["records"], "records", flush=True)
-    with open(meta_path, "w") as fh:
-        json.dump(meta, fh, indent=1, sort_keys=True)
+        with open(meta_path, "w") as fh:
+            json.dump(meta, fh, indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":
