@@ -178,6 +178,14 @@ void pm_engine_destroy(pm_engine *eng);
  * family slots per lane.  Diagnostics and tests only (no reference counterpart). */
 int pm_engine_plan(pm_engine *eng, int32_t *threads, int32_t *slots);
 
+/* famlk[0]'s stale state across sites: whether CalcPostProb has already run earlier in the run (any
+ * earlier site reached OutputVCF).  The reference's likelihoodONEKid reads the object's member `sex`
+ * (NucFamGenotypeLikelihood.cpp:1193, 1202-1264), which CalcPostProb leaves at the last person's sex; it
+ * changes the first family's chrX/Y genotype posteriors.  The engine tracks it itself across
+ * pm_engine_run calls; a driver that splits a run over several engines (site shards) sets it at each
+ * shard's start.  0 at creation. */
+int pm_engine_set_posterior_carry(pm_engine *eng, int32_t seen);
+
 /* Start a GLF section: sets the chromosome class, recomputes the polymorphism prior
  * (GetPolyPrior, NucFamGenotypeLikelihood.cpp:295-304) and zeroes the section counters. */
 int pm_engine_begin_section(pm_engine *eng, int32_t chrom);

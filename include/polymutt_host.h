@@ -33,8 +33,20 @@ int pmh_glf_next_section(pmh_glf_reader *r, char *label, int32_t label_cap, int3
 int pmh_glf_read_sites(pmh_glf_reader *r, int32_t max_sites, int32_t *pos, uint8_t *ref, uint8_t *pl, uint32_t *dm);
 void pmh_glf_close(pmh_glf_reader *r);
 
+/* The polymutt command line (src/main.cpp:57-627) on the HIP engine; returns the exit code.
+ * world > 1: this process is shard `rank` of a multi-GPU run (one process per GPU, launched by
+ * polymutt_amd/launch.py): it analyses a contiguous position range of every section and calls
+ * allgather(ctx, send, n, recv) -- recv receives world x n int64, rank-major -- once per section and
+ * once at the end; rank 0 prints the summed summaries and writes the merged VCF.  device >= 0 overrides
+ * --gpu.  allgather returns 0 on success. */
+typedef int (*pmh_allgather_fn)(void *ctx, const int64_t *send, int32_t n, int64_t *recv);
+int pmh_run_polymutt(int argc, char **argv, int32_t rank, int32_t world, int32_t device, pmh_allgather_fn allgather,
+                     void *ctx);
+
 /* Synthetic workload.  shape: "quad", "trio", "ext10" (3-generation, 10 members),
- * "roof" (double-roof 8 members), "mixed" (alternating trio/quad), "single" (unrelated singletons). */
+ * "roof" (double-roof 8 members), "roof2" (12 members: a type-3 peel with a marriage partial), "mixed"
+ * (alternating trio/quad), "single" (unrelated singletons), "quadext" (quads with an ext10 at families
+ * 256, 513, ...); "<shape>+dn" plants de novo calls. */
 int pmh_synth_write_dataset(const char *dir, const char *shape, int32_t n_fam, int32_t n_sites, uint64_t seed);
 /* Host generation of the same dense block pm_engine_synth produces on the device. */
 int pmh_synth_block(const pm_pedigree *ped, int32_t n, uint64_t seed, uint64_t site_offset, uint8_t *pl, uint32_t *dm, uint8_t *ref);

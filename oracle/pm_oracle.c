@@ -893,6 +893,12 @@ void pmo_destroy(pmo_ctx *c) {
   free(c);
 }
 
+/* famlk[0] after CalcPostProb holds the last person's sex (calc_post_prob visits every person in order) */
+void pmo_set_posterior_carry(pmo_ctx *c, int32_t seen) {
+  c->any_postprob = seen != 0;
+  c->lk[0].sex = seen ? c->sex[c->ped.n_person - 1] : 0;
+}
+
 void pmo_begin_section(pmo_ctx *c, int32_t chrom) {
   c->chrom = chrom; c->isX = chrom == PM_CHR_X; c->isY = chrom == PM_CHR_Y; c->isMT = chrom == PM_CHR_MT;
   c->prior = poly_prior(c);

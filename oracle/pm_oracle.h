@@ -24,6 +24,8 @@ typedef struct pmo_ctx pmo_ctx;
 pmo_ctx *pmo_create(const pm_pedigree *ped, const pm_params *par);
 void pmo_destroy(pmo_ctx *c);
 void pmo_begin_section(pmo_ctx *c, int32_t chrom);
+/* famlk[0]'s stale posterior state (see pm_engine_set_posterior_carry). */
+void pmo_set_posterior_carry(pmo_ctx *c, int32_t seen);
 double pmo_poly_prior(const pmo_ctx *c);
 
 /* One site of main.cpp:327-594.  calls[n_person] is written when res->emit != 0.

@@ -122,7 +122,6 @@ struct DevArgs {
   double* minv;            // [n][8] Brent minimiser
   int* evals;              // [n][8]
   double* mono_plain;      // [n] MonomorphismLogLikelihood
-  int8_t* item_sex;        // [n] member `sex` of famlk[0] for the cfg-7 item
   int* items[N_LISTS];
   int* counts;             // [0..2] list sizes, [3] rows, [4] first emitted site, [5] Brent stuck, [8]/[9] quick items/site visits
   unsigned long long* eval_total;
@@ -1116,7 +1115,7 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
     I.g11 = d_gi(I.a1, I.a1); I.g12 = d_gi(I.a1, I.a2); I.g22 = d_gi(I.a2, I.a2);
     // the lean polynomial kernel also runs autosomal --denovo items (its hoisting has the de novo kid terms)
     I.denovo = (GEN || (POLYK && DN)) ? (A.denovo && cfg != 7) : 0;
-    I.sex = (GEN && cfg == 7) ? A.item_sex[site] : 0;
+    I.sex = 0;   // famlk[1..6]'s member sex stays 0; famlk[0]'s stale one only reaches the posteriors (de novo cfg-7 items: 0)
     I.chrom = GEN ? A.chrom : PM_CHR_AUTO;
     int pmode;
     if (I.denovo) pmode = A.n_fam_gt1 ? PR_AUTO : PR_DN_SINGLE;
@@ -1619,12 +1618,6 @@ __device__ __forceinline__ int d_member_sex_before(const DevArgs& A, int site) {
   return seen ? A.sex[A.n_person - 1] : 0;
 }
 
-__global__ void k_prepare_items7(DevArgs A) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= A.counts[2]) return;
-  const int site = A.items[2][i] >> 3;
-  A.item_sex[site] = (int8_t)d_member_sex_before(A, site);
-}
 
 // --denovo: denovoLR = varllk_noprior[maxidx] - lk_poly (main.cpp:567-573); famlk[0].min is overwritten
 // by that re-optimisation (the printed AF) whenever a Brent ran.
@@ -2096,7 +2089,6 @@ struct pm_engine {
   pm_geno_call* d_calls = nullptr;
   double *d_raw = nullptr, *d_minv = nullptr, *d_mono = nullptr;
   int* d_evals = nullptr;
-  int8_t* d_item_sex = nullptr;
   // extended families (Elston-Stewart)
   int n_ext = 0, max_ext = 0, ws_per_lane = 0, grid_post = 0;
   int *d_fam_founders = nullptr, *d_peel_start = nullptr, *d_ext_count = nullptr, *d_ext_fam = nullptr;
@@ -2270,7 +2262,7 @@ void pm_engine_destroy(pm_engine* E) {
                   E->d_T10dn, E->d_ws, E->d_units_q,
                   E->d_fam_start, E->d_fam_kind, E->d_fa, E->d_mo, E->d_sex, E->d_units, E->d_lktab, E->d_M, E->d_syn,
                   E->d_pl, E->d_stage, E->d_ref, E->d_dm, E->d_res, E->d_calls, E->d_raw, E->d_minv, E->d_mono, E->d_evals,
-                  E->d_item_sex, E->d_items[0], E->d_items[1], E->d_items[2], E->d_counts, E->d_eval_total, E->d_row_site,
+                  E->d_items[0], E->d_items[1], E->d_items[2], E->d_counts, E->d_eval_total, E->d_row_site,
                   E->d_counters, E->d_row_blk};
   for (void* b : bufs) if (b) hipFree(b);
   for (auto& pr : E->brent_events) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
@@ -2511,7 +2503,6 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
   DALLOC(E->d_minv, nb * 8);
   DALLOC(E->d_evals, nb * 8);
   DALLOC(E->d_mono, nb);
-  DALLOC(E->d_item_sex, nb);
   for (int l = 0; l < N_LISTS; l++) DALLOC(E->d_items[l], nb * 4);
   DALLOC(E->d_counts, 16);
   DALLOC(E->d_eval_total, 1);
@@ -2530,6 +2521,12 @@ int pm_engine_plan(pm_engine* E, int32_t* threads, int32_t* slots) {
   if (!E || !threads || !slots) { pm_set_last_error("pm_engine_plan: invalid arguments"); return PM_EINVAL; }
   *threads = E->T;
   *slots = E->S;
+  return PM_OK;
+}
+
+int pm_engine_set_posterior_carry(pm_engine* E, int32_t seen) {
+  if (!E) { pm_set_last_error("pm_engine_set_posterior_carry: invalid arguments"); return PM_EINVAL; }
+  E->carry_postprob = seen != 0;
   return PM_OK;
 }
 
@@ -2596,7 +2593,7 @@ static DevArgs make_args(pm_engine* E, int n, const uint8_t* pl, const uint32_t*
   A.np_ts = log10(prior * 2. / 3.);              // :472
   A.np_tv = log10(prior * 1. / 6.);              // :482, :492
   A.n = n; A.pl = pl; A.dm = dm; A.ref = ref; A.res = res; A.calls = calls;
-  A.raw = E->d_raw; A.minv = E->d_minv; A.evals = E->d_evals; A.mono_plain = E->d_mono; A.item_sex = E->d_item_sex;
+  A.raw = E->d_raw; A.minv = E->d_minv; A.evals = E->d_evals; A.mono_plain = E->d_mono;
   for (int l = 0; l < N_LISTS; l++) A.items[l] = E->d_items[l];
   A.counts = E->d_counts; A.eval_total = E->d_eval_total; A.row_site = E->d_row_site; A.row_blk = E->d_row_blk; A.counters = E->d_counters;
   A.carry_postprob = E->carry_postprob ? 1 : 0;
@@ -2748,7 +2745,6 @@ static int run_pipeline(pm_engine* E, int n, const uint8_t* pl, const uint32_t* 
     HIP_TRY(hipGetLastError());
   }
   if (E->par.denovo) {
-    hipLaunchKernelGGL(k_prepare_items7, dim3(gb), dim3(tb), 0, E->stream, A);
     if ((rc = launch_brent(E, A, 2))) return rc;
     hipLaunchKernelGGL(k_final_dn, dim3(gb), dim3(tb), 0, E->stream, A);
     HIP_TRY(hipGetLastError());

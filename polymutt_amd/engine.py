@@ -95,6 +95,7 @@ EXPORTS = {
     "pm_engine_create": (i32, [P(PedigreeStruct), P(Params), i32, i32, P(C.c_void_p)]),
     "pm_engine_destroy": (None, [C.c_void_p]),
     "pm_engine_plan": (i32, [C.c_void_p, P(i32), P(i32)]),
+    "pm_engine_set_posterior_carry": (i32, [C.c_void_p, i32]),
     "pm_engine_begin_section": (i32, [C.c_void_p, i32]),
     "pm_engine_run": (i32, [C.c_void_p, i32, C.c_void_p, C.c_void_p, C.c_void_p, i32, C.c_void_p, C.c_void_p, P(i32)]),
     "pm_engine_run_device": (i32, [C.c_void_p, i32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
@@ -121,6 +122,7 @@ EXPORTS = {
     "pmh_glf_read_sites": (i32, [C.c_void_p, i32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "pmh_glf_close": (None, [C.c_void_p]),
     "pmh_synth_write_dataset": (i32, [C.c_char_p, C.c_char_p, i32, i32, u64]),
+    "pmh_run_polymutt": (i32, [i32, P(C.c_char_p), i32, i32, i32, C.c_void_p, C.c_void_p]),   # see launch.py
     "pmh_synth_block": (i32, [P(PedigreeStruct), i32, u64, u64, C.c_void_p, C.c_void_p, C.c_void_p]),
 }
 
@@ -284,6 +286,9 @@ class Engine:
 
     def synth(self, n, seed, site_offset, d_pl, d_dm, d_ref):
         self._check(self.lib.pm_engine_synth(self.h, n, seed, site_offset, d_pl, d_dm, d_ref))
+
+    def set_posterior_carry(self, seen):
+        self._check(self.lib.pm_engine_set_posterior_carry(self.h, 1 if seen else 0))
 
     def plan(self):
         """(threads per Brent item, family slots per lane) of the engine's lane plan."""

@@ -1,9 +1,13 @@
 // capi.cpp -- C ABI of the host helpers (include/polymutt_host.h).
+#include <cstdio>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 #include "../../include/polymutt_host.h"
 #include "../csrc/synth_core.h"
+#include "driver.h"
+#include "engine_eval.h"
 #include "glf.h"
 #include "pedigree.h"
 #include "synth.h"
@@ -89,6 +93,21 @@ int pmh_glf_read_sites(pmh_glf_reader* r, int32_t max_sites, int32_t* pos, uint8
 }
 
 void pmh_glf_close(pmh_glf_reader* r) { delete r; }
+
+int pmh_run_polymutt(int argc, char** argv, int32_t rank, int32_t world, int32_t device, pmh_allgather_fn allgather, void* ctx) {
+  pmhost::ShardComm comm;
+  comm.rank = rank;
+  comm.world = world;
+  if (world > 1) {
+    if (!allgather || rank < 0 || rank >= world) { fprintf(stderr, "pmh_run_polymutt: invalid shard arguments\n"); return 1; }
+    comm.allgather = [=](const int64_t* send, int n, int64_t* recv) {
+      if (allgather(ctx, send, n, recv) != 0) throw pmhost::FatalError("shard exchange (allgather) failed\n");
+    };
+  }
+  return pmhost::polymutt_main(argc, argv, &comm, [&](const pm_pedigree& v, const pm_params& par, const pmhost::Options& opt) {
+    return std::unique_ptr<pmhost::SiteEvaluator>(new pmhost::EngineEvaluator(v, par, device >= 0 ? device : opt.device, opt.batch));
+  });
+}
 
 int pmh_synth_write_dataset(const char* dir, const char* shape, int32_t nfam, int32_t nsites, uint64_t seed) {
   std::string err;

@@ -1,5 +1,6 @@
 // driver.cpp -- see driver.h.
 #include "driver.h"
+#include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -188,16 +189,234 @@ struct Batch {
   }
 };
 
+std::map<std::string, int> parse_chr_selection(const std::string& s) {   // --chr2process (main.cpp:286-308)
+  std::map<std::string, int> chrSel;
+  size_t i = 0;
+  while (i < s.size()) {
+    size_t j = s.find(',', i);
+    if (j == std::string::npos) j = s.size();
+    if (j > i) chrSel[s.substr(i, j - i)]++;
+    i = j + 1;
+  }
+  return chrSel;
+}
+
+void copy_range(FILE* in, int64_t b, int64_t e, FILE* out) {
+  std::vector<char> buf(1 << 20);
+  if (fseek(in, (long)b, SEEK_SET) != 0) throw FatalError("VCF shard merge: seek failed\n");
+  while (b < e) {
+    const size_t want = (size_t)std::min<int64_t>(e - b, (int64_t)buf.size());
+    const size_t got = fread(buf.data(), 1, want, in);
+    if (got != want) throw FatalError("VCF shard merge: short read\n");
+    fwrite(buf.data(), 1, got, out);
+    b += (int64_t)got;
+  }
+}
+
 }  // namespace
 
-int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval) {
-  print_status(opt);
+// One shard of a multi-process run: rank R of N analyses the sites of every section whose
+// 0-based position lies in [maxPosition * R / N, maxPosition * (R + 1) / N) (the last rank: to the end),
+// writes their records to <out_vcf>.part<R>, and at each section end exchanges one small vector per rank
+// (the section counters of main.cpp:264-282, the entry count, how many sites reached OutputVCF, the byte
+// range of its records).  Rank 0 prints the summed section summary (main.cpp:596-619) and finally
+// concatenates the parts in (section, rank) order behind the header, which the reference writes lazily on
+// the first OutputVCF call.
+//
+// Cross-shard state: famlk[0]'s stale member sex (pm_engine_set_posterior_carry) depends on whether any
+// earlier site in run order reached CalcPostProb.  Earlier sections are known to every rank; for its own
+// section range rank R > 0 assumes an earlier shard emitted something, and after the exchange, when that
+// guess was wrong and the shard has a record, re-runs the shard's first recorded site with the true state
+// and writes that record to <out_vcf>.part<R>.fix<section>, which the merge puts in place of the first one.
+int run_polymutt_sharded(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, const ShardComm& comm, SiteStream& src) {
+  const int R = comm.rank, N = comm.world;
+  const bool lead = R == 0;
+  if (!opt.positionFile.empty()) throw FatalError("--pos runs cannot be sharded over several processes\n");
+  const std::string part = opt.vcfOutFile + ".part" + std::to_string(R);
+  FILE* fh = fopen(part.c_str(), "w+b");
+  if (!fh) throw FatalError("vcfOutFile can not be opened for output!\n");
+  VcfWriter W;
+  W.fh = fh; W.ped = &ped; W.cmd = opt.cmd; W.minMapQuality = opt.minMapQuality; W.minTotalDepth = opt.minTotalDepth;
+  W.maxTotalDepth = opt.maxTotalDepth; W.posterior = opt.posterior; W.gl_off = opt.gl_off; W.force_call = opt.force_call;
+  W.denovo = opt.denovo;
+  W.header_written = true;   // parts hold records only
+  std::map<std::string, int> chrSel = parse_chr_selection(opt.chrs2process);
+  const size_t chrSelCount = chrSel.size();
+  time_t t0; time(&t0);
+  if (lead) printf("Analysis started on %s\n", ctime(&t0));
+  const int np = (int)ped.column_pid.size();
+  Batch B;
+  B.init(opt.batch > 0 ? opt.batch : 4096, np);
+  enum { K_ENTRIES = 16, K_OUT, K_REC, K_START, K_END, K_FIRST_END, K };
+  bool earlier = false;        // a site of an earlier section (any shard) reached CalcPostProb
+  int64_t outputs = 0;         // OutputVCF calls over all shards: the header exists iff > 0
+  std::vector<std::vector<int64_t>> secs;   // lead: every section's exchange (N x K)
+  std::vector<std::vector<char>> fixes;     // lead: per section and rank, a .fix record replaces the first one
+  size_t chrDone = 0;
+  std::vector<int> wpos(src.window()), rowOf(src.window());
+  std::vector<uint8_t> wref(src.window());
+  while (src.nextSection()) {
+    if (!chrSel.empty() && chrDone >= chrSelCount) break;
+    const std::string label = src.label();
+    if (!chrSel.empty() && chrSel[label] < 1) continue;
+    const int chrom = label == opt.chrX ? PM_CHR_X : label == opt.chrY ? PM_CHR_Y : label == opt.MT ? PM_CHR_MT : PM_CHR_AUTO;
+    chrDone++;
+    eval.begin_section(chrom);
+    W.chrom = chrom;
+    const int64_t mp = src.maxPosition();
+    const int64_t lo = mp * R / N, hi = (R == N - 1) ? INT64_MAX : mp * (R + 1) / N;
+    const bool guess = earlier || R > 0;
+    eval.set_posterior_carry(guess);
+    int64_t entries = 0, n_out = 0, n_rec = 0, first_end = -1;
+    const int64_t start = ftell(fh);
+    std::vector<uint8_t> fpl((size_t)np * 10);
+    std::vector<uint32_t> fdm(np);
+    uint8_t fref = 0;
+    int fpos = 0;
+    bool past = false;
+    auto flush = [&]() {
+      if (B.n == 0) return;
+      int rows = 0;
+      eval.run(B.n, B.pl.data(), B.dm.data(), B.ref.data(), B.res.data(), B.calls.data(), &rows);
+      for (int i = 0; i < B.n; i++) {
+        const pm_site_result& r = B.res[i];
+        if (!r.emit) continue;
+        n_out++;
+        const uint8_t* pl = B.pl.data() + (size_t)i * np * 10;
+        const uint32_t* dm = B.dm.data() + (size_t)i * np;
+        W.output(label, B.pos[i], B.ref[i], r, r.call_row >= 0 ? B.calls.data() + (size_t)r.call_row * np : nullptr, pl, dm);
+        if (r.emit != 1) continue;
+        if (n_rec++ == 0) {   // the shard's first record: keep its site for a possible re-run
+          first_end = ftell(fh);
+          memcpy(fpl.data(), pl, fpl.size());
+          memcpy(fdm.data(), dm, fdm.size() * sizeof(uint32_t));
+          fref = B.ref[i];
+          fpos = B.pos[i];
+        }
+      }
+      B.n = 0;
+    };
+    for (;;) {
+      const int got = src.nextSites(std::min(src.window(), B.cap - B.n), wpos.data(), wref.data());
+      if (got > 0) entries = mp;
+      for (int k = 0; k < got; k++) {
+        rowOf[k] = -1;
+        if (wpos[k] < lo) continue;
+        if (wpos[k] >= hi) { past = true; continue; }
+        const int i = B.n++;
+        B.pos[i] = wpos[k] + 1;
+        B.ref[i] = wref[k];
+        rowOf[k] = i;
+      }
+      src.fill(rowOf.data(), B.pl.data(), B.dm.data());
+      if (B.n == B.cap) flush();
+      if (past || src.ended()) break;
+    }
+    flush();
+    pm_counters C;
+    eval.counters(&C);
+    static_assert(sizeof(pm_counters) == 16 * sizeof(int64_t), "counter layout");
+    std::vector<int64_t> send(K), recv((size_t)N * K);
+    memcpy(send.data(), &C, sizeof(C));
+    send[K_ENTRIES] = entries; send[K_OUT] = n_out; send[K_REC] = n_rec;
+    send[K_START] = start; send[K_END] = ftell(fh); send[K_FIRST_END] = first_end;
+    comm.allgather(send.data(), K, recv.data());
+    auto needs_fix = [&](int q) {   // shard q's first record was formatted with the wrong famlk[0] state
+      bool truth = earlier;
+      for (int p = 0; p < q; p++) truth = truth || recv[(size_t)p * K + K_OUT] > 0;
+      return recv[(size_t)q * K + K_REC] > 0 && truth != (earlier || q > 0);
+    };
+    if (needs_fix(R)) {
+      fprintf(stderr, "shard %d: section %s: first record re-run with famlk[0] posterior state %s\n", R, label.c_str(),
+              (earlier || R > 0) ? "unset" : "set");
+      eval.set_posterior_carry(!(earlier || R > 0));
+      pm_site_result r1;
+      std::vector<pm_geno_call> c1(np);
+      int rows = 0;
+      eval.run(1, fpl.data(), fdm.data(), &fref, &r1, c1.data(), &rows);
+      char* buf = nullptr;
+      size_t len = 0;
+      FILE* ms = open_memstream(&buf, &len);
+      VcfWriter W1 = W;
+      W1.fh = ms;
+      W1.output(label, fpos, fref, r1, r1.call_row >= 0 ? c1.data() : nullptr, fpl.data(), fdm.data());
+      fclose(ms);
+      FILE* fx = fopen((part + ".fix" + std::to_string(secs.size())).c_str(), "wb");
+      if (!fx) { free(buf); throw FatalError("vcfOutFile can not be opened for output!\n"); }
+      fwrite(buf, 1, len, fx);
+      fclose(fx);
+      free(buf);
+    }
+    if (lead) {
+      pm_counters S;
+      memset(&S, 0, sizeof(S));
+      int64_t* s = (int64_t*)&S;
+      int64_t ent = 0;
+      std::vector<char> fx(N);
+      for (int q = 0; q < N; q++) {
+        for (int k = 0; k < 16; k++) s[k] += recv[(size_t)q * K + k];
+        ent = std::max(ent, recv[(size_t)q * K + K_ENTRIES]);
+        fx[q] = needs_fix(q);
+      }
+      print_summary(label, (int)ent, S, t0);
+      secs.push_back(recv);
+      fixes.push_back(fx);
+    } else secs.emplace_back();   // keeps the section numbering of the .fix files
+    for (int q = 0; q < N; q++) {
+      outputs += recv[(size_t)q * K + K_OUT];
+      earlier = earlier || recv[(size_t)q * K + K_OUT] > 0;
+    }
+  }
+  fflush(fh);
+  fclose(fh);
+  {   // every shard's part and fixes are complete before the lead concatenates them
+    int64_t one = 1;
+    std::vector<int64_t> all(N);
+    comm.allgather(&one, 1, all.data());
+  }
+  if (!lead) return 0;
+  FILE* out = fopen(opt.vcfOutFile.c_str(), "w");
+  if (!out) throw FatalError("vcfOutFile can not be opened for output!\n");
+  if (outputs > 0) { W.fh = out; W.header_written = false; W.header(); }
+  std::vector<FILE*> parts(N);
+  for (int q = 0; q < N; q++) {
+    parts[q] = fopen((opt.vcfOutFile + ".part" + std::to_string(q)).c_str(), "rb");
+    if (!parts[q]) throw FatalError("VCF shard merge: a shard's part file is missing\n");
+  }
+  for (size_t s = 0; s < secs.size(); s++)
+    for (int q = 0; q < N; q++) {
+      const int64_t* v = secs[s].data() + (size_t)q * K;
+      if (fixes[s][q]) {
+        const std::string fxp = opt.vcfOutFile + ".part" + std::to_string(q) + ".fix" + std::to_string(s);
+        FILE* fx = fopen(fxp.c_str(), "rb");
+        if (!fx) throw FatalError("VCF shard merge: a shard's fix record is missing\n");
+        fseek(fx, 0, SEEK_END);
+        copy_range(fx, 0, ftell(fx), out);
+        fclose(fx);
+        remove(fxp.c_str());
+        copy_range(parts[q], v[K_FIRST_END], v[K_END], out);
+      } else copy_range(parts[q], v[K_START], v[K_END], out);
+    }
+  for (int q = 0; q < N; q++) {
+    fclose(parts[q]);
+    remove((opt.vcfOutFile + ".part" + std::to_string(q)).c_str());
+  }
+  fclose(out);
+  return 0;
+}
+
+int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, const ShardComm* comm) {
+  const bool sharded = comm && comm->world > 1;
+  if (!sharded || comm->rank == 0) print_status(opt);
   if (opt.vcfInFile == opt.vcfOutFile) throw FatalError("Input and output VCF files are the same!\n");
   if (opt.pedFile.empty()) throw FatalError("pedFile not provided for input!\n");
   if (opt.glfListFile.empty() && opt.vcfInFile.empty() && opt.blocksIn.empty())
     throw FatalError("glfListFile or input VCF file not provided for input!\n");
   if (opt.vcfOutFile.empty()) throw FatalError("vcfOutFile not provided for output!\n");
-  if (!opt.vcfInFile.empty()) return run_polymutt_vcf(opt, ped, eval);   // main.cpp:238-246
+  if (!opt.vcfInFile.empty()) {   // main.cpp:238-246
+    if (sharded) throw FatalError("--in_vcf runs cannot be sharded over several processes\n");
+    return run_polymutt_vcf(opt, ped, eval);
+  }
   if (opt.denovo && opt.denovo_llr < 0) throw FatalError("denovo_min_LLR can only be greater than 0 !\n");
 
   std::map<std::string, int> positionMap;
@@ -216,6 +435,7 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval) {
   }
   SiteStream& src = *srcp;
   if (getenv("PM_TIMING")) fprintf(stderr, "PM_TIMING open inputs %.3f s\n", now_s() - t_open0);
+  if (sharded) return run_polymutt_sharded(opt, ped, eval, *comm, src);
   FILE* vcf = fopen(opt.vcfOutFile.c_str(), "w");
   if (!vcf) throw FatalError("vcfOutFile can not be opened for output!\n");
 
@@ -224,17 +444,7 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval) {
   W.maxTotalDepth = opt.maxTotalDepth; W.posterior = opt.posterior; W.gl_off = opt.gl_off; W.force_call = opt.force_call;
   W.denovo = opt.denovo;
 
-  std::map<std::string, int> chrSel;
-  {
-    size_t i = 0;
-    const std::string& s = opt.chrs2process;
-    while (i < s.size()) {
-      size_t j = s.find(',', i);
-      if (j == std::string::npos) j = s.size();
-      if (j > i) chrSel[s.substr(i, j - i)]++;
-      i = j + 1;
-    }
-  }
+  std::map<std::string, int> chrSel = parse_chr_selection(opt.chrs2process);
   const size_t chrSelCount = chrSel.size();
   time_t t0; time(&t0);
   printf("Analysis started on %s\n", ctime(&t0));
@@ -446,6 +656,28 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval) {
   }
   fclose(vcf);
   return 0;
+}
+
+int polymutt_main(int argc, char** argv, const ShardComm* comm, const EvaluatorFactory& make) {
+  try {
+    Options opt = parse_command_line(argc, argv);
+    Pedigree ped;
+    ped.load(opt.datFile, opt.pedFile);
+    if (!opt.blocksOut.empty()) {   // --glf2blocks: GLF site stream -> dense indexed blocks, no engine
+      if (opt.glfListFile.empty()) throw FatalError("--glf2blocks needs the GLF index file (-g)\n");
+      if (comm && comm->world > 1) throw FatalError("--glf2blocks runs in one process\n");
+      const long n = convert_glf_to_blocks(ped, opt.glfListFile, opt.blocksOut, default_io_threads(opt), opt.blockSites);
+      printf("%ld sites written to %s\n", n, opt.blocksOut.c_str());
+      return 0;
+    }
+    const pm_pedigree v = ped.view();
+    const pm_params par = opt.params();
+    std::unique_ptr<SiteEvaluator> ev = make(v, par, opt);
+    return run_polymutt(opt, ped, *ev, comm);
+  } catch (const FatalError& e) {
+    printf("\nFATAL ERROR - \n%s\n\n", e.what());
+    return 1;
+  }
 }
 
 }  // namespace pmhost

@@ -1,7 +1,9 @@
 // driver.h -- polymutt-compatible command line and section/site loop (src/main.cpp:57-627),
 // batching sites into dense blocks for a SiteEvaluator (the HIP engine in the product binary).
 #pragma once
+#include <functional>
 #include <map>
+#include <memory>
 #include <string>
 #include <vector>
 #include "../../include/polymutt_engine.h"
@@ -38,11 +40,28 @@ class SiteEvaluator {
   virtual void run(int n, const uint8_t* pl, const uint32_t* dm, const uint8_t* ref, pm_site_result* res, pm_geno_call* calls,
                    int* n_rows) = 0;
   virtual void counters(pm_counters* out) = 0;
+  // famlk[0]'s stale posterior state at a shard start (pm_engine_set_posterior_carry)
+  virtual void set_posterior_carry(bool seen) = 0;
 };
+
+// A run split over processes (one per GPU; polymutt_amd/launch.py): rank `rank` of `world` analyses a
+// contiguous position range of every section.  `allgather` exchanges n int64 per rank (recv: world x n,
+// rank-major); it is called the same number of times on every rank (once per section, once at the end).
+struct ShardComm {
+  int rank = 0, world = 1;
+  std::function<void(const int64_t* send, int n, int64_t* recv)> allgather;
+};
+
+using EvaluatorFactory = std::function<std::unique_ptr<SiteEvaluator>(const pm_pedigree&, const pm_params&, const Options&)>;
 
 int default_io_threads(const Options& opt);
 
-// Runs the whole analysis; returns the process exit code.
-int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval);
+// Runs the whole analysis; returns the process exit code.  With comm->world > 1 the run is one shard
+// (run_polymutt_sharded).
+int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, const ShardComm* comm = nullptr);
+
+// The command line end to end (parse, pedigree, --glf2blocks, evaluator, run); FatalError -> the reference's
+// "FATAL ERROR" text on stdout and exit code 1.
+int polymutt_main(int argc, char** argv, const ShardComm* comm, const EvaluatorFactory& make);
 
 }  // namespace pmhost

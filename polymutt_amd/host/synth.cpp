@@ -64,6 +64,16 @@ bool synth_shape(const std::string& shape, int fam, std::vector<SynthMember>& ou
     add(0, 1, 1, 3); add(2, 3, 2, 6); add(4, 5, 1, 7); add(4, 5, 2, 8);
     return true;
   }
+  if (shape == "roof2") {
+    // 1 x 2 -> 5(f); 3 x 4 -> 6(m); 6 x 5 -> 7, 8(m); 11 x 12 -> 9(f); 8 x 9 -> 10.  Three roofs peel first
+    // (parents -> only child); the (6, 5) couple then becomes a roof itself, keyed (father, mother) like the
+    // marriage partial its leaf child 7 created, so its type-3 peel runs WITH marriage partials
+    // (FamilyLikelihoodES.cpp:1358-1395; plain `transmission` under --denovo, :1391).
+    // path: founders 1,2,3,4,11,12 then 5,6,7,8,9,10
+    add(-1, -1, 1, 1); add(-1, -1, 2, 2); add(-1, -1, 1, 3); add(-1, -1, 2, 4); add(-1, -1, 1, 11); add(-1, -1, 2, 12);
+    add(0, 1, 2, 5); add(2, 3, 1, 6); add(7, 6, 1, 7); add(7, 6, 1, 8); add(4, 5, 2, 9); add(9, 10, 2, 10);
+    return true;
+  }
   if (shape == "single") { add(-1, -1, 1 + fam % 2, 1); return true; }
   // quads with an ext10 pedigree at families 256, 513, ...: a few extended families next to hundreds of
   // nuclear ones (the lane plan must pair nuclear slots with per-lane extended lists)
@@ -72,13 +82,18 @@ bool synth_shape(const std::string& shape, int fam, std::vector<SynthMember>& ou
 }
 
 // shape "<template>+dn": additionally plants a de novo het call (ref/transition) in one non-founder
-// of one family at ~3% of sites, so the --denovo output path has records to check.  Files only:
-// the device generator (bench) never plants.
+// of one family at ~3% of sites, so the --denovo output path has records to check.  "+late": the first
+// half of the sites are monomorphic (a site shard whose range emits nothing).  Files only: the device
+// generator (bench) does neither.
 int synth_write_dataset(const std::string& dir, const std::string& shape_arg, int nfam, int nsites, uint64_t seed,
                         std::string& err) {
   std::string shape = shape_arg;
-  bool plant = false;
-  if (shape.size() > 3 && shape.compare(shape.size() - 3, 3, "+dn") == 0) { plant = true; shape.resize(shape.size() - 3); }
+  bool plant = false, late = false;
+  for (bool more = true; more;) {
+    more = false;
+    if (shape.size() > 3 && shape.compare(shape.size() - 3, 3, "+dn") == 0) { plant = more = true; shape.resize(shape.size() - 3); }
+    if (shape.size() > 5 && shape.compare(shape.size() - 5, 5, "+late") == 0) { late = more = true; shape.resize(shape.size() - 5); }
+  }
   mkdir(dir.c_str(), 0755);
   static pm_synth_tables T;
   static bool built = false;
@@ -128,6 +143,7 @@ int synth_write_dataset(const std::string& dir, const std::string& shape_arg, in
   for (int s = 0; s < nsites; s++) {
     int ref; double af;
     pm_syn_site(seed, (uint64_t)s, &ref, &af);
+    if (late && s < nsites / 2) af = 0.0;   // "+late": no polymorphism in the first half of the section
     for (int f = 0; f < nfam; f++) {
       const auto& F = fams[f];
       int n = (int)F.size();

@@ -22,9 +22,9 @@ struct VcfWriter {
   // One OutputVCF(_denovo) call: writes the header on first use, then the record unless suppressed.
   void output(const std::string& label, int pos1, int refBase, const pm_site_result& r, const pm_geno_call* calls,
               const uint8_t* pl, const uint32_t* dm);
+  void header();   // written by output() on first use; a sharded run's lead writes it once at the merge
 
  private:
-  void header();
   bool singleNuclear() const;
   std::string line_;   // genotype columns of the record being written (reused)
 };

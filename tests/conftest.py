@@ -47,8 +47,12 @@ def cpu_driver():
     """tests/native/build/cpu_polymutt: the product host driver with the CPU oracle as evaluator."""
     exe = os.path.join(ROOT, "tests", "native", "build", "cpu_polymutt")
     import __graft_entry__
-    srcs = [os.path.join(ROOT, "tests", "native", "cpu_polymutt.cpp"), os.path.join(ROOT, "oracle", "pm_oracle.c")] + \
+    lib = os.path.join(ROOT, "tests", "native", "build", "libpm_cpu_driver.so")
+    nat = os.path.join(ROOT, "tests", "native")
+    srcs = [os.path.join(nat, f) for f in os.listdir(nat) if f.endswith((".cpp", ".h"))] + \
+        [os.path.join(ROOT, "oracle", f) for f in ("pm_oracle.c", "pm_oracle.h")] + \
         [os.path.join(ROOT, "polymutt_amd", "host", f) for f in os.listdir(os.path.join(ROOT, "polymutt_amd", "host"))]
-    if not os.path.exists(exe) or max(os.path.getmtime(s) for s in srcs) > os.path.getmtime(exe):
+    if not os.path.exists(exe) or not os.path.exists(lib) or \
+            max(os.path.getmtime(s) for s in srcs) > min(os.path.getmtime(exe), os.path.getmtime(lib)):
         __graft_entry__.build_cpu_driver()
     return exe

@@ -101,6 +101,10 @@ def _steps(ped, f):
     ("ext10", [(1, 6, -1, 4, 2), (1, 7, -1, 4, 2), (1, 8, -1, 3, 5), (1, 9, -1, 3, 5), (2, 2, -1, 4, -1),
                (2, 3, -1, 5, -1), (1, 4, -1, 0, 1), (1, 5, -1, 0, 1), (2, 0, -1, 1, -1)]),
     ("roof", [(1, 6, -1, 4, 5), (1, 7, -1, 4, 5), (3, 0, 1, 4, -1), (3, 2, 3, 5, -1), (2, 4, -1, 5, -1)]),
+    # traced by hand through ES_Peeling::BuildPeelingOrder (FamilyLikelihoodES.cpp:135-277): the roof (7, 6) is
+    # created by UpdateRoof after the type-3 peel into 7 and keyed like the marriage partial of leaf 8
+    ("roof2", [(1, 8, -1, 7, 6), (1, 11, -1, 9, 10), (3, 0, 1, 6, -1), (3, 2, 3, 7, -1), (3, 4, 5, 10, -1),
+               (3, 7, 6, 9, -1), (2, 10, -1, 9, -1)]),
 ])
 def test_peeling_schedule_matches_reference(tmp_path, shape, expected):
     pm.synth_write_dataset(str(tmp_path), shape, 2, 1, 1)
@@ -135,44 +139,72 @@ def test_shard_range_partitions():
             assert max(h - l for l, h in rs) - min(h - l for l, h in rs) <= 1
 
 
-def _sharded_worker(rank, world, port, d, out):
-    import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    import sys
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from fixtures import read_dataset
-    from oracle_binding import Oracle
-    from polymutt_amd.shard import allreduce_counters
-    ped, secs, _ = read_dataset(d)
-    (label, pos, ref, pl, dm), = secs
-    lo, hi = shard_range(len(ref), rank, world)
-    ora = Oracle(ped.view, pm.Params.defaults())
-    ora.begin_section(pm.PM_CHR_AUTO)
-    ora.run(pl[lo:hi], dm[lo:hi], ref[lo:hi])
-    total = allreduce_counters(ora.counters().as_array())
-    if rank == 0:
-        np.save(out, total)
-    dist.destroy_process_group()
-
-
-def test_sharded_counters_allreduce_gloo(tmp_path):
+def _free_port():
     import socket
-    import torch.multiprocessing as mp
-    from fixtures import read_dataset
-    from oracle_binding import Oracle
-    d = str(tmp_path / "ds")
-    pm.synth_write_dataset(d, "quad", 20, 301, 9)
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    out = str(tmp_path / "total.npy")
-    mp.start_processes(_sharded_worker, args=(2, port, d, out), nprocs=2, join=True, start_method="spawn")
-    ped, secs, _ = read_dataset(d)
-    (label, pos, ref, pl, dm), = secs
-    ora = Oracle(ped.view, pm.Params.defaults())
-    ora.begin_section(pm.PM_CHR_AUTO)
-    ora.run(pl, dm, ref)
-    whole = ora.counters().as_array()
-    assert (np.load(out) == whole).all()
-    assert whole[:5].sum() == 301
+        return s.getsockname()[1]
+
+
+def run_sharded(cwd, args, world, lib=None, timeout=600):
+    """polymutt_amd.launch under torchrun: `world` one-process shards of the product driver (lib: another
+    pmh_run_polymutt build, e.g. the CPU-oracle one).  Returns the CompletedProcess."""
+    import sys
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "-m", "polymutt_amd.launch"]
+    cmd += (["--lib", lib] if lib else []) + list(args)
+    env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""), OMP_NUM_THREADS="1")
+    return subprocess.run(cmd, cwd=cwd, capture_output=True, text=True, timeout=timeout, env=env)
+
+
+def summary_lines(stdout):
+    """The section summaries a run prints (main.cpp:596-619), without the wall-clock lines."""
+    keep, on = [], False
+    for l in stdout.splitlines():
+        if l.startswith("Summary of reference"):
+            on = True
+        if on and l.strip() and not l.startswith(("Analysis ended", "Running time")):
+            keep.append(l)
+    return keep
+
+
+def vcf_body(path):
+    return [l for l in open(path).read().splitlines() if not l.startswith("##")]
+
+
+def _sharded_case(tmp_path, case):
+    from conftest import EXAMPLE
+    import shutil
+    if case == "example":
+        return EXAMPLE, ["-p", "test.ped", "-d", "test.dat", "-g", "test.gif"]
+    if case == "ragged":
+        return os.path.join(os.path.dirname(EXAMPLE), "ingest"), ["-p", "test.ped", "-d", "test.dat", "-g", "test.gif",
+                                                                  "--all_sites"]
+    d = str(tmp_path / case)
+    if case == "quad_chrX":
+        from fixtures import make_dataset
+        make_dataset("quad_chrX", d)
+        return d, ["-p", "test.ped", "-d", "test.dat", "-g", "test.gif", "--chrX", "1"]
+    if case == "late_chrX":   # shard 0 emits nothing: shard 1 must redo its first record with famlk[0] unseen
+        pm.synth_write_dataset(d, "trio+late", 30, 400, 31)   # (trios: the last person is male, so the state matters)
+        return d, ["-p", "test.ped", "-d", "test.dat", "-g", "test.gif", "--chrX", "1"]
+    raise ValueError(case)
+
+
+@pytest.mark.parametrize("case,world", [("example", 2), ("ragged", 2), ("quad_chrX", 2), ("late_chrX", 2),
+                                        ("quad_chrX", 3)])
+def test_sharded_driver_matches_one_process_gloo(cpu_driver, tmp_path, case, world):
+    """The multi-process driver (polymutt_amd/launch.py: contiguous position range per rank, one exchange per
+    section over gloo) on the CPU oracle writes the same VCF and section summaries as one process."""
+    cwd, args = _sharded_case(tmp_path, case)
+    one = str(tmp_path / "one.vcf")
+    r1 = subprocess.run([cpu_driver] + args + ["--out_vcf", one], cwd=cwd, capture_output=True, text=True, timeout=600)
+    assert r1.returncode == 0, r1.stdout[-2000:]
+    sh = str(tmp_path / "sharded.vcf")
+    lib = os.path.join(ROOT, "tests", "native", "build", "libpm_cpu_driver.so")
+    r2 = run_sharded(cwd, args + ["--out_vcf", sh], world, lib=lib)
+    assert r2.returncode == 0, r2.stdout[-3000:] + r2.stderr[-3000:]
+    assert vcf_body(sh) == vcf_body(one)
+    assert summary_lines(r2.stdout) == summary_lines(r1.stdout) and summary_lines(r1.stdout)
+    assert not [f for f in os.listdir(os.path.dirname(sh)) if ".part" in f]   # shard files merged and removed
+    assert ("first record re-run" in r2.stderr) == (case == "late_chrX"), r2.stderr[-2000:]

@@ -222,3 +222,50 @@ def test_headline_config_parity(built, denovo):
     o, oc = Oracle(ped, params).run(pl, dm, ref)
     st = compare_results(e, o, ec, oc, label="headline ")
     assert st["sites"] == 1024 and st["called"] > 0
+
+
+@pytest.mark.parametrize("case", ["example", "quad_chrX", "late_chrX"])
+def test_cli_two_shards_match_one_process(built, tmp_path, case):
+    """polymutt_amd.launch with 2 ranks (here both on the one GPU, gloo for the per-section exchange; RCCL
+    when each rank has its own GPU) writes the same VCF and section summaries as the one-process CLI."""
+    from test_cpu_host import _sharded_case, run_sharded, summary_lines, vcf_body
+    cwd, args = _sharded_case(tmp_path, case)
+    one = str(tmp_path / "one.vcf")
+    r1 = subprocess.run([pm.BIN_PATH] + args + ["--out_vcf", one], cwd=cwd, capture_output=True, text=True, timeout=300)
+    assert r1.returncode == 0, r1.stdout[-2000:]
+    sh = str(tmp_path / "sharded.vcf")
+    r2 = run_sharded(cwd, args + ["--out_vcf", sh], 2)
+    assert r2.returncode == 0, r2.stdout[-3000:] + r2.stderr[-3000:]
+    assert vcf_body(sh) == vcf_body(one)
+    assert summary_lines(r2.stdout) == summary_lines(r1.stdout) and summary_lines(r1.stdout)
+    assert ("first record re-run" in r2.stderr) == (case == "late_chrX")
+
+
+def test_posterior_carry_matches_oracle(built, tmp_path):
+    """famlk[0]'s stale posterior state (pm_engine_set_posterior_carry) set explicitly, as a shard start does:
+    the engine's chrX genotype posteriors follow the oracle's for both states, and the state is visible in
+    them (trios: the last person is male, so the stale member sex changes the first family's kid terms)."""
+    d = str(tmp_path / "t")
+    pm.synth_write_dataset(d, "trio+late", 30, 400, 31)
+    ped = pm.Pedigree(os.path.join(d, "test.dat"), os.path.join(d, "test.ped"))
+    label, pos, ref, pl, dm = _read_all(ped, d)[0]
+    from oracle_binding import lib
+    import ctypes as C
+    L = lib()
+    L.pmo_set_posterior_carry.argtypes = [C.c_void_p, C.c_int32]
+    dos = []
+    for carry in (0, 1):
+        eng = pm.Engine(ped.view, pm.Params.defaults(), max_batch=256)
+        ora = Oracle(ped.view, pm.Params.defaults())
+        eng.begin_section(pm.PM_CHR_X)
+        ora.begin_section(pm.PM_CHR_X)
+        eng.set_posterior_carry(carry)
+        L.pmo_set_posterior_carry(ora.h, carry)
+        e, ec = eng.run(pl[200:456], dm[200:456], ref[200:456])
+        o, oc = ora.run(pl[200:456], dm[200:456], ref[200:456])
+        compare_results(e, o, ec, oc, label=f"carry={carry} ")
+        assert ec.shape[0] > 0
+        np.testing.assert_allclose(ec["dosage"], oc["dosage"], rtol=1e-9, atol=1e-300)
+        dos.append(ec["dosage"][0].copy())
+        eng.close()
+    assert (dos[0] != dos[1]).any()   # the first record's posteriors depend on the state

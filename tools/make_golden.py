@@ -57,6 +57,10 @@ CASES = {
     # ES type-3 peels (parents -> only child) under the 10-state de novo model and on chrX
     "roof_denovo": ("roof+dn", 12, 300, 83, ["--denovo", "--rate_denovo", "1e-6"]),
     "roof_chrX": ("roof", 12, 300, 89, ["--chrX", "1"]),
+    # type-3 peel WITH a marriage partial (a roof created by UpdateRoof): BA, --denovo (:1391), chrX
+    "roof2_auto": ("roof2", 10, 300, 103, []),
+    "roof2_denovo": ("roof2+dn", 10, 300, 107, ["--denovo", "--rate_denovo", "1e-6"]),
+    "roof2_chrX": ("roof2", 10, 300, 109, ["--chrX", "1"]),
     # BASELINE.json config geometries (the lane plans and kernels the bench selects for them)
     "big_trio_1000": ("trio", 1000, 256, 11, []),
     "big_quad_1000_denovo": ("quad", 1000, 256, 7, ["--denovo"]),
