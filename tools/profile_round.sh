@@ -11,7 +11,7 @@ R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$R/gpurun_out/prof_$ROUND
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-BENCH="python3 $R/bench.py --no-cpu-baseline"
+BENCH="python3 $R/bench.py --no-cpu-baseline --steps 40 --calib-steps 4"
 step() {   # step NAME SECONDS CMD...
   local name=$1 secs=$2; shift 2
   echo "[$(date +%T)] $name" >&2
@@ -20,8 +20,13 @@ step() {   # step NAME SECONDS CMD...
   if [ $rc -ne 0 ]; then echo "step $name failed rc=$rc" >&2; tail -20 "$OUT/$name.err" >&2; exit $rc; fi
 }
 step fp64_peak 120 "$R/tools/fp64_peak"
+# default bench (3 overlapping engines): whole-step kernel mix; per-kernel durations there include GPU sharing
 step trace 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- $BENCH
-step pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- $BENCH --steps 4 --warmup 1
-step pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- $BENCH --steps 4 --warmup 1
-step pmc_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmc_sq" -o run -- $BENCH --steps 4 --warmup 1
+# one engine: each kernel alone on the GPU -- the per-kernel times the roofline uses
+step trace1 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace1" -o run -- $BENCH --engines 1
+# BASELINE config 4 shape (200 ext10 pedigrees, Elston-Stewart peeling), one engine
+step trace_ext10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_ext10" -o run -- $BENCH --engines 1 --shape ext10 --families 200 --batch 16384 --no-denovo --steps 8
+step pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- $BENCH --engines 1 --steps 4 --warmup 1 --calib-steps 0
+step pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- $BENCH --engines 1 --steps 4 --warmup 1 --calib-steps 0
+step pmc_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmc_sq" -o run -- $BENCH --engines 1 --steps 4 --warmup 1 --calib-steps 0
 echo done >&2

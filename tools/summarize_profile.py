@@ -2,9 +2,11 @@
 """Summarise a tools/profile_round.sh run (gpurun_out/prof_ROUND) into committed files under profiles/:
 
   profiles/ROUND_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary of the default bench command
-  profiles/ROUND_bench.json         the bench JSON line printed under that profiler run
-  profiles/ROUND_pmc.json           per kernel: dispatches and mean FETCH_SIZE / WRITE_SIZE / SQ counters per
-                                    dispatch, plus HBM bytes per dispatch with the gfx950 correction
+  profiles/ROUND_kernel_stats_1engine.csv   ... of the same workload on one engine (kernels never overlap)
+  profiles/ROUND_kernel_stats_ext10.csv     ... of BASELINE config 4's shape (200 ext10 pedigrees), one engine
+  profiles/ROUND_bench*.json        the bench JSON lines printed under those profiler runs
+  profiles/ROUND_pmc.json           per kernel (one-engine bench): dispatches and mean FETCH_SIZE / WRITE_SIZE /
+                                    SQ counters per dispatch, plus HBM bytes per dispatch with the gfx950 correction
                                     (MI355X_MICROARCH.md "HBM": FETCH_SIZE counts 1/2 of the bytes -> x2)
   profiles/ROUND_fp64_peak.json     measured FP64 issue rates (tools/fp64_peak.hip)
 """
@@ -28,11 +30,14 @@ def main():
     src = os.path.join(ROOT, "gpurun_out", f"prof_{rnd}")
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
-    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, f"{rnd}_kernel_stats.csv"))
-    bench = [l for l in open(os.path.join(src, "trace.out")).read().splitlines() if l.startswith("{")]
-    if bench:
-        with open(os.path.join(dst, f"{rnd}_bench.json"), "w") as fh:
-            fh.write(bench[-1] + "\n")
+    for sub, suffix in (("trace", ""), ("trace1", "_1engine"), ("trace_ext10", "_ext10")):
+        if not os.path.exists(os.path.join(src, sub, "run_kernel_stats.csv")):
+            continue
+        shutil.copy(os.path.join(src, sub, "run_kernel_stats.csv"), os.path.join(dst, f"{rnd}_kernel_stats{suffix}.csv"))
+        bench = [l for l in open(os.path.join(src, sub + ".out")).read().splitlines() if l.startswith("{")]
+        if bench:
+            with open(os.path.join(dst, f"{rnd}_bench{suffix}.json"), "w") as fh:
+                fh.write(bench[-1] + "\n")
     peak = [l for l in open(os.path.join(src, "fp64_peak.out")).read().splitlines() if l.startswith("{")]
     if peak:
         with open(os.path.join(dst, f"{rnd}_fp64_peak.json"), "w") as fh:
