@@ -93,6 +93,14 @@ struct DevArgs {
   double* ws;              // peeling workspace, lane-interleaved
   int ws_per_lane;         // doubles per lane (max over ES families of n*ns + couples*ns*ns)
   int ws_lds;              // ES workspace in dynamic LDS (lane-interleaved) instead of HBM
+  // ES polynomial form (es_poly = 1, PM_NUM_POLY): per family, poly_lay[poly_start[f]..] = {couples, tmp offset,
+  // degree D per chromosome class [4], per person off | cap << 24, per couple off | cap << 24}; poly_deg[4 s + class]
+  // = the degrees a step combines (7 bits each); coefficients of the lane's q-th family at ws + poly_coef + q * poly_dcap
+  int es_poly;
+  const int* poly_start;
+  const int* poly_lay;
+  const int* poly_deg;
+  int poly_coef, poly_dcap;
   int unrelated;           // --quick_call MakeUnrelated(): every family is all-founder
   double theta_one;        // 1.0 (opaque to the compiler; timing experiments only)
   int vcf;                 // vcf_mode: one (ref, alt) Brent per site, FamilyLikelihoodSeq_VCF family rules
@@ -440,6 +448,176 @@ __device__ __forceinline__ double d_es_lk(const DevArgs& A, int f, const uint8_t
 }
 
 // ------------------------------------------------------------------------------------------------
+// ------------------------------------------------------------------------------------------------
+// Elston-Stewart peeling in polynomial form (PM_NUM_POLY).  Every founder prior is a homogeneous polynomial in
+// (f, g = 1 - f): f^2, 2fg, g^2 (degree 2); f, 0, g on chrX/Y males and chrMT (degree 1); constants for chrY
+// females (degree 0).  The peel only multiplies and adds, so a family likelihood is
+//     L(f) = sum_a c_a f^a g^(D - a),   c_a >= 0,   D = the founders' degrees summed,
+// and every partial / marriage-partial entry along the way is such a polynomial of a degree the host tracks per
+// step (poly_layout).  The same steps as d_es_lk (FamilyLikelihoodES.cpp :1013-1032, :1105-1395) run once per
+// Brent item on coefficient vectors; each objective evaluation is then one Horner pass over D + 1 non-negative
+// coefficients (no cancellation: relative error ~ (D + 2) ulp, the class of PM_NUM_POLY's nuclear quartics).
+// The reference-order numeric peel stays in d_es_lk (PM_NUM_PRODUCT / PM_NUM_EXACT, and the posteriors).
+template <int NS>
+__device__ __forceinline__ int es_poly_hoist(const DevArgs& A, int f, const uint8_t* pl, const double* lk, int g11, int g12,
+                                             int g22, int chrom, double* ws, size_t st, double* out) {
+  const int p0 = A.fam_start[f], n = A.fam_start[f + 1] - p0, nf = A.fam_founders[f];
+  const bool X = chrom == PM_CHR_X, Y = chrom == PM_CHR_Y, MT = chrom == PM_CHR_MT;
+  const int* L = A.poly_lay + A.poly_start[f];
+  const int tof = L[1], D = L[2 + chrom];
+  const size_t np = (size_t)A.n_person;
+#define WV(o) ws[(size_t)(o) * st]
+#define POFF(i) (L[6 + (i)] & 0xFFFFFF)
+#define PCAP(i) (L[6 + (i)] >> 24)
+#define MOFF(m) (L[6 + n + (m)] & 0xFFFFFF)
+#define MCAP(m) (L[6 + n + (m)] >> 24)
+  for (int i = 0; i < n; i++) {   // InitializePartials(_BA) x SetFounderPriors(_BA)
+    const int sx = A.sex[p0 + i];
+    const bool fo = A.is_founder[p0 + i] != 0 && i < nf;
+    const uint8_t* R = pl + p0 + i;
+    const int o = POFF(i), cap = PCAP(i);
+    const bool yf = Y && sx == FEMALE;
+    const int d = !fo ? 0 : (Y && sx == FEMALE) ? 0 : ((X || Y) && sx == MALE) || MT ? 1 : 2;
+    const int gidx[3] = {g11, g12, g22};
+    for (int j = 0; j < NS; j++) {
+      for (int a = 0; a <= d; a++) WV(o + j * cap + a) = 0.0;
+      if (NS == 3) {
+        const double pen = lk[R[gidx[j] * np]];
+        if (yf) { WV(o + j * cap) = 1.0; continue; }   // BA chrY females: partial 1.0 (:1449-1465)
+        if (!fo) { WV(o + j * cap) = pen; continue; }
+        if (d == 2) WV(o + j * cap + 2 - j) = j == 1 ? 2 * pen : pen;   // f^2, 2fg, g^2
+        else if (j != 1) WV(o + j * cap + (j == 0 ? 1 : 0)) = pen;      // f, 0, g
+      } else {
+        const double pen = lk[R[j * np]];
+        if (!fo) { WV(o + j * cap) = pen; continue; }
+        const int q = j == g11 ? 0 : j == g12 ? 1 : j == g22 ? 2 : 3;
+        if (q == 3) continue;
+        if (d == 2) WV(o + j * cap + 2 - q) = q == 1 ? 2 * pen : pen;
+        else if (d == 1) { if (q != 1) WV(o + j * cap + (q == 0 ? 1 : 0)) = pen; }
+        else WV(o + j * cap) = pen;   // chrY female founder: q = 1, 1, 1
+      }
+    }
+  }
+  const int s0 = A.peel_start[f], s1 = A.peel_start[f + 1];
+  for (int s = s0; s < s1; s++) {
+    const int2 S = A.steps[s];
+    const int type = S.x & 255, from0 = (S.x >> 8) & 255, from1 = (S.x >> 16) & 255, to0 = (S.x >> 24) & 255;
+    const int slot = (S.y >> 8) & 255, create = (S.y >> 16) & 1, fa2mo = (S.y >> 17) & 1;
+    const int dg = A.poly_deg[4 * s + chrom];
+    const int da = dg & 127, db = (dg >> 7) & 127, dc = (dg >> 14) & 127, de = (dg >> 21) & 127;
+    if (type == 1) {   // offspring -> parents: M(i, j) *= sum_k T(i, j, k) P_off[k]   (da = deg P_off, db = deg M)
+      const int off = from0, po = POFF(off), pc = PCAP(off), mo = MOFF(slot), mc = MCAP(slot);
+      const int csex = A.sex[p0 + off];
+      if (create)
+        for (int e = 0; e < NS * NS; e++) WV(mo + e * mc) = 1.0;
+      for (int i = 0; i < NS; i++)
+        for (int j = 0; j < NS; j++) {
+          for (int a = 0; a <= da; a++) {
+            double sum = 0;
+            for (int k = 0; k < NS; k++) {
+              const double t = (NS == 3) ? d_tba(i, j, k, chrom, csex) : A.T10dn[(i * 10 + j) * 10 + k];
+              sum += t * WV(po + k * pc + a);
+            }
+            WV(tof + a) = sum;
+          }
+          const int e0 = mo + (i * NS + j) * mc;
+          for (int a = db + da; a >= 0; a--) {   // in place, highest coefficient first
+            double acc = 0;
+            for (int c = max(0, a - da); c <= min(a, db); c++) acc += WV(e0 + c) * WV(tof + a - c);
+            WV(e0 + a) = acc;
+          }
+        }
+    } else if (type == 2) {   // spouse -> spouse: P_to[i] *= sum_j P_from[j] M(j, i)   (da from, db M, dc to)
+      const int sf = from0, stt = to0, fo_ = POFF(sf), fc = PCAP(sf), to_ = POFF(stt), tc = PCAP(stt);
+      const int mo = slot == 255 ? 0 : MOFF(slot), mc = slot == 255 ? 0 : MCAP(slot);
+      for (int i = 0; i < NS; i++) {
+        for (int a = 0; a <= da + db; a++) {
+          double sum = 0;
+          for (int j = 0; j < NS; j++) {
+            if (slot == 255) { sum += a <= da ? WV(fo_ + j * fc + a) : 0.0; continue; }
+            const int e0 = mo + (fa2mo ? j * NS + i : i * NS + j) * mc;
+            for (int u = max(0, a - db); u <= min(a, da); u++) sum += WV(fo_ + j * fc + u) * WV(e0 + a - u);
+          }
+          WV(tof + a) = sum;
+        }
+        const int e0 = to_ + i * tc, ds = da + db;
+        for (int a = dc + ds; a >= 0; a--) {
+          double acc = 0;
+          for (int c = max(0, a - ds); c <= min(a, dc); c++) acc += WV(e0 + c) * WV(tof + a - c);
+          WV(e0 + a) = acc;
+        }
+      }
+    } else {   // parents -> only offspring: P_off[k] *= sum_ij P_fa[i] M(i, j) P_mo[j] T(i, j, k)   (da fa, db M, dc mo, de off)
+      const int fa = from0, mo_ = from1, off = to0;
+      const int fao = POFF(fa), fac = PCAP(fa), moo = POFF(mo_), moc = PCAP(mo_), oo = POFF(off), oc = PCAP(off);
+      const int mo = slot == 255 ? 0 : MOFF(slot), mc = slot == 255 ? 0 : MCAP(slot);
+      const int csex = A.sex[p0 + off];
+      const int dw = da + db + dc, w = tof + NS * (dw + 1);   // S_k at tof + k (dw + 1), W(i, j) at w
+      for (int e = 0; e < NS * (dw + 1); e++) WV(tof + e) = 0.0;
+      for (int i = 0; i < NS; i++)
+        for (int j = 0; j < NS; j++) {
+          for (int a = 0; a <= dw; a++) {
+            double acc = 0;
+            for (int u = 0; u <= da; u++)
+              for (int v = 0; v <= db; v++) {
+                const int r = a - u - v;
+                if (r < 0 || r > dc) continue;
+                const double m = slot == 255 ? 1.0 : WV(mo + (i * NS + j) * mc + v);
+                acc += WV(fao + i * fac + u) * m * WV(moo + j * moc + r);
+              }
+            WV(w + a) = acc;
+          }
+          for (int k = 0; k < NS; k++) {
+            double t;
+            if (NS == 3) t = d_tba(i, j, k, chrom, csex);
+            else t = (slot == 255) ? A.T10dn[(i * 10 + j) * 10 + k] : A.T10[(i * 10 + j) * 10 + k];   // quirk :1391
+            for (int a = 0; a <= dw; a++) WV(tof + k * (dw + 1) + a) += t * WV(w + a);
+          }
+        }
+      for (int k = 0; k < NS; k++) {
+        const int e0 = oo + k * oc;
+        for (int a = de + dw; a >= 0; a--) {
+          double acc = 0;
+          for (int c = max(0, a - dw); c <= min(a, de); c++) acc += WV(e0 + c) * WV(tof + k * (dw + 1) + a - c);
+          WV(e0 + a) = acc;
+        }
+      }
+    }
+  }
+  const int fin = (A.steps[s1 - 1].x >> 24) & 255, fo_ = POFF(fin), fc = PCAP(fin);
+  for (int a = 0; a <= D; a++) {
+    double sum = 0.0;
+    for (int i = 0; i < NS; i++) sum += WV(fo_ + i * fc + a);
+    out[(size_t)a * st] = sum;
+  }
+#undef WV
+#undef POFF
+#undef PCAP
+#undef MOFF
+#undef MCAP
+  return D;
+}
+
+// L(f) from the coefficients: g^D sum_a c_a t^a (t = f / g <= 1) or f^D sum_a c_a s^(D - a) (s = g / f < 1)
+__device__ __forceinline__ double es_poly_eval(const double* c, size_t st, int D, double x) {
+  const double g = 1 - x;
+  double acc, base;
+  if (x <= 0.5) {
+    const double t = x / g;
+    acc = c[(size_t)D * st];
+    for (int a = D - 1; a >= 0; a--) acc = acc * t + c[(size_t)a * st];
+    base = g;
+  } else {
+    const double sr = g / x;
+    acc = c[0];
+    for (int a = 1; a <= D; a++) acc = acc * sr + c[(size_t)a * st];
+    base = x;
+  }
+  double p = 1.0;
+  for (int a = 0; a < D; a++) p *= base;
+  return acc * p;
+}
+
 template <int T>
 __device__ __forceinline__ double block_sum(double x, double* red, int& par) {
 #pragma unroll
@@ -1069,8 +1247,10 @@ constexpr int brent_waves() { return (NUM == PM_NUM_POLY && !GEN && (T == 64 || 
 // DN: lean polynomial kernel for autosomal --denovo (instantiated separately so the common kernel carries
 // no de novo hoisting code or register pressure).
 // PF: lean kernel whose items' genotype planes are prefetched into LDS (prefetch_planes); no other hoisting path.
-template <int T, int S, int NUM, bool GEN, bool ES, bool DN = false, bool PF = false>
-__global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(DevArgs A, int list) {
+// EP: extended families in polynomial form (es_poly_hoist once per item, es_poly_eval per evaluation); the
+// reference-order peel (d_es_lk) is compiled out, and the block asks for 2 waves per SIMD.
+template <int T, int S, int NUM, bool GEN, bool ES, bool DN = false, bool PF = false, bool EP = false>
+__global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k_brent(DevArgs A, int list) {
   constexpr bool PROD = NUM != PM_NUM_EXACT;
   constexpr bool POLYK = NUM == PM_NUM_POLY && !GEN;
   __shared__ double s_lk[256];
@@ -1172,6 +1352,16 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
     // (two pointers, so each inlined peel keeps a known address space: ds_* or global_* accesses, no flat)
     double* wsl = ES ? A.ws + (size_t)blockIdx.x * A.ws_per_lane * T + threadIdx.x : nullptr;
     double* wsl_lds = ES ? (double*)s_pf + threadIdx.x : nullptr;
+    if constexpr (ES && EP) {   // polynomial form: the lane's extended families peeled once per item (es_poly_hoist)
+      if (A.ext_count)
+        for (int q = 0; q < A.ext_count[threadIdx.x]; q++) {
+          const int f = A.ext_fam[q * T + threadIdx.x];
+          double* co = wsl + (size_t)(A.poly_coef + q * A.poly_dcap) * T;
+          const int D = I.denovo ? es_poly_hoist<10>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, wsl, T, co)
+                                 : es_poly_hoist<3>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, wsl, T, co);
+          co[(size_t)(A.poly_dcap - 1) * T] = (double)D;
+        }
+    }
     const bool single = !A.vcf && ((cfg == 0) || (A.single_nuclear && !A.unrelated));
     // One evaluation site for the objective: the three bracketing evaluations of OptimizeFrequency
     // (:432-444) and every Brent step (core/MathGold.cpp:81-177) run through the same loop body.
@@ -1203,9 +1393,15 @@ __global__ void __launch_bounds__(T, (brent_waves<T, S, NUM, GEN>())) k_brent(De
         if (ES && A.ext_count)   // extended families of this lane: Elston-Stewart peeling per evaluation
           for (int q = 0; q < A.ext_count[threadIdx.x]; q++) {
             const int f = A.ext_fam[q * T + threadIdx.x];
-            const double v = I.denovo  ? d_es_lk<10>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, x, -1, -1, wsl, T)
-                             : A.ws_lds ? d_es_lk<3>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, x, -1, -1, wsl_lds, T)
-                                        : d_es_lk<3>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, x, -1, -1, wsl, T);
+            double v;
+            if constexpr (EP) {
+              const double* co = wsl + (size_t)(A.poly_coef + q * A.poly_dcap) * T;
+              v = es_poly_eval(co, T, (int)co[(size_t)(A.poly_dcap - 1) * T], x);
+            } else {
+              v = I.denovo  ? d_es_lk<10>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, x, -1, -1, wsl, T)
+                : A.ws_lds ? d_es_lk<3>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, x, -1, -1, wsl_lds, T)
+                           : d_es_lk<3>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, x, -1, -1, wsl, T);
+            }
             int e1, e2;
             const double mv = frexp(v, &e1);
             m = frexp(m * mv, &e2);
@@ -2095,6 +2291,10 @@ struct pm_engine {
   int8_t* d_is_founder = nullptr;
   int2* d_steps = nullptr;
   double *d_T10 = nullptr, *d_T10dn = nullptr, *d_ws = nullptr;
+  // ES polynomial form (PM_NUM_POLY): per-family layouts and per-step degrees (poly_layout)
+  bool es_poly = false;
+  int poly_ws = 0, poly_coef = 0, poly_dcap = 0;
+  int *d_poly_start = nullptr, *d_poly_lay = nullptr, *d_poly_deg = nullptr;
   // vcf_mode on chrX/Y/MT or with a single family: nuclear families go through ES peeling as well
   // (FamilyLikelihoodSeq_VCF.cpp:97-103), so a second lane plan with them in the per-lane ES lists
   bool vcf = false, plan1_ok = false, use_plan1 = false;
@@ -2148,7 +2348,7 @@ static int dalloc(X** p, size_t count) {
 }
 #define DALLOC(p, n) do { int _r = dalloc(&(p), (n)); if (_r) { pm_engine_destroy(E); return _r; } } while (0)
 
-static const struct { int T, S; } kVariants[] = {{64, 1}, {64, 2}, {64, 4}, {128, 4}, {256, 4}, {512, 2}, {512, 4},
+static const struct { int T, S; } kVariants[] = {{64, 1}, {64, 2}, {64, 4}, {128, 4}, {256, 1}, {256, 4}, {512, 2}, {512, 4},
                                                  {1024, 1}, {1024, 2}, {1024, 4}, {1024, 8}, {128, 8}, {64, 8}, {64, 16}};
 
 // Deal families to lanes: family-major round robin; founders-only families are split into <=3-person chunks
@@ -2221,6 +2421,67 @@ static int pack_steps(const pm_pedigree* ped, int f, int ns, std::vector<int2>& 
   return n * ns + (int)keys.size() * ns * ns;
 }
 
+// Layout of one family's peel in polynomial form (es_poly_hoist): for every chromosome class the degree each
+// step combines (founders: 2; 1 for chrX/Y males and chrMT; 0 for chrY females), per slot the coefficient
+// capacity (largest degree + 1 over the classes), a temp region, and the likelihood's degree D.  Appends the
+// family's layout ints to lay and its steps' degree words to deg; returns the workspace doubles, -1 if a degree
+// exceeds the packing (the exact peel is used then).
+static int poly_layout(const pm_pedigree* ped, int f, int ns, const int2* st, int nst, std::vector<int>& lay, std::vector<int>& deg) {
+  const int p0 = ped->fam_start[f], n = ped->fam_start[f + 1] - p0, nf = ped->fam_founders[f];
+  int nkeys = 0;
+  for (int s = 0; s < nst; s++)
+    if ((st[s].x & 255) == 1) nkeys = std::max(nkeys, ((st[s].y >> 8) & 255) + 1);
+  std::vector<int> capP(n, 1), capM(nkeys, 1), Dc(4, 0);
+  std::vector<int> dg((size_t)nst * 4, 0);
+  int tmp = 1;
+  for (int cls = 0; cls < 4; cls++) {
+    const bool X = cls == PM_CHR_X, Y = cls == PM_CHR_Y, MT = cls == PM_CHR_MT;
+    std::vector<int> dP(n), dM(nkeys, 0);
+    for (int i = 0; i < n; i++) {
+      const bool fo = ped->is_founder[p0 + i] && i < nf;
+      const int sx = ped->sex[p0 + i];
+      dP[i] = !fo ? 0 : (Y && sx == FEMALE) ? 0 : (((X || Y) && sx == MALE) || MT) ? 1 : 2;
+      capP[i] = std::max(capP[i], dP[i] + 1);
+    }
+    for (int s = 0; s < nst; s++) {
+      const int type = st[s].x & 255, from0 = (st[s].x >> 8) & 255, from1 = (st[s].x >> 16) & 255, to0 = (st[s].x >> 24) & 255;
+      const int slot = (st[s].y >> 8) & 255, create = (st[s].y >> 16) & 1;
+      int a = 0, b = 0, c = 0, e = 0;
+      if (type == 1) {
+        a = dP[from0]; b = create ? 0 : dM[slot];
+        dM[slot] = a + b;
+        capM[slot] = std::max(capM[slot], dM[slot] + 1);
+        tmp = std::max(tmp, a + 1);
+      } else if (type == 2) {
+        a = dP[from0]; b = slot == 255 ? 0 : dM[slot]; c = dP[to0];
+        dP[to0] = a + b + c;
+        capP[to0] = std::max(capP[to0], dP[to0] + 1);
+        tmp = std::max(tmp, a + b + 1);
+      } else {
+        a = dP[from0]; b = slot == 255 ? 0 : dM[slot]; c = dP[from1]; e = dP[to0];
+        dP[to0] = a + b + c + e;
+        capP[to0] = std::max(capP[to0], dP[to0] + 1);
+        tmp = std::max(tmp, (ns + 1) * (a + b + c + 1));
+      }
+      if (std::max({a, b, c, e, a + b + c + e}) > 120) return -1;
+      dg[(size_t)s * 4 + cls] = a | (b << 7) | (c << 14) | (e << 21);
+    }
+    Dc[cls] = dP[(st[nst - 1].x >> 24) & 255];
+  }
+  const size_t base = lay.size();
+  lay.push_back(nkeys);
+  lay.push_back(0);   // temp offset, below
+  for (int c = 0; c < 4; c++) lay.push_back(Dc[c]);
+  int off = 0;
+  for (int i = 0; i < n; i++) { if (capP[i] > 127) return -1; lay.push_back(off | (capP[i] << 24)); off += ns * capP[i]; }
+  for (int m = 0; m < nkeys; m++) { if (capM[m] > 127) return -1; lay.push_back(off | (capM[m] << 24)); off += ns * ns * capM[m]; }
+  lay[base + 1] = off;
+  off += tmp;
+  if (off >= (1 << 24)) return -1;
+  deg.insert(deg.end(), dg.begin(), dg.end());
+  return off;
+}
+
 static int gi_h(int b1, int b2) { return b1 < b2 ? (b1 - 1) * (10 - b1) / 2 + (b2 - b1) : (b2 - 1) * (10 - b2) / 2 + (b1 - b2); }
 
 // FamilyLikelihoodES::SetTransmissionMatrix (:752-785) and SetTransmissionMatrix_denovo (:787-810)
@@ -2259,7 +2520,7 @@ void pm_engine_destroy(pm_engine* E) {
   if (!E) return;
   hipSetDevice(E->device);
   void* bufs[] = {E->d_units1, E->d_ext_count1, E->d_ext_fam1, E->d_fam_founders, E->d_peel_start, E->d_ext_count, E->d_ext_fam, E->d_is_founder, E->d_steps, E->d_T10,
-                  E->d_T10dn, E->d_ws, E->d_units_q,
+                  E->d_T10dn, E->d_ws, E->d_units_q, E->d_poly_start, E->d_poly_lay, E->d_poly_deg,
                   E->d_fam_start, E->d_fam_kind, E->d_fa, E->d_mo, E->d_sex, E->d_units, E->d_lktab, E->d_M, E->d_syn,
                   E->d_pl, E->d_stage, E->d_ref, E->d_dm, E->d_res, E->d_calls, E->d_raw, E->d_minv, E->d_mono, E->d_evals,
                   E->d_items[0], E->d_items[1], E->d_items[2], E->d_counts, E->d_eval_total, E->d_row_site,
@@ -2330,7 +2591,7 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
   {
     const bool gen = (par->denovo && par->numerics != PM_NUM_POLY) || E->has_fp || ped->n_fam == 1;
     static const int2 lean[] = {{64, 1}, {64, 2}, {64, 4}, {64, 8}, {64, 16}, {512, 4}, {1024, 4}, {1024, 8}};
-    static const int2 generic[] = {{64, 1}, {64, 2}, {64, 4}, {64, 8}, {256, 4}, {512, 4}, {1024, 4}, {1024, 8}};
+    static const int2 generic[] = {{64, 1}, {64, 2}, {64, 4}, {64, 8}, {256, 1}, {256, 4}, {512, 4}, {1024, 4}, {1024, 8}};
     // lean --denovo: the de novo hoisting state does not fit 16 slots per lane without spilling; 8 slots on
     // 2 waves per item is faster (measured: 6.6 vs 6.1 M sites/s, 1000 quads)
     static const int2 lean_dn[] = {{64, 1}, {64, 2}, {64, 4}, {64, 8}, {128, 8}, {512, 4}, {1024, 4}, {1024, 8}};
@@ -2344,7 +2605,8 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
     // extended families are the expensive terms: spread them one per lane up to 256 lanes
     int tmin = 1;
     while (tmin < std::min(E->n_ext, 256)) tmin *= 2;
-    for (int i = 0; i < 8 && !planned; i++)
+    const int npref = gen ? 9 : 8;
+    for (int i = 0; i < npref && !planned; i++)
       if (pref[i].x >= tmin && plan_units(ped, pref[i].x, pref[i].y, units)) { E->T = pref[i].x; E->S = pref[i].y; planned = true; }
   }
   if (!planned) { pm_engine_destroy(E); pm_set_last_error("pm_engine_create: pedigree too large for the lane plan"); return PM_EPED; }
@@ -2410,6 +2672,23 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
     }
     peel_start[ped->n_fam] = (int)steps.size();
     E->ws_per_lane = wsmax;
+    // polynomial-form layouts (PM_NUM_POLY): every family with a schedule.  Under --denovo the 10-state layout
+    // also serves the BA (cfg-7) items: the degrees do not depend on the state count, the slots are larger.
+    std::vector<int> poly_start(ped->n_fam + 1, 0), poly_lay, poly_deg((size_t)steps.size() * 4, 0);
+    int poly_w = 0, poly_d = 0;
+    E->es_poly = par->numerics == PM_NUM_POLY && !steps.empty();
+    for (int f = 0; f < ped->n_fam && E->es_poly; f++) {
+      poly_start[f] = (int)poly_lay.size();
+      const int ns0 = peel_start[f], ns1 = peel_start[f + 1];
+      if (ns1 == ns0) continue;
+      std::vector<int> dg;
+      const int w = poly_layout(ped, f, par->denovo ? 10 : 3, steps.data() + ns0, ns1 - ns0, poly_lay, dg);
+      if (w < 0) { E->es_poly = false; break; }
+      std::copy(dg.begin(), dg.end(), poly_deg.begin() + (size_t)ns0 * 4);
+      poly_w = std::max(poly_w, w);
+      for (int c = 0; c < 4; c++) poly_d = std::max(poly_d, poly_lay[poly_start[f] + 2 + c]);
+    }
+    poly_start[ped->n_fam] = (int)poly_lay.size();
     const int T = E->T;
     E->max_ext = (E->n_ext + T - 1) / T;
     std::vector<int> ext_count(T, 0), ext_fam((size_t)std::max(1, E->max_ext) * T, -1);
@@ -2465,19 +2744,34 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
         E->grid1 = E->n_cu * std::max(1, 1024 / E->T1);
       }
     }
+    // polynomial form: per lane the peel workspace (reused family by family) and each ES family's D + 1
+    // coefficients + D, kept for the item's evaluations
+    if (E->es_poly) {
+      E->poly_dcap = poly_d + 2;
+      E->poly_coef = poly_w;
+      E->poly_ws = poly_w + std::max({E->max_ext, E->max_ext1, 1}) * E->poly_dcap;
+      DALLOC(E->d_poly_start, poly_start.size());
+      DALLOC(E->d_poly_lay, std::max<size_t>(1, poly_lay.size()));
+      DALLOC(E->d_poly_deg, std::max<size_t>(1, poly_deg.size()));
+      HIP_TRY(hipMemcpy(E->d_poly_start, poly_start.data(), sizeof(int) * poly_start.size(), hipMemcpyHostToDevice));
+      if (!poly_lay.empty()) HIP_TRY(hipMemcpy(E->d_poly_lay, poly_lay.data(), sizeof(int) * poly_lay.size(), hipMemcpyHostToDevice));
+      if (!poly_deg.empty()) HIP_TRY(hipMemcpy(E->d_poly_deg, poly_deg.data(), sizeof(int) * poly_deg.size(), hipMemcpyHostToDevice));
+    }
     // workspace: the Brent grids and the posterior grid are capped so each needs <= 1 GiB
     E->grid_post = E->n_cu * 8;
     if (wsmax > 0) {
       const size_t cap = (size_t)1 << 30, per_lane = (size_t)wsmax * sizeof(double);
-      E->grid_brent = (int)std::max<size_t>(E->n_cu, std::min<size_t>(E->grid_brent, cap / (per_lane * T)));
+      const size_t per_lane_b = (size_t)std::max(wsmax, E->es_poly ? E->poly_ws : 0) * sizeof(double);   // Brent grids
+      E->grid_brent = (int)std::max<size_t>(E->n_cu, std::min<size_t>(E->grid_brent, cap / (per_lane_b * T)));
       E->grid_brent -= E->grid_brent % 8;   // keep the XCD-aware item order exact
       if (E->T1) {
-        E->grid1 = (int)std::max<size_t>(E->n_cu, std::min<size_t>(E->grid1, cap / (per_lane * E->T1)));
+        E->grid1 = (int)std::max<size_t>(E->n_cu, std::min<size_t>(E->grid1, cap / (per_lane_b * E->T1)));
         E->grid1 -= E->grid1 % 8;
       }
       E->grid_post = (int)std::max<size_t>(E->n_cu, std::min<size_t>(E->grid_post, cap / (per_lane * 256)));
-      const size_t lanes = std::max({(size_t)E->grid_brent * T, (size_t)E->grid1 * E->T1, (size_t)E->grid_post * 256});
-      DALLOC(E->d_ws, lanes * wsmax);
+      const size_t words = std::max({(size_t)E->grid_brent * T * (per_lane_b / sizeof(double)),
+                                     (size_t)E->grid1 * E->T1 * (per_lane_b / sizeof(double)), (size_t)E->grid_post * 256 * wsmax});
+      DALLOC(E->d_ws, words);
     }
   }
   // --- --quick_call: the unrelated plan (all persons in <=3-person founder chunks)
@@ -2573,6 +2867,9 @@ static DevArgs make_args(pm_engine* E, int n, const uint8_t* pl, const uint32_t*
   A.fam_founders = E->d_fam_founders; A.is_founder = E->d_is_founder; A.peel_start = E->d_peel_start; A.steps = E->d_steps;
   A.ext_count = E->n_ext ? E->d_ext_count : nullptr; A.ext_fam = E->d_ext_fam;
   A.T10 = E->d_T10; A.T10dn = E->d_T10dn; A.ws = E->d_ws; A.ws_per_lane = E->ws_per_lane;
+  A.es_poly = 0;   // set per Brent launch (launch_brent)
+  A.poly_start = E->d_poly_start; A.poly_lay = E->d_poly_lay; A.poly_deg = E->d_poly_deg;
+  A.poly_coef = E->poly_coef; A.poly_dcap = E->poly_dcap;
   A.theta_one = 1.0;
   A.unrelated = E->par.quick_call ? 1 : 0;   // k_prep: route sites through the quick pre-filter first
   A.vcf = E->vcf ? 1 : 0;
@@ -2604,8 +2901,14 @@ static DevArgs make_args(pm_engine* E, int n, const uint8_t* pl, const uint32_t*
 typedef void (*BrentFn)(DevArgs, int);
 // numerics: PM_NUM_PRODUCT / PM_NUM_EXACT for every flavour; PM_NUM_POLY only for the lean kernel
 // (the generic and ES flavours fall back to PRODUCT numerics).
-static BrentFn brent_kernel(int T, int S, int num, bool gen, bool es, bool dn = false, bool pf = false) {
+static BrentFn brent_kernel(int T, int S, int num, bool gen, bool es, bool dn = false, bool pf = false, bool ep = false) {
   const int n = (num == PM_NUM_POLY && gen) ? PM_NUM_PRODUCT : num;
+  if (es && ep) {   // extended families in polynomial form (PM_NUM_POLY)
+#define PMKEP(t, s) if (T == t && S == s) return k_brent<t, s, PM_NUM_PRODUCT, true, true, false, false, true>;
+    PMKEP(64, 1) PMKEP(64, 2) PMKEP(64, 4) PMKEP(64, 8) PMKEP(256, 1) PMKEP(256, 4) PMKEP(512, 4) PMKEP(1024, 4) PMKEP(1024, 8)
+#undef PMKEP
+    return nullptr;
+  }
   if (dn && !gen && !es && n == PM_NUM_POLY && pf && T == 64 && S == 16)   // lean --denovo, LDS-staged hoisting only
     return k_brent<64, 16, PM_NUM_POLY, false, false, true, true>;
   if (pf && !dn) {   // lean autosomal kernel with LDS plane prefetch
@@ -2629,7 +2932,7 @@ static BrentFn brent_kernel(int T, int S, int num, bool gen, bool es, bool dn = 
 #define PMKE(t, s) \
   if (T == t && S == s) return n == PM_NUM_EXACT ? k_brent<t, s, PM_NUM_EXACT, true, true> : k_brent<t, s, PM_NUM_PRODUCT, true, true>;
   if (es) {
-    PMKE(64, 1) PMKE(64, 2) PMKE(64, 4) PMKE(64, 8) PMKE(256, 4) PMKE(512, 4) PMKE(1024, 4) PMKE(1024, 8)
+    PMKE(64, 1) PMKE(64, 2) PMKE(64, 4) PMKE(64, 8) PMKE(256, 1) PMKE(256, 4) PMKE(512, 4) PMKE(1024, 4) PMKE(1024, 8)
     return nullptr;
   }
   PMK(64, 1) PMK(64, 2) PMK(64, 4) PMK(128, 4) PMK(256, 4) PMK(512, 2) PMK(512, 4) PMK(1024, 1) PMK(1024, 2)
@@ -2667,7 +2970,8 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
     A.dn_pf = 1;
     shmem = (size_t)(T / 64) * 2 * DN_PF_BUF;
   }
-  BrentFn fn = brent_kernel(T, S, E->par.numerics, gen, !unrelated && n_ext > 0, A.denovo != 0, A.pf_npad > 0 || A.dn_pf);
+  const bool ep = !unrelated && n_ext > 0 && E->es_poly && E->par.numerics == PM_NUM_POLY;
+  BrentFn fn = brent_kernel(T, S, E->par.numerics, gen, !unrelated && n_ext > 0, A.denovo != 0, A.pf_npad > 0 || A.dn_pf, ep);
   if (!fn) { pm_set_last_error("launch_brent: no kernel variant for the lane plan"); return PM_EINVAL; }
   // multi-wave de novo plans (T = 512 / 1024: more than 1024 families) stage 2 buffers per wave: above the
   // default 64 KB dynamic-LDS limit the kernel must opt in, and the block (plus its static LDS: lane plan,
@@ -2682,7 +2986,10 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
   // Elston-Stewart workspace in LDS: every partial / marriage-partial access of the peel becomes an LDS round
   // trip instead of an L2 one.  Blocks per CU follow from the LDS budget (160 KB per CU).
   A.ws_lds = 0;
-  if (!unrelated && n_ext > 0 && !E->par.denovo) {   // BA peels (the 10-state one is too big)
+  if (ep) {   // polynomial-form peels (HBM workspace)
+    A.es_poly = 1;
+    A.ws_per_lane = std::max(E->ws_per_lane, E->poly_ws);
+  } else if (!unrelated && n_ext > 0 && !E->par.denovo) {   // BA peels (the 10-state one is too big)
     const size_t need = (size_t)E->ws_per_lane * T * sizeof(double);
     if (need > 0 && need <= 150 * 1024) {
       if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)need) == hipSuccess) {

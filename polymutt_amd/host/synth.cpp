@@ -83,14 +83,15 @@ bool synth_shape(const std::string& shape, int fam, std::vector<SynthMember>& ou
 
 // shape "<template>+dn": additionally plants a de novo het call (ref/transition) in one non-founder
 // of one family at ~3% of sites, so the --denovo output path has records to check.  "+late": the first
-// half of the sites are monomorphic (a site shard whose range emits nothing).  Files only: the device
+// half of the sites are monomorphic (a site shard whose range emits nothing).  "+multi": three sections.  Files only: the device
 // generator (bench) does neither.
 int synth_write_dataset(const std::string& dir, const std::string& shape_arg, int nfam, int nsites, uint64_t seed,
                         std::string& err) {
   std::string shape = shape_arg;
-  bool plant = false, late = false;
+  bool plant = false, late = false, multi = false;
   for (bool more = true; more;) {
     more = false;
+    if (shape.size() > 6 && shape.compare(shape.size() - 6, 6, "+multi") == 0) { multi = more = true; shape.resize(shape.size() - 6); }
     if (shape.size() > 3 && shape.compare(shape.size() - 3, 3, "+dn") == 0) { plant = more = true; shape.resize(shape.size() - 3); }
     if (shape.size() > 5 && shape.compare(shape.size() - 5, 5, "+late") == 0) { late = more = true; shape.resize(shape.size() - 5); }
   }
@@ -127,11 +128,10 @@ int synth_write_dataset(const std::string& dir, const std::string& shape_arg, in
       FILE* fh = fopen((dir + "/p" + std::to_string(g + 1) + ".glf").c_str(), "wb");
       if (!fh) { err = "cannot create GLF file"; return -1; }
       glf[g] = fh;
-      // header: "GLF\3", u32 0; section: i32 labelLen=2, "1\0", i32 maxPosition
+      // header: "GLF\3", u32 0 (sections follow: i32 labelLen incl. NUL, label, i32 maxPosition, records, end)
       const char magic[4] = {'G', 'L', 'F', 3};
       uint32_t zero = 0;
-      int32_t ll = 2, mp = nsites;
-      fwrite(magic, 1, 4, fh); fwrite(&zero, 4, 1, fh); fwrite(&ll, 4, 1, fh); fwrite("1", 1, 2, fh); fwrite(&mp, 4, 1, fh);
+      fwrite(magic, 1, 4, fh); fwrite(&zero, 4, 1, fh);
       g++;
     }
   }
@@ -140,10 +140,18 @@ int synth_write_dataset(const std::string& dir, const std::string& shape_arg, in
   std::vector<uint8_t> pl, hap;
   std::vector<uint32_t> dm;
   static const uint8_t iupac[5] = {0, 1, 2, 4, 8};
-  for (int s = 0; s < nsites; s++) {
+  // "+multi": sections "1", "X", "2" (nsites each; the site stream continues across them)
+  const std::vector<std::string> labels = multi ? std::vector<std::string>{"1", "X", "2"} : std::vector<std::string>{"1"};
+  for (size_t sec = 0; sec < labels.size(); sec++) {
+  for (auto fh : glf) {
+    const int32_t ll = (int32_t)labels[sec].size() + 1, mp = nsites;
+    fwrite(&ll, 4, 1, fh); fwrite(labels[sec].c_str(), 1, ll, fh); fwrite(&mp, 4, 1, fh);
+  }
+  for (int s0 = 0; s0 < nsites; s0++) {
+    const int s = (int)sec * nsites + s0;
     int ref; double af;
     pm_syn_site(seed, (uint64_t)s, &ref, &af);
-    if (late && s < nsites / 2) af = 0.0;   // "+late": no polymorphism in the first half of the section
+    if (late && s0 < nsites / 2) af = 0.0;   // "+late": no polymorphism in the first half of the section
     for (int f = 0; f < nfam; f++) {
       const auto& F = fams[f];
       int n = (int)F.size();
@@ -176,7 +184,9 @@ int synth_write_dataset(const std::string& dir, const std::string& shape_arg, in
       }
     }
   }
-  for (auto fh : glf) { uint8_t end = 0; fwrite(&end, 1, 1, fh); fclose(fh); }
+  for (auto fh : glf) { uint8_t end = 0; fwrite(&end, 1, 1, fh); }
+  }
+  for (auto fh : glf) fclose(fh);
   return 0;
 }
 

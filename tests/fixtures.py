@@ -13,6 +13,14 @@ import polymutt_amd as pm
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SYNTH = os.path.join(ROOT, "tests", "golden", "synth")
 CASES = json.load(open(os.path.join(SYNTH, "cases.json")))
+# cases with one section and no --pos: also compared site by site against the reference's --dump_sites records
+DUMP_CASES = sorted(n for n, c in CASES.items() if not c.get("cli_only"))
+
+
+def summary_block(stdout):
+    """The section-summary lines a run prints (main.cpp:596-619), as make_golden.py keeps them."""
+    return [l for l in stdout.splitlines() if l.startswith(("Summary of", "Total ", "Non-Poly", "Transi", "Transv",
+                                                             "Other ", "Filter", "\t", "Hard ", "Skipped"))]
 
 LLK_RTOL = 1e-9
 FREQ_ATOL = 1e-6
@@ -22,6 +30,9 @@ FLAT_RTOL = 1e-12
 def make_dataset(name, directory):
     c = CASES[name]
     pm.synth_write_dataset(directory, c["shape"], c["families"], c["sites"], c["seed"])
+    if "pos" in c:   # the --pos file the reference read
+        with open(os.path.join(directory, "pos.txt"), "w") as fh:
+            fh.write("".join(f"{l} {p}\n" for l, p in c["pos"]))
     return c
 
 
@@ -49,7 +60,7 @@ _FLAG_PARAMS = {"--theta": ("theta", float), "--poly_tstv": ("poly_tstv", float)
                 "--maxDepth": ("max_total_depth", int), "--minPercSampleWithData": ("min_ps", float),
                 "--minMapQuality": ("min_map_quality", int), "--rate_denovo": ("denovo_mut_rate", float),
                 "--tstv_denovo": ("denovo_tstv", float), "--minLLR_denovo": ("denovo_min_llr", float)}
-_FLAG_BOOL = {"--denovo": "denovo", "--all_sites": "all_sites", "--quick_call": "quick_call"}
+_FLAG_BOOL = {"--denovo": "denovo", "--all_sites": "all_sites", "--quick_call": "quick_call", "--gl_off": None}
 
 
 def params_and_chrom(flags, **extra):
@@ -58,7 +69,8 @@ def params_and_chrom(flags, **extra):
     while i < len(flags):
         f = flags[i]
         if f in _FLAG_BOOL:
-            kw[_FLAG_BOOL[f]] = 1
+            if _FLAG_BOOL[f]:   # (--gl_off only changes the VCF text)
+                kw[_FLAG_BOOL[f]] = 1
             i += 1
             continue
         v = flags[i + 1]

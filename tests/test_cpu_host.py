@@ -185,6 +185,10 @@ def _sharded_case(tmp_path, case):
         from fixtures import make_dataset
         make_dataset("quad_chrX", d)
         return d, ["-p", "test.ped", "-d", "test.dat", "-g", "test.gif", "--chrX", "1"]
+    if case in ("multi_all", "multi_chr2process"):   # three sections (1, X, 2): the exchange once per section
+        from fixtures import make_dataset
+        c = make_dataset(case, d)
+        return d, ["-p", "test.ped", "-d", "test.dat", "-g", "test.gif"] + c["flags"]
     if case == "late_chrX":   # shard 0 emits nothing: shard 1 must redo its first record with famlk[0] unseen
         pm.synth_write_dataset(d, "trio+late", 30, 400, 31)   # (trios: the last person is male, so the state matters)
         return d, ["-p", "test.ped", "-d", "test.dat", "-g", "test.gif", "--chrX", "1"]
@@ -192,7 +196,7 @@ def _sharded_case(tmp_path, case):
 
 
 @pytest.mark.parametrize("case,world", [("example", 2), ("ragged", 2), ("quad_chrX", 2), ("late_chrX", 2),
-                                        ("quad_chrX", 3)])
+                                        ("quad_chrX", 3), ("multi_all", 3), ("multi_chr2process", 2)])
 def test_sharded_driver_matches_one_process_gloo(cpu_driver, tmp_path, case, world):
     """The multi-process driver (polymutt_amd/launch.py: contiguous position range per rank, one exchange per
     section over gloo) on the CPU oracle writes the same VCF and section summaries as one process."""

@@ -10,7 +10,8 @@ import pytest
 
 import polymutt_amd as pm
 from conftest import EXAMPLE
-from fixtures import CASES, compare_to_dump, golden_dump, golden_vcf_body, make_dataset, params_and_chrom, read_dataset
+from fixtures import (CASES, DUMP_CASES, compare_to_dump, golden_dump, golden_vcf_body, make_dataset, params_and_chrom,
+                      read_dataset, summary_block)
 from oracle_binding import Oracle
 
 
@@ -39,7 +40,7 @@ def test_cpu_driver_reproduces_example_goldens(cpu_driver, tmp_path, args, golde
     assert got == exp
 
 
-@pytest.mark.parametrize("name", sorted(CASES))
+@pytest.mark.parametrize("name", DUMP_CASES)
 def test_oracle_matches_reference_dump(built, tmp_path, name):
     case = make_dataset(name, str(tmp_path))
     ped, secs, sha = read_dataset(str(tmp_path))
@@ -66,6 +67,8 @@ def test_cpu_driver_matches_reference_vcf(cpu_driver, tmp_path, name):
     assert len(got) == len(exp)
     diff = [i for i, (a, b) in enumerate(zip(got, exp)) if a != b]
     assert not diff, f"{len(diff)} lines differ; first:\n{got[diff[0]][:300]}\n{exp[diff[0]][:300]}"
+    if "summary" in case:   # sections, filters and --pos early return (main.cpp:593: no summary) as the reference printed
+        assert summary_block(r.stdout) == case["summary"]
 
 
 def test_cpu_driver_reproduces_vcf_input_golden(cpu_driver, tmp_path):

@@ -224,7 +224,7 @@ def test_headline_config_parity(built, denovo):
     assert st["sites"] == 1024 and st["called"] > 0
 
 
-@pytest.mark.parametrize("case", ["example", "quad_chrX", "late_chrX"])
+@pytest.mark.parametrize("case", ["example", "quad_chrX", "late_chrX", "multi_all"])
 def test_cli_two_shards_match_one_process(built, tmp_path, case):
     """polymutt_amd.launch with 2 ranks (here both on the one GPU, gloo for the per-section exchange; RCCL
     when each rank has its own GPU) writes the same VCF and section summaries as the one-process CLI."""

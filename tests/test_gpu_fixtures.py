@@ -8,7 +8,8 @@ import subprocess
 import pytest
 
 import polymutt_amd as pm
-from fixtures import CASES, compare_to_dump, golden_dump, golden_vcf_body, make_dataset, params_and_chrom, read_dataset
+from fixtures import (CASES, DUMP_CASES, compare_to_dump, golden_dump, golden_vcf_body, make_dataset, params_and_chrom,
+                      read_dataset, summary_block)
 from oracle_binding import Oracle
 from parity import compare_results
 
@@ -19,7 +20,7 @@ pytestmark = pytest.mark.gpu
 # extended pedigrees next to > 512 nuclear families): the lane plans and kernel instantiations the bench
 # selects for those shapes.  They run in the default numerics only (the oracle needs ~45 s for 200 ext10
 # --denovo) and in one batch per 128 sites like the rest.
-_DUMP_CASES = [(n, num) for n in sorted(CASES) for num in
+_DUMP_CASES = [(n, num) for n in DUMP_CASES for num in
                ([pm.NUM_POLY] if n.startswith("big_") else [pm.NUM_PRODUCT, pm.NUM_EXACT, pm.NUM_POLY])]
 
 
@@ -60,3 +61,5 @@ def test_cli_matches_reference_vcf(built, tmp_path, name, numerics):
     assert len(got) == len(exp)
     diff = [i for i, (a, b) in enumerate(zip(got, exp)) if a != b]
     assert not diff, f"{len(diff)} lines differ; first:\n{got[diff[0]][:300]}\n{exp[diff[0]][:300]}"
+    if "summary" in case:   # sections, filters and --pos early return (main.cpp:593: no summary) as the reference printed
+        assert summary_block(r.stdout) == case["summary"]

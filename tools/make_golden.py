@@ -30,7 +30,8 @@ sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "tests", "golden", "synth")
 PM_REF = os.path.join(ROOT, "oracle", "_ref", "pm_ref")
 
-# name: (shape, families, sites, seed, extra CLI flags)
+# name: (shape, families, sites, seed, extra CLI flags[, extras]); extras: {"pos": [[label, position], ...]} writes the
+# --pos file pos.txt; "cli_only": the case is checked through the CLI's VCF only (several sections or --pos)
 CASES = {
     "quad_auto": ("quad", 30, 400, 7, []),
     "trio_auto": ("trio", 30, 400, 11, []),
@@ -69,6 +70,15 @@ CASES = {
     # a few extended pedigrees next to > 512 nuclear families
     "big_quadext_600": ("quadext", 600, 256, 97, []),
     "big_quadext_600_denovo": ("quadext", 600, 200, 101, ["--denovo", "--rate_denovo", "1e-6"]),
+    # CLI surface of the site loop (main.cpp:286-308, :332-337, :593; OutputVCF's PL columns :1751-1830)
+    "quad_gl_off": ("quad", 20, 300, 113, ["--gl_off"]),
+    "quad_pos": ("quad", 20, 300, 127, ["--pos", "pos.txt"],
+                 {"pos": [["1", p] for p in range(5, 301, 13)], "cli_only": True}),
+    "quad_pos_missing": ("quad", 20, 300, 139, ["--pos", "pos.txt"],
+                         {"pos": [["1", p] for p in range(3, 301, 29)] + [["1", 5000], ["2", 7]], "cli_only": True}),
+    "multi_all": ("quad+multi", 20, 200, 131, [], {"cli_only": True}),
+    "multi_chr2process": ("trio+multi", 20, 200, 137, ["--chr2process", "2,X"], {"cli_only": True}),
+    "multi_chr2process_one": ("quad+multi", 20, 200, 149, ["--chr2process", "2"], {"cli_only": True}),
 }
 
 SITE_DUMP = np.dtype([("pos", "<i4"), ("ref", "<i4"), ("status", "<i4"), ("total_depth", "<i4"),
@@ -99,10 +109,14 @@ def block_sha256(directory):
 
 def make_case(name):
     import polymutt_amd as pm
-    shape, nfam, nsites, seed, flags = CASES[name]
+    shape, nfam, nsites, seed, flags = CASES[name][:5]
+    extras = CASES[name][5] if len(CASES[name]) > 5 else {}
     tmp = tempfile.mkdtemp(prefix="pm_gold_")
     try:
         pm.synth_write_dataset(tmp, shape, nfam, nsites, seed)
+        if "pos" in extras:
+            with open(os.path.join(tmp, "pos.txt"), "w") as fh:
+                fh.write("".join(f"{l} {p}\n" for l, p in extras["pos"]))
         cmd = [PM_REF, "-p", "test.ped", "-d", "test.dat", "-g", "test.gif", "--out_vcf", "out.vcf",
                "--dump_sites", "sites.bin"] + flags
         r = subprocess.run(cmd, cwd=tmp, capture_output=True, text=True, timeout=600)
@@ -117,9 +131,13 @@ def make_case(name):
             fh.write(("\n".join(body) + "\n").encode() if body else b"")
         summary = [l for l in r.stdout.splitlines() if l.strip() and not l.startswith("Analysis")
                    and "started" not in l and "ended" not in l and "Time" not in l]
-        return {"shape": shape, "families": nfam, "sites": nsites, "seed": seed, "flags": flags,
-                "block_sha256": block_sha256(tmp), "records": max(0, len(body) - 1),
-                "dumped_sites": int(len(dump))}
+        out = {"shape": shape, "families": nfam, "sites": nsites, "seed": seed, "flags": flags,
+               "block_sha256": block_sha256(tmp), "records": max(0, len(body) - 1), "dumped_sites": int(len(dump))}
+        out.update(extras)
+        if extras.get("cli_only"):   # the summary block the reference printed (wall-clock lines dropped)
+            out["summary"] = [l for l in r.stdout.splitlines() if l.startswith(("Summary of", "Total ", "Non-Poly", "Transi",
+                              "Transv", "Other ", "Filter", "\t", "Hard ", "Skipped"))]
+        return out
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 
