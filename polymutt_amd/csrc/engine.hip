@@ -101,6 +101,9 @@ struct DevArgs {
   const int* poly_lay;
   const int* poly_deg;
   int poly_coef, poly_dcap;
+  // posteriors of peeled families: one work item per (row, person) of es_pers[n_es_pers] = family << 8 | member
+  const int* es_pers;
+  int n_es_pers;
   int unrelated;           // --quick_call MakeUnrelated(): every family is all-founder
   double theta_one;        // 1.0 (opaque to the compiler; timing experiments only)
   int vcf;                 // vcf_mode: one (ref, alt) Brent per site, FamilyLikelihoodSeq_VCF family rules
@@ -458,6 +461,27 @@ __device__ __forceinline__ double d_es_lk(const DevArgs& A, int f, const uint8_t
 // Brent item on coefficient vectors; each objective evaluation is then one Horner pass over D + 1 non-negative
 // coefficients (no cancellation: relative error ~ (D + 2) ulp, the class of PM_NUM_POLY's nuclear quartics).
 // The reference-order numeric peel stays in d_es_lk (PM_NUM_PRODUCT / PM_NUM_EXACT, and the posteriors).
+// register tiles for the hoisting: a polynomial of degree <= PDM as PDM + 1 coefficients (zero above its degree)
+#define PDM 8
+__device__ __forceinline__ void pl_load(const double* ws, size_t st, int o, int d, double* r) {
+#pragma unroll
+  for (int a = 0; a <= PDM; a++) r[a] = a <= d ? ws[(size_t)(o + a) * st] : 0.0;
+}
+__device__ __forceinline__ void pl_store(double* ws, size_t st, int o, int d, const double* r) {
+#pragma unroll
+  for (int a = 0; a <= PDM; a++)
+    if (a <= d) ws[(size_t)(o + a) * st] = r[a];
+}
+__device__ __forceinline__ void pl_mul(const double* x, const double* y, double* r) {   // degrees summing to <= PDM
+#pragma unroll
+  for (int a = PDM; a >= 0; a--) {
+    double s = 0;
+#pragma unroll
+    for (int b = 0; b <= a; b++) s += x[b] * y[a - b];
+    r[a] = s;
+  }
+}
+
 template <int NS>
 __device__ __forceinline__ int es_poly_hoist(const DevArgs& A, int f, const uint8_t* pl, const double* lk, int g11, int g12,
                                              int g22, int chrom, double* ws, size_t st, double* out) {
@@ -505,7 +529,72 @@ __device__ __forceinline__ int es_poly_hoist(const DevArgs& A, int f, const uint
     const int slot = (S.y >> 8) & 255, create = (S.y >> 16) & 1, fa2mo = (S.y >> 17) & 1;
     const int dg = A.poly_deg[4 * s + chrom];
     const int da = dg & 127, db = (dg >> 7) & 127, dc = (dg >> 14) & 127, de = (dg >> 21) & 127;
-    if (type == 1) {   // offspring -> parents: M(i, j) *= sum_k T(i, j, k) P_off[k]   (da = deg P_off, db = deg M)
+    if (type == 1 && da == 0) {   // offspring with a constant partial (leaves): scalar sums, M scaled in place
+      const int off = from0, po = POFF(off), pc = PCAP(off), mo = MOFF(slot), mc = MCAP(slot);
+      const int csex = A.sex[p0 + off];
+      double pk[NS];
+#pragma unroll
+      for (int k = 0; k < NS; k++) pk[k] = WV(po + k * pc);
+      for (int i = 0; i < NS; i++)
+        for (int j = 0; j < NS; j++) {
+          double sum = 0;
+#pragma unroll
+          for (int k = 0; k < NS; k++) sum += ((NS == 3) ? d_tba(i, j, k, chrom, csex) : A.T10dn[(i * 10 + j) * 10 + k]) * pk[k];
+          const int e0 = mo + (i * NS + j) * mc;
+          if (create) WV(e0) = sum;
+          else
+            for (int a = 0; a <= db; a++) WV(e0 + a) *= sum;
+        }
+    } else if (NS == 3 && type == 1 && da + db <= PDM) {   // BA, register tiles
+      const int off = from0, po = POFF(off), pc = PCAP(off), mo = MOFF(slot), mc = MCAP(slot);
+      const int csex = A.sex[p0 + off];
+      double P[3][PDM + 1];
+#pragma unroll
+      for (int k = 0; k < 3; k++) pl_load(ws, st, po + k * pc, da, P[k]);
+      for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+          double S[PDM + 1], M[PDM + 1], R[PDM + 1];
+#pragma unroll
+          for (int a = 0; a <= PDM; a++) S[a] = 0.0;
+#pragma unroll
+          for (int k = 0; k < 3; k++) {
+            const double t = d_tba(i, j, k, chrom, csex);
+#pragma unroll
+            for (int a = 0; a <= PDM; a++) S[a] += t * P[k][a];
+          }
+          const int e0 = mo + (i * 3 + j) * mc;
+          if (create) { pl_store(ws, st, e0, da, S); continue; }
+          pl_load(ws, st, e0, db, M);
+          pl_mul(M, S, R);
+          pl_store(ws, st, e0, da + db, R);
+        }
+    } else if (NS == 3 && type == 2 && da + db + dc <= PDM) {   // BA, register tiles
+      const int sf = from0, stt = to0, fo_ = POFF(sf), fc = PCAP(sf), to_ = POFF(stt), tc = PCAP(stt);
+      const int mo = slot == 255 ? 0 : MOFF(slot), mc = slot == 255 ? 0 : MCAP(slot);
+      double P[3][PDM + 1];
+#pragma unroll
+      for (int j = 0; j < 3; j++) pl_load(ws, st, fo_ + j * fc, da, P[j]);
+      for (int i = 0; i < 3; i++) {
+        double S[PDM + 1], M[PDM + 1], R[PDM + 1];
+#pragma unroll
+        for (int a = 0; a <= PDM; a++) S[a] = 0.0;
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+          if (slot == 255) {
+#pragma unroll
+            for (int a = 0; a <= PDM; a++) S[a] += P[j][a];
+          } else {
+            pl_load(ws, st, mo + (fa2mo ? j * 3 + i : i * 3 + j) * mc, db, M);
+            pl_mul(P[j], M, R);
+#pragma unroll
+            for (int a = 0; a <= PDM; a++) S[a] += R[a];
+          }
+        }
+        pl_load(ws, st, to_ + i * tc, dc, M);
+        pl_mul(M, S, R);
+        pl_store(ws, st, to_ + i * tc, da + db + dc, R);
+      }
+    } else if (type == 1) {   // offspring -> parents: M(i, j) *= sum_k T(i, j, k) P_off[k]   (da = deg P_off, db = deg M)
       const int off = from0, po = POFF(off), pc = PCAP(off), mo = MOFF(slot), mc = MCAP(slot);
       const int csex = A.sex[p0 + off];
       if (create)
@@ -1969,37 +2058,7 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
         }
         continue;
       }
-      if (ES && (kind == PM_FAM_EXTENDED || (A.nuc_es && kind == PM_FAM_NUCLEAR))) {   // CalcPostProb_SingleExtendedPed_BA :171-216 / _denovo :140-169
-        double* wsl = A.ws + gid_base;
-        const size_t st = stride;
-        for (int j = 0; j < n; j++) {
-          const int p = p0 + j, sx = A.sex[p];
-          if (!dn) {
-            if (chrom == PM_CHR_Y && sx == FEMALE) {
-              const double z[3] = {0, 0, 0};
-              d_emit_call(out + p, z, 0, PM_LBL_DOT, 0.0);
-              continue;
-            }
-            const double l11 = d_es_lk<3>(A, f, pl, s_lk, g11, g12, g22, chrom, freq, j, g11, wsl, st);
-            const double l12 = d_es_lk<3>(A, f, pl, s_lk, g11, g12, g22, chrom, freq, j, g12, wsl, st);
-            const double l22 = d_es_lk<3>(A, f, pl, s_lk, g11, g12, g22, chrom, freq, j, g22, wsl, st);
-            const double sum = l11 + l12 + l22;
-            double post[3] = {0, 0, 0};
-            if (sum != 0) { post[0] = l11 / sum; post[1] = l12 / sum; post[2] = l22 / sum; }
-            d_emit_call(out + p, post, d_best3(l11, l12, l22), d_vcf_label(chrom, sx), post[1] + post[2] * 2);
-          } else {
-            double lkv[10], sum = 0.0;
-            for (int k = 0; k < 10; k++) lkv[k] = d_es_lk<10>(A, f, pl, s_lk, g11, g12, g22, chrom, freq, j, k, wsl, st);
-            for (int k = 0; k < 10; k++) sum += lkv[k];
-            double post[10];
-            for (int k = 0; k < 10; k++) post[k] = (sum == 0) ? 0 : lkv[k] / sum;
-            int b = 0; double mx = 0.0;
-            for (int k = 0; k < 10; k++) if (mx < lkv[k]) { mx = lkv[k]; b = k; }
-            d_emit_call(out + p, post, b, PM_LBL_GENO10, 0.0);
-          }
-        }
-        continue;
-      }
+      if (ES && (kind == PM_FAM_EXTENDED || (A.nuc_es && kind == PM_FAM_NUCLEAR))) continue;   // k_posterior_es
       if (kind != PM_FAM_NUCLEAR) continue;
       // CalcParentMarginal(_denovo) at freq
       ItemCtx I;
@@ -2140,6 +2199,57 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
 // CalculateAB (:1006-1039) for emitted autosomal non-de-novo sites: wave per row, per-person terms in
 // parallel, the two sums reduced as lane partials + butterfly.  The reference sums in person order; the
 // reordering changes AB by ~1e-16 relative (AB is printed with %.3f; parity tolerance 1e-9).
+// CalcPostProb_SingleExtendedPed_BA (FamilyLikelihoodSeq.cpp:171-216) / _denovo (:140-169) for the peeled
+// families: one thread per (row, person), three (or ten) FillZeroPenetrance peels (:327-356) of the person's
+// family at the site's frequency, in the reference's operation order (d_es_lk).  Splitting the families'
+// persons over threads gives ten times the parallelism of a thread per (row, family).
+template <bool DN>
+__global__ void __launch_bounds__(256) k_posterior_es(DevArgs A) {
+  __shared__ double s_lk[256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) s_lk[i] = A.lktab[i];
+  __syncthreads();
+  const long long work = (long long)A.counts[3] * A.n_es_pers;
+  const size_t gid_base = (size_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (size_t)gridDim.x * blockDim.x;
+  double* wsl = A.ws + gid_base;
+  for (long long gid = (long long)gid_base; gid < work; gid += (long long)stride) {
+    const int row = (int)(gid / A.n_es_pers), e = A.es_pers[gid % A.n_es_pers];
+    const int f = e >> 8, j = e & 255;
+    const int site = A.row_site[row];
+    const pm_site_result* R = A.res + site;
+    const int np = A.n_person;
+    const uint8_t* pl = A.pl + (size_t)site * np * 10;
+    pm_geno_call* out = A.calls + (size_t)row * np;
+    const int a1 = R->allele1, a2 = R->allele2;
+    const int g11 = d_gi(a1, a1), g12 = d_gi(a1, a2), g22 = d_gi(a2, a2);
+    const int chrom = A.chrom;
+    const double freq = (R->maxidx == 0) ? (DN ? 1.0 : 1 - A.theta) : R->af;   // main.cpp:576-587
+    const int p = A.fam_start[f] + j, sx = A.sex[p];
+    if (!DN) {
+      if (chrom == PM_CHR_Y && sx == FEMALE) {
+        const double z[3] = {0, 0, 0};
+        d_emit_call(out + p, z, 0, PM_LBL_DOT, 0.0);
+        continue;
+      }
+      const double l11 = d_es_lk<3>(A, f, pl, s_lk, g11, g12, g22, chrom, freq, j, g11, wsl, stride);
+      const double l12 = d_es_lk<3>(A, f, pl, s_lk, g11, g12, g22, chrom, freq, j, g12, wsl, stride);
+      const double l22 = d_es_lk<3>(A, f, pl, s_lk, g11, g12, g22, chrom, freq, j, g22, wsl, stride);
+      const double sum = l11 + l12 + l22;
+      double post[3] = {0, 0, 0};
+      if (sum != 0) { post[0] = l11 / sum; post[1] = l12 / sum; post[2] = l22 / sum; }
+      d_emit_call(out + p, post, d_best3(l11, l12, l22), d_vcf_label(chrom, sx), post[1] + post[2] * 2);
+    } else {
+      double lkv[10], sum = 0.0;
+      for (int k = 0; k < 10; k++) lkv[k] = d_es_lk<10>(A, f, pl, s_lk, g11, g12, g22, chrom, freq, j, k, wsl, stride);
+      for (int k = 0; k < 10; k++) sum += lkv[k];
+      double post[10];
+      for (int k = 0; k < 10; k++) post[k] = (sum == 0) ? 0 : lkv[k] / sum;
+      int b = 0; double mx = 0.0;
+      for (int k = 0; k < 10; k++) if (mx < lkv[k]) { mx = lkv[k]; b = k; }
+      d_emit_call(out + p, post, b, PM_LBL_GENO10, 0.0);
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) k_ab(DevArgs A) {
   __shared__ double s_lk[256];
   for (int i = threadIdx.x; i < 256; i += blockDim.x) s_lk[i] = A.lktab[i];
@@ -2295,6 +2405,8 @@ struct pm_engine {
   bool es_poly = false;
   int poly_ws = 0, poly_coef = 0, poly_dcap = 0;
   int *d_poly_start = nullptr, *d_poly_lay = nullptr, *d_poly_deg = nullptr;
+  int *d_es_pers = nullptr, *d_es_pers1 = nullptr;   // (family << 8 | member) of peeled families: plan 0 / plan 1
+  int n_es_pers = 0, n_es_pers1 = 0;
   // vcf_mode on chrX/Y/MT or with a single family: nuclear families go through ES peeling as well
   // (FamilyLikelihoodSeq_VCF.cpp:97-103), so a second lane plan with them in the per-lane ES lists
   bool vcf = false, plan1_ok = false, use_plan1 = false;
@@ -2520,7 +2632,7 @@ void pm_engine_destroy(pm_engine* E) {
   if (!E) return;
   hipSetDevice(E->device);
   void* bufs[] = {E->d_units1, E->d_ext_count1, E->d_ext_fam1, E->d_fam_founders, E->d_peel_start, E->d_ext_count, E->d_ext_fam, E->d_is_founder, E->d_steps, E->d_T10,
-                  E->d_T10dn, E->d_ws, E->d_units_q, E->d_poly_start, E->d_poly_lay, E->d_poly_deg,
+                  E->d_T10dn, E->d_ws, E->d_units_q, E->d_poly_start, E->d_poly_lay, E->d_poly_deg, E->d_es_pers, E->d_es_pers1,
                   E->d_fam_start, E->d_fam_kind, E->d_fa, E->d_mo, E->d_sex, E->d_units, E->d_lktab, E->d_M, E->d_syn,
                   E->d_pl, E->d_stage, E->d_ref, E->d_dm, E->d_res, E->d_calls, E->d_raw, E->d_minv, E->d_mono, E->d_evals,
                   E->d_items[0], E->d_items[1], E->d_items[2], E->d_counts, E->d_eval_total, E->d_row_site,
@@ -2695,6 +2807,22 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
     int q = 0;
     for (int f = 0; f < ped->n_fam; f++)
       if (ped->fam_kind[f] == PM_FAM_EXTENDED) { const int lane = q % T; ext_fam[(size_t)ext_count[lane]++ * T + lane] = f; q++; }
+    {   // persons of the peeled families, for k_posterior_es: plan 0 (extended) and plan 1 (every family with offspring)
+      std::vector<int> e0, e1;
+      for (int f = 0; f < ped->n_fam; f++) {
+        const int n = ped->fam_start[f + 1] - ped->fam_start[f];
+        for (int j = 0; j < n && n <= 255; j++) {
+          if (ped->fam_kind[f] == PM_FAM_EXTENDED) e0.push_back(f << 8 | j);
+          if (ped->fam_kind[f] != PM_FAM_FOUNDERS) e1.push_back(f << 8 | j);
+        }
+      }
+      E->n_es_pers = (int)e0.size();
+      E->n_es_pers1 = (int)e1.size();
+      DALLOC(E->d_es_pers, std::max<size_t>(1, e0.size()));
+      DALLOC(E->d_es_pers1, std::max<size_t>(1, e1.size()));
+      if (!e0.empty()) HIP_TRY(hipMemcpy(E->d_es_pers, e0.data(), sizeof(int) * e0.size(), hipMemcpyHostToDevice));
+      if (!e1.empty()) HIP_TRY(hipMemcpy(E->d_es_pers1, e1.data(), sizeof(int) * e1.size(), hipMemcpyHostToDevice));
+    }
     std::vector<double> T10, T10dn;
     transmission_tables(E->M_h, T10, T10dn);
     DALLOC(E->d_fam_founders, ped->n_fam);
@@ -2870,6 +2998,8 @@ static DevArgs make_args(pm_engine* E, int n, const uint8_t* pl, const uint32_t*
   A.es_poly = 0;   // set per Brent launch (launch_brent)
   A.poly_start = E->d_poly_start; A.poly_lay = E->d_poly_lay; A.poly_deg = E->d_poly_deg;
   A.poly_coef = E->poly_coef; A.poly_dcap = E->poly_dcap;
+  A.es_pers = E->use_plan1 ? E->d_es_pers1 : E->d_es_pers;
+  A.n_es_pers = E->use_plan1 ? E->n_es_pers1 : E->n_es_pers;
   A.theta_one = 1.0;
   A.unrelated = E->par.quick_call ? 1 : 0;   // k_prep: route sites through the quick pre-filter first
   A.vcf = E->vcf ? 1 : 0;
@@ -3068,6 +3198,10 @@ static int run_pipeline(pm_engine* E, int n, const uint8_t* pl, const uint32_t* 
     void (*post)(DevArgs) = E->par.denovo ? (es ? k_posterior<true, true> : k_posterior<true, false>)
                           : es ? k_posterior<false, true> : lean ? k_posterior<false, false, true> : k_posterior<false, false>;
     hipLaunchKernelGGL(post, dim3(E->grid_post), dim3(256), 0, E->stream, A);
+    if (es && A.n_es_pers > 0) {
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(E->par.denovo ? k_posterior_es<true> : k_posterior_es<false>, dim3(E->grid_post), dim3(256), 0, E->stream, A);
+    }
   }
   HIP_TRY(hipGetLastError());
   if (!E->par.denovo && E->chrom == PM_CHR_AUTO && !E->vcf) {
