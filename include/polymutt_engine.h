@@ -160,6 +160,16 @@ typedef struct {
   int8_t  _pad[3];
 } pm_geno_call;
 
+/* vcf_mode genotype row entry (FamilyLikelihoodSeq_VCF::OutputVCF prints GT/GQ only): the device rows of a
+ * vcf_mode engine (pm_engine_run_device's d_calls) use this 4-byte layout; pm_engine_run expands them into
+ * pm_geno_call rows with dosage 0. */
+typedef struct {
+  int8_t best;
+  int8_t gq;
+  int8_t label;                /* pm_label_kind */
+  int8_t pad;
+} pm_vcf_call;
+
 /* Summary counters of one section (main.cpp:264-282, printed :596-619); summed over shards/GPUs. */
 typedef struct {
   int64_t ref_base_counts[5];

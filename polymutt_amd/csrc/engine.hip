@@ -707,6 +707,29 @@ __device__ __forceinline__ double es_poly_eval(const double* c, size_t st, int D
   return acc * p;
 }
 
+// es_poly_eval on register-resident coefficients (c[a] = 0 above D <= PDM): the leading zeros leave the Horner
+// sum's bits unchanged (0 * t + c = c)
+#define PM_EPE 4   // extended families per lane whose coefficients stay in registers through an item's evaluations
+__device__ __forceinline__ double es_poly_eval_r(const double* c, int D, double x) {
+  const double g = 1 - x;
+  double acc = 0.0, base;
+  if (x <= 0.5) {
+    const double t = x / g;
+#pragma unroll
+    for (int a = PDM; a >= 0; a--) acc = acc * t + c[a];
+    base = g;
+  } else {
+    const double sr = g / x;
+#pragma unroll
+    for (int a = 0; a <= PDM; a++) acc = a <= D ? acc * sr + c[a] : acc;
+    base = x;
+  }
+  double p = 1.0;
+#pragma unroll
+  for (int a = 0; a < PDM; a++) p = a < D ? p * base : p;
+  return acc * p;
+}
+
 template <int T>
 __device__ __forceinline__ double block_sum(double x, double* red, int& par) {
 #pragma unroll
@@ -1441,15 +1464,28 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
     // (two pointers, so each inlined peel keeps a known address space: ds_* or global_* accesses, no flat)
     double* wsl = ES ? A.ws + (size_t)blockIdx.x * A.ws_per_lane * T + threadIdx.x : nullptr;
     double* wsl_lds = ES ? (double*)s_pf + threadIdx.x : nullptr;
+    // EP: the first PM_EPE families' coefficients in registers for the item's evaluations (ed < 0: none or D > PDM)
+    // (one-wave plans only: at 256 lanes the cache spills, and those plans hold one family per lane anyway)
+    constexpr int EPE = (EP && T == 64) ? PM_EPE : 0;
+    double ce[EPE ? EPE : 1][EPE ? PDM + 1 : 1];
+    int ed[EPE ? EPE : 1];
     if constexpr (ES && EP) {   // polynomial form: the lane's extended families peeled once per item (es_poly_hoist)
-      if (A.ext_count)
-        for (int q = 0; q < A.ext_count[threadIdx.x]; q++) {
-          const int f = A.ext_fam[q * T + threadIdx.x];
-          double* co = wsl + (size_t)(A.poly_coef + q * A.poly_dcap) * T;
-          const int D = I.denovo ? es_poly_hoist<10>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, wsl, T, co)
-                                 : es_poly_hoist<3>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, wsl, T, co);
-          co[(size_t)(A.poly_dcap - 1) * T] = (double)D;
-        }
+      const int cnt = A.ext_count ? A.ext_count[threadIdx.x] : 0;
+      for (int q = 0; q < cnt; q++) {
+        const int f = A.ext_fam[q * T + threadIdx.x];
+        double* co = wsl + (size_t)(A.poly_coef + q * A.poly_dcap) * T;
+        const int D = I.denovo ? es_poly_hoist<10>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, wsl, T, co)
+                               : es_poly_hoist<3>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, wsl, T, co);
+        co[(size_t)(A.poly_dcap - 1) * T] = (double)D;
+      }
+#pragma unroll
+      for (int q = 0; q < EPE; q++) {
+        const double* co = wsl + (size_t)(A.poly_coef + q * A.poly_dcap) * T;
+        ed[q] = q < cnt ? (int)co[(size_t)(A.poly_dcap - 1) * T] : -1;
+        if (ed[q] > PDM) ed[q] = -1;
+#pragma unroll
+        for (int a = 0; a <= PDM; a++) ce[q][a] = a <= ed[q] ? co[(size_t)a * T] : 0.0;
+      }
     }
     const bool single = !A.vcf && ((cfg == 0) || (A.single_nuclear && !A.unrelated));
     // One evaluation site for the objective: the three bracketing evaluations of OptimizeFrequency
@@ -1479,11 +1515,23 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
       } else if (PROD) {
         double m; int e;
         lane_prod<S, GEN>(x, unit, (const double(*)[9])cond, fl, pmode, m, e);
+        if constexpr (ES && EP && EPE > 0) {   // register-resident coefficients first (independent Horner chains)
+#pragma unroll
+          for (int q = 0; q < EPE; q++)
+            if (ed[q] >= 0) {
+              int e1, e2;
+              const double mv = frexp(es_poly_eval_r(ce[q], ed[q], x), &e1);
+              m = frexp(m * mv, &e2);
+              e += e1 + e2;
+            }
+        }
         if (ES && A.ext_count)   // extended families of this lane: Elston-Stewart peeling per evaluation
           for (int q = 0; q < A.ext_count[threadIdx.x]; q++) {
             const int f = A.ext_fam[q * T + threadIdx.x];
             double v;
             if constexpr (EP) {
+              if constexpr (EPE > 0)
+                if (q < EPE && ed[q] >= 0) continue;   // (evaluated from registers above)
               const double* co = wsl + (size_t)(A.poly_coef + q * A.poly_dcap) * T;
               v = es_poly_eval(co, T, (int)co[(size_t)(A.poly_dcap - 1) * T], x);
             } else {
@@ -1933,13 +1981,37 @@ __device__ __forceinline__ int8_t d_vcf_label(int chrom, int membersex) {
   if (chrom == PM_CHR_X && membersex == MALE) return PM_LBL_VCF_HAPLOID;
   return PM_LBL_VCF_DIPLOID;
 }
-__device__ __forceinline__ void d_emit_call(pm_geno_call* C, const double* post, int best, int8_t label, double dosage) {
+// GQ = (pb > 0.9999999999) ? 100 : int(-10 log10(1 - pb) + 0.5) (OutputVCF :1818-1820) without a log10: the
+// host derives, with glibc's log10 in that very expression, the smallest q = 1 - pb giving GQ <= k for every
+// k (c_gq_thr[k], decreasing in k); a float log10 guesses k and at most a step or two against the thresholds
+// makes it exact.  Identical to the reference's glibc result for every double pb.
+__constant__ double c_gq_thr[101];
+__device__ __forceinline__ int d_gq(double pb) {
+  if (pb > 0.9999999999) return 100;
+  const double q = 1. - pb;
+  int k = (int)(-10.0f * __log10f((float)q) + 0.5f);
+  k = k < 0 ? 0 : k > 100 ? 100 : k;
+  while (k < 100 && q < c_gq_thr[k]) k++;
+  while (k > 0 && q >= c_gq_thr[k - 1]) k--;
+  return k;
+}
+
+// one person's genotype row entry: pm_geno_call (16 B), or in vcf_mode the 4-B pm_vcf_call (best, GQ, label:
+// FamilyLikelihoodSeq_VCF::OutputVCF prints no dosage), a quarter of the bytes of the row stream
+__device__ __forceinline__ void d_emit_call(const DevArgs& A, size_t idx, const double* post, int best, int8_t label,
+                                            double dosage) {
   const double pb = post[best];
-  const int gq = (pb > 0.9999999999) ? 100 : (int)(-10. * log10(1. - pb) + 0.5);   // OutputVCF :1818-1820
+  const int gq = d_gq(pb);
+  if (A.vcf) {
+    pm_vcf_call c;
+    c.best = (int8_t)best; c.gq = (int8_t)gq; c.label = label; c.pad = 0;
+    ((pm_vcf_call*)A.calls)[idx] = c;
+    return;
+  }
   pm_geno_call c;
   c.dosage = dosage; c.best = (int16_t)best; c.gq = (int16_t)gq; c.label = label;
   c._pad[0] = c._pad[1] = c._pad[2] = 0;
-  *C = c;
+  A.calls[idx] = c;
 }
 
 // likelihoodKidGenotype, :1334-1443
@@ -2023,7 +2095,7 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
     const pm_site_result* R = A.res + site;
     const int np = A.n_person;
     const uint8_t* pl = A.pl + (size_t)site * np * 10;
-    pm_geno_call* out = A.calls + (size_t)row * np;
+    const size_t out = (size_t)row * np;   // genotype row index base
     const int a1 = R->allele1, a2 = R->allele2;
     const int g11 = d_gi(a1, a1), g12 = d_gi(a1, a2), g22 = d_gi(a2, a2);
     const int chrom = LEAN ? (int)PM_CHR_AUTO : A.chrom;
@@ -2054,7 +2126,7 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
           const int best = d_best3(m11, m12, m22);
           // label: own sex (non-de-novo sets member sex first); de novo leaves it stale (0)
           const int8_t lab = yf ? PM_LBL_DOT : d_vcf_label(chrom, dn ? 0 : sx);
-          d_emit_call(out + p, post, best, lab, post[1] + post[2] * 2);
+          d_emit_call(A, out + p, post, best, lab, post[1] + post[2] * 2);
         }
         continue;
       }
@@ -2095,7 +2167,7 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
           if (sum != 0) { post[0] = q11 / sum; post[1] = q12 / sum; post[2] = q22 / sum; }
           const int best = d_best3(q11, q12, q22);
           const int8_t lab = dn ? (int8_t)PM_LBL_ALLELES : ((chrom == PM_CHR_Y && sx == FEMALE) ? (int8_t)PM_LBL_DOT : d_vcf_label(chrom, sx));
-          d_emit_call(out + p, post, best, lab, post[1] + post[2] * 2);
+          d_emit_call(A, out + p, post, best, lab, post[1] + post[2] * 2);
         } else if (!dn && chrom == PM_CHR_AUTO && n <= 4) {   // KidJointGenoLikelihood :798-835, autosomal, <= 2 kids
           // d_kid_geno's autosomal branches with every kid's three likelihoods loaded once and k unrolled; the
           // products run over the kids in the same order from 1.0, so the values are d_kid_geno's bit for bit
@@ -2132,7 +2204,7 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
           const double sum = g[0] + g[1] + g[2];
           double post[3] = {0, 0, 0};
           if (sum != 0.0) { post[0] = g[0] / sum; post[1] = g[1] / sum; post[2] = g[2] / sum; }
-          d_emit_call(out + p, post, d_best3(post[0], post[1], post[2]), d_vcf_label(chrom, sx), post[1] + post[2] * 2);
+          d_emit_call(A, out + p, post, d_best3(post[0], post[1], post[2]), d_vcf_label(chrom, sx), post[1] + post[2] * 2);
         } else if (LEAN) {   // (every nuclear family has <= 4 persons: the branch above took them)
         } else if (!dn) {   // KidJointGenoLikelihood :798-835
           double J[9][3];
@@ -2148,7 +2220,7 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
           if (sum != 0.0) { post[0] = g[0] / sum; post[1] = g[1] / sum; post[2] = g[2] / sum; }
           const int best = d_best3(post[0], post[1], post[2]);
           const int8_t lab = (chrom == PM_CHR_Y && sx == FEMALE) ? (int8_t)PM_LBL_DOT : d_vcf_label(chrom, sx);
-          d_emit_call(out + p, post, best, lab, post[1] + post[2] * 2);
+          d_emit_call(A, out + p, post, best, lab, post[1] + post[2] * 2);
         } else {   // KidJointGenoLikelihood_denovo :838-868
           double gsum[10];
           for (int t = 0; t < 10; t++) gsum[t] = 0.0;
@@ -2189,7 +2261,7 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
           for (int t = 0; t < 10; t++) post[t] = (sum == 0.0) ? 0.0 : gsum[t] / sum;
           int best = 0; double mx = 0.0;
           for (int t = 0; t < 10; t++) if (mx < post[t]) { mx = post[t]; best = t; }
-          d_emit_call(out + p, post, best, PM_LBL_GENO10, 0.0);
+          d_emit_call(A, out + p, post, best, PM_LBL_GENO10, 0.0);
         }
       }
     }
@@ -2218,7 +2290,7 @@ __global__ void __launch_bounds__(256) k_posterior_es(DevArgs A) {
     const pm_site_result* R = A.res + site;
     const int np = A.n_person;
     const uint8_t* pl = A.pl + (size_t)site * np * 10;
-    pm_geno_call* out = A.calls + (size_t)row * np;
+    const size_t out = (size_t)row * np;   // genotype row index base
     const int a1 = R->allele1, a2 = R->allele2;
     const int g11 = d_gi(a1, a1), g12 = d_gi(a1, a2), g22 = d_gi(a2, a2);
     const int chrom = A.chrom;
@@ -2227,7 +2299,7 @@ __global__ void __launch_bounds__(256) k_posterior_es(DevArgs A) {
     if (!DN) {
       if (chrom == PM_CHR_Y && sx == FEMALE) {
         const double z[3] = {0, 0, 0};
-        d_emit_call(out + p, z, 0, PM_LBL_DOT, 0.0);
+        d_emit_call(A, out + p, z, 0, PM_LBL_DOT, 0.0);
         continue;
       }
       const double l11 = d_es_lk<3>(A, f, pl, s_lk, g11, g12, g22, chrom, freq, j, g11, wsl, stride);
@@ -2236,7 +2308,7 @@ __global__ void __launch_bounds__(256) k_posterior_es(DevArgs A) {
       const double sum = l11 + l12 + l22;
       double post[3] = {0, 0, 0};
       if (sum != 0) { post[0] = l11 / sum; post[1] = l12 / sum; post[2] = l22 / sum; }
-      d_emit_call(out + p, post, d_best3(l11, l12, l22), d_vcf_label(chrom, sx), post[1] + post[2] * 2);
+      d_emit_call(A, out + p, post, d_best3(l11, l12, l22), d_vcf_label(chrom, sx), post[1] + post[2] * 2);
     } else {
       double lkv[10], sum = 0.0;
       for (int k = 0; k < 10; k++) lkv[k] = d_es_lk<10>(A, f, pl, s_lk, g11, g12, g22, chrom, freq, j, k, wsl, stride);
@@ -2245,7 +2317,7 @@ __global__ void __launch_bounds__(256) k_posterior_es(DevArgs A) {
       for (int k = 0; k < 10; k++) post[k] = (sum == 0) ? 0 : lkv[k] / sum;
       int b = 0; double mx = 0.0;
       for (int k = 0; k < 10; k++) if (mx < lkv[k]) { mx = lkv[k]; b = k; }
-      d_emit_call(out + p, post, b, PM_LBL_GENO10, 0.0);
+      d_emit_call(A, out + p, post, b, PM_LBL_GENO10, 0.0);
     }
   }
 }
@@ -2715,8 +2787,10 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
                        ped->n_person >= 16 && !getenv("PM_NO_PREFETCH");
     const int2* pref = gen ? generic : dn_lean ? (dn_pf ? lean_dn_pf : lean_dn) : lean;
     // extended families are the expensive terms: spread them one per lane up to 256 lanes
+    // (polynomial form: up to PM_EPE families per lane, their coefficients in registers, one wave per item)
+    const int per_lane = (par->numerics == PM_NUM_POLY && !par->denovo) ? PM_EPE : 1;   // (10-state hoisting: one per lane)
     int tmin = 1;
-    while (tmin < std::min(E->n_ext, 256)) tmin *= 2;
+    while (tmin < std::min((E->n_ext + per_lane - 1) / per_lane, 256)) tmin *= 2;
     const int npref = gen ? 9 : 8;
     for (int i = 0; i < npref && !planned; i++)
       if (pref[i].x >= tmin && plan_units(ped, pref[i].x, pref[i].y, units)) { E->T = pref[i].x; E->S = pref[i].y; planned = true; }
@@ -2842,6 +2916,22 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
     HIP_TRY(hipMemcpy(E->d_T10, T10.data(), sizeof(double) * 1000, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(E->d_T10dn, T10dn.data(), sizeof(double) * 1000, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_TBA), kTBA, sizeof(kTBA)));
+    {   // GQ thresholds (d_gq): smallest double q in (0, 1] with int(-10 log10(q) + 0.5) <= k, by bisection on the
+        // bit patterns of positive doubles (ordered like their values), with the host's glibc log10
+      double thr[101];
+      auto gq_of = [](double q) { return (int)(-10. * log10(q) + 0.5); };
+      for (int k = 0; k <= 100; k++) {
+        uint64_t lo = 1, hi = 0x3FF0000000000000ull;   // gq_of(hi = 1.0) = 0 <= k; search the first bit pattern with gq <= k
+        while (lo < hi) {
+          const uint64_t mid = lo + (hi - lo) / 2;
+          double q;
+          memcpy(&q, &mid, 8);
+          if (gq_of(q) <= k) hi = mid; else lo = mid + 1;
+        }
+        memcpy(&thr[k], &lo, 8);
+      }
+      HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_gq_thr), thr, sizeof(thr)));
+    }
     // vcf_mode plan 1: nuclear families peeled too (chrX/Y/MT sections, or a single family)
     if (E->plan1_ok) {
       int n1 = 0;
@@ -3274,8 +3364,19 @@ int pm_engine_run(pm_engine* E, int32_t n, const uint8_t* pl, const uint32_t* dm
   int counts[16];
   HIP_TRY(hipMemcpy(counts, E->d_counts, sizeof(counts), hipMemcpyDeviceToHost));
   *n_rows = counts[3];
-  if (calls && counts[3] > 0)
-    HIP_TRY(hipMemcpy(calls, E->d_calls, sizeof(pm_geno_call) * np * counts[3], hipMemcpyDeviceToHost));
+  if (calls && counts[3] > 0) {
+    if (E->vcf) {   // 4-B rows on the device (pm_vcf_call), expanded into the caller's pm_geno_call rows
+      const size_t nr = np * (size_t)counts[3];
+      std::vector<pm_vcf_call> v(nr);
+      HIP_TRY(hipMemcpy(v.data(), E->d_calls, sizeof(pm_vcf_call) * nr, hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < nr; i++) {
+        pm_geno_call c;
+        c.dosage = 0.0; c.best = v[i].best; c.gq = v[i].gq; c.label = v[i].label;
+        c._pad[0] = c._pad[1] = c._pad[2] = 0;
+        calls[i] = c;
+      }
+    } else HIP_TRY(hipMemcpy(calls, E->d_calls, sizeof(pm_geno_call) * np * counts[3], hipMemcpyDeviceToHost));
+  }
   return PM_OK;
 }
 

@@ -11,8 +11,9 @@ FLAT_RTOL = 1e-12    # |llk_engine - llk_oracle| / |llk| at which an objective c
 DOSE_ATOL = 1e-9
 
 
-def compare_results(eng, ora, ecalls, ocalls, label=""):
-    """Returns a dict of mismatch counts; raises AssertionError with details on any failure."""
+def compare_results(eng, ora, ecalls, ocalls, label="", dosage=True):
+    """Returns a dict of mismatch counts; raises AssertionError with details on any failure.
+    dosage=False: vcf_mode rows carry no dosage (FamilyLikelihoodSeq_VCF::OutputVCF prints none)."""
     assert len(eng) == len(ora)
     problems = []
     for f in EXACT:
@@ -59,7 +60,7 @@ def compare_results(eng, ora, ecalls, ocalls, label=""):
         if len(bad):
             r, p = bad[0]
             problems.append(f"{label}calls.{f}: {len(bad)} differ; first row {r} person {p}: engine {ecalls[f][r, p]} oracle {ocalls[f][r, p]}")
-    d = np.abs(ecalls["dosage"] - ocalls["dosage"])
+    d = np.abs(ecalls["dosage"] - ocalls["dosage"]) if dosage else np.zeros(0)
     if d.size and (d > DOSE_ATOL).any():
         problems.append(f"{label}calls.dosage max abs err {d.max():.3g}")
     eval_mismatch = int(((eng["evals"] != ora["evals"]) & called[:, None]).any(axis=1).sum())

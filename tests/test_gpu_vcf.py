@@ -73,7 +73,7 @@ def test_engine_vcf_mode_config5_geometry(built, tmp_path, numerics):
     for s in range(0, len(ref), 256):
         e, ec = eng.run(pl[s:s + 256], zeros[s:s + 256], refalt[s:s + 256])
         o, oc = ora.run(pl[s:s + 256], zeros[s:s + 256], refalt[s:s + 256])
-        st = compare_results(e, o, ec, oc, label=f"cfg5[{s}] ")
+        st = compare_results(e, o, ec, oc, label=f"cfg5[{s}] ", dosage=False)
         assert st["emitted"] == st["called"] == len(e)
     eng.close()
 
@@ -106,6 +106,6 @@ def test_engine_vcf_mode_matches_oracle(built, tmp_path, shape, nfam, chrom, num
     for s in range(0, len(ref), 128):
         e, ec = eng.run(pl[s:s + 128], zeros[s:s + 128], refalt[s:s + 128])
         o, oc = ora.run(pl[s:s + 128], zeros[s:s + 128], refalt[s:s + 128])
-        st = compare_results(e, o, ec, oc, label=f"{shape}/{chrom}[{s}] ")
+        st = compare_results(e, o, ec, oc, label=f"{shape}/{chrom}[{s}] ", dosage=False)
         assert st["emitted"] == st["called"] == len(e)
     eng.close()
