@@ -2532,7 +2532,7 @@ static int dalloc(X** p, size_t count) {
 }
 #define DALLOC(p, n) do { int _r = dalloc(&(p), (n)); if (_r) { pm_engine_destroy(E); return _r; } } while (0)
 
-static const struct { int T, S; } kVariants[] = {{64, 1}, {64, 2}, {64, 4}, {128, 4}, {256, 1}, {256, 4}, {512, 2}, {512, 4},
+static const struct { int T, S; } kVariants[] = {{64, 1}, {64, 2}, {64, 4}, {128, 4}, {128, 16}, {256, 1}, {256, 4}, {512, 2}, {512, 4},
                                                  {1024, 1}, {1024, 2}, {1024, 4}, {1024, 8}, {128, 8}, {64, 8}, {64, 16}};
 
 // Deal families to lanes: family-major round robin; founders-only families are split into <=3-person chunks
@@ -2774,7 +2774,8 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
   // kernel on the same plan.
   {
     const bool gen = (par->denovo && par->numerics != PM_NUM_POLY) || E->has_fp || ped->n_fam == 1;
-    static const int2 lean[] = {{64, 1}, {64, 2}, {64, 4}, {64, 8}, {64, 16}, {512, 4}, {1024, 4}, {1024, 8}};
+    // (1025-2048 families: 2 waves x 16 slots, one two-wave exchange per evaluation, before 8 waves x 4)
+    static const int2 lean[] = {{64, 1}, {64, 2}, {64, 4}, {64, 8}, {64, 16}, {128, 16}, {1024, 4}, {1024, 8}};
     static const int2 generic[] = {{64, 1}, {64, 2}, {64, 4}, {64, 8}, {256, 1}, {256, 4}, {512, 4}, {1024, 4}, {1024, 8}};
     // lean --denovo: the de novo hoisting state does not fit 16 slots per lane without spilling; 8 slots on
     // 2 waves per item is faster (measured: 6.6 vs 6.1 M sites/s, 1000 quads)
@@ -3156,7 +3157,7 @@ static BrentFn brent_kernel(int T, int S, int num, bool gen, bool es, bool dn = 
     return nullptr;
   }
   PMK(64, 1) PMK(64, 2) PMK(64, 4) PMK(128, 4) PMK(256, 4) PMK(512, 2) PMK(512, 4) PMK(1024, 1) PMK(1024, 2)
-  PMK(1024, 4) PMK(1024, 8) PMK(128, 8) PMK(64, 8) PMK(64, 16)
+  PMK(1024, 4) PMK(1024, 8) PMK(128, 8) PMK(64, 8) PMK(64, 16) PMK(128, 16)
 #undef PMK
 #undef PMKE
   return nullptr;

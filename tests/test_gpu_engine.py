@@ -90,7 +90,7 @@ def test_cli_reproduces_reference_goldens(built, tmp_path, args, golden, numeric
 
 
 @pytest.mark.parametrize("shape,nfam,nsites", [("quad", 300, 600), ("trio", 200, 600), ("mixed", 101, 400),
-                                               ("single", 64, 300)])
+                                               ("single", 64, 300), ("quad", 1500, 160)])
 def test_synthetic_device_generator_and_parity(built, shape, nfam, nsites, tmp_path):
     d = str(tmp_path / shape)
     pm.synth_write_dataset(d, shape, nfam, nsites, 7)
@@ -119,6 +119,10 @@ def test_synthetic_device_generator_and_parity(built, shape, nfam, nsites, tmp_p
     eng.close()
     stats = _run_both(ped, pm.Params.defaults(), secs, batch=256)
     assert sum(s["called"] for s in stats) > 0
+    if nfam > 1024:   # 1025-2048 nuclear families: the two-wave 128 x 16 plan
+        eng = pm.Engine(ped.view, pm.Params.defaults(), max_batch=16)
+        assert eng.plan() == (128, 16)
+        eng.close()
 
 
 
