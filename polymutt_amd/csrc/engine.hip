@@ -568,6 +568,65 @@ __device__ __forceinline__ int es_poly_hoist(const DevArgs& A, int f, const uint
           pl_mul(M, S, R);
           pl_store(ws, st, e0, da + db, R);
         }
+    } else if (NS == 10 && type == 1 && da <= 2 && da + db <= PDM) {   // 10 states, register tiles (offspring degree <= 2)
+      const int off = from0, po = POFF(off), pc = PCAP(off), mo = MOFF(slot), mc = MCAP(slot);
+      double P[10][3];
+#pragma unroll
+      for (int k = 0; k < 10; k++)
+#pragma unroll
+        for (int a = 0; a < 3; a++) P[k][a] = a <= da ? WV(po + k * pc + a) : 0.0;
+      for (int i = 0; i < 10; i++)
+        for (int j = 0; j < 10; j++) {
+          double S[PDM + 1], M[PDM + 1], R[PDM + 1];
+#pragma unroll
+          for (int a = 0; a <= PDM; a++) S[a] = 0.0;
+#pragma unroll
+          for (int k = 0; k < 10; k++) {
+            const double t = A.T10dn[(i * 10 + j) * 10 + k];
+#pragma unroll
+            for (int a = 0; a < 3; a++) S[a] += t * P[k][a];
+          }
+          const int e0 = mo + (i * 10 + j) * mc;
+          if (create) { pl_store(ws, st, e0, da, S); continue; }
+          pl_load(ws, st, e0, db, M);
+          pl_mul(M, S, R);
+          pl_store(ws, st, e0, da + db, R);
+        }
+    } else if (NS == 10 && type == 2 && da <= 2 && da + db + dc <= PDM) {   // 10 states, register tiles (from degree <= 2)
+      const int sf = from0, stt = to0, fo_ = POFF(sf), fc = PCAP(sf), to_ = POFF(stt), tc = PCAP(stt);
+      const int mo = slot == 255 ? 0 : MOFF(slot), mc = slot == 255 ? 0 : MCAP(slot);
+      double P[10][3];
+#pragma unroll
+      for (int j = 0; j < 10; j++)
+#pragma unroll
+        for (int a = 0; a < 3; a++) P[j][a] = a <= da ? WV(fo_ + j * fc + a) : 0.0;
+      for (int i = 0; i < 10; i++) {
+        double S[PDM + 1], M[PDM + 1], R[PDM + 1];
+#pragma unroll
+        for (int a = 0; a <= PDM; a++) S[a] = 0.0;
+#pragma unroll
+        for (int j = 0; j < 10; j++) {
+          if (slot == 255) {
+#pragma unroll
+            for (int a = 0; a < 3; a++) S[a] += P[j][a];
+          } else {
+            pl_load(ws, st, mo + (fa2mo ? j * 10 + i : i * 10 + j) * mc, db, M);
+#pragma unroll
+            for (int a = 0; a <= PDM; a++) {   // R = P[j] (degree <= 2) x M
+              double acc = 0;
+#pragma unroll
+              for (int b = 0; b < 3; b++)
+                if (a - b >= 0) acc += P[j][b] * M[a - b];
+              R[a] = acc;
+            }
+#pragma unroll
+            for (int a = 0; a <= PDM; a++) S[a] += R[a];
+          }
+        }
+        pl_load(ws, st, to_ + i * tc, dc, M);
+        pl_mul(M, S, R);
+        pl_store(ws, st, to_ + i * tc, da + db + dc, R);
+      }
     } else if (NS == 3 && type == 2 && da + db + dc <= PDM) {   // BA, register tiles
       const int sf = from0, stt = to0, fo_ = POFF(sf), fc = PCAP(sf), to_ = POFF(stt), tc = PCAP(stt);
       const int mo = slot == 255 ? 0 : MOFF(slot), mc = slot == 255 ? 0 : MCAP(slot);
@@ -1474,8 +1533,10 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
       for (int q = 0; q < cnt; q++) {
         const int f = A.ext_fam[q * T + threadIdx.x];
         double* co = wsl + (size_t)(A.poly_coef + q * A.poly_dcap) * T;
-        const int D = I.denovo ? es_poly_hoist<10>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, wsl, T, co)
-                               : es_poly_hoist<3>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, wsl, T, co);
+        int D;   // (the 10-state hoisting is compiled into the --denovo instantiation only: DN)
+        if constexpr (DN) D = I.denovo ? es_poly_hoist<10>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, wsl, T, co)
+                                       : es_poly_hoist<3>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, wsl, T, co);
+        else D = es_poly_hoist<3>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, wsl, T, co);
         co[(size_t)(A.poly_dcap - 1) * T] = (double)D;
       }
 #pragma unroll
@@ -3124,8 +3185,9 @@ typedef void (*BrentFn)(DevArgs, int);
 // (the generic and ES flavours fall back to PRODUCT numerics).
 static BrentFn brent_kernel(int T, int S, int num, bool gen, bool es, bool dn = false, bool pf = false, bool ep = false) {
   const int n = (num == PM_NUM_POLY && gen) ? PM_NUM_PRODUCT : num;
-  if (es && ep) {   // extended families in polynomial form (PM_NUM_POLY)
-#define PMKEP(t, s) if (T == t && S == s) return k_brent<t, s, PM_NUM_PRODUCT, true, true, false, false, true>;
+  if (es && ep) {   // extended families in polynomial form (PM_NUM_POLY); DN: with the 10-state (--denovo) hoisting
+#define PMKEP(t, s) \
+  if (T == t && S == s) return dn ? k_brent<t, s, PM_NUM_PRODUCT, true, true, true, false, true> : k_brent<t, s, PM_NUM_PRODUCT, true, true, false, false, true>;
     PMKEP(64, 1) PMKEP(64, 2) PMKEP(64, 4) PMKEP(64, 8) PMKEP(256, 1) PMKEP(256, 4) PMKEP(512, 4) PMKEP(1024, 4) PMKEP(1024, 8)
 #undef PMKEP
     return nullptr;
