@@ -482,13 +482,15 @@ __device__ __forceinline__ void pl_mul(const double* x, const double* y, double*
   }
 }
 
+// top: only the f^D coefficient (the item is the de novo monomorphism, one evaluation at f = 1 where
+// L = c_D): every founder keeps just its top term and every step runs at degree 0 -- a numeric peel at f = 1.
 template <int NS>
 __device__ __forceinline__ int es_poly_hoist(const DevArgs& A, int f, const uint8_t* pl, const double* lk, int g11, int g12,
-                                             int g22, int chrom, double* ws, size_t st, double* out) {
+                                             int g22, int chrom, double* ws, size_t st, double* out, bool top = false) {
   const int p0 = A.fam_start[f], n = A.fam_start[f + 1] - p0, nf = A.fam_founders[f];
   const bool X = chrom == PM_CHR_X, Y = chrom == PM_CHR_Y, MT = chrom == PM_CHR_MT;
   const int* L = A.poly_lay + A.poly_start[f];
-  const int tof = L[1], D = L[2 + chrom];
+  const int tof = L[1], D = top ? 0 : L[2 + chrom];
   const size_t np = (size_t)A.n_person;
 #define WV(o) ws[(size_t)(o) * st]
 #define POFF(i) (L[6 + (i)] & 0xFFFFFF)
@@ -501,7 +503,8 @@ __device__ __forceinline__ int es_poly_hoist(const DevArgs& A, int f, const uint
     const uint8_t* R = pl + p0 + i;
     const int o = POFF(i), cap = PCAP(i);
     const bool yf = Y && sx == FEMALE;
-    const int d = !fo ? 0 : (Y && sx == FEMALE) ? 0 : ((X || Y) && sx == MALE) || MT ? 1 : 2;
+    const int dfull = !fo ? 0 : (Y && sx == FEMALE) ? 0 : ((X || Y) && sx == MALE) || MT ? 1 : 2;
+    const int d = top ? 0 : dfull;
     const int gidx[3] = {g11, g12, g22};
     for (int j = 0; j < NS; j++) {
       for (int a = 0; a <= d; a++) WV(o + j * cap + a) = 0.0;
@@ -509,6 +512,7 @@ __device__ __forceinline__ int es_poly_hoist(const DevArgs& A, int f, const uint
         const double pen = lk[R[gidx[j] * np]];
         if (yf) { WV(o + j * cap) = 1.0; continue; }   // BA chrY females: partial 1.0 (:1449-1465)
         if (!fo) { WV(o + j * cap) = pen; continue; }
+        if (top) { if (j == 0) WV(o + j * cap) = pen; continue; }       // the f^d term: f^2 or f
         if (d == 2) WV(o + j * cap + 2 - j) = j == 1 ? 2 * pen : pen;   // f^2, 2fg, g^2
         else if (j != 1) WV(o + j * cap + (j == 0 ? 1 : 0)) = pen;      // f, 0, g
       } else {
@@ -516,6 +520,7 @@ __device__ __forceinline__ int es_poly_hoist(const DevArgs& A, int f, const uint
         if (!fo) { WV(o + j * cap) = pen; continue; }
         const int q = j == g11 ? 0 : j == g12 ? 1 : j == g22 ? 2 : 3;
         if (q == 3) continue;
+        if (top && dfull > 0) { if (q == 0) WV(o + j * cap) = pen; continue; }   // the f^d term
         if (d == 2) WV(o + j * cap + 2 - q) = q == 1 ? 2 * pen : pen;
         else if (d == 1) { if (q != 1) WV(o + j * cap + (q == 0 ? 1 : 0)) = pen; }
         else WV(o + j * cap) = pen;   // chrY female founder: q = 1, 1, 1
@@ -527,7 +532,7 @@ __device__ __forceinline__ int es_poly_hoist(const DevArgs& A, int f, const uint
     const int2 S = A.steps[s];
     const int type = S.x & 255, from0 = (S.x >> 8) & 255, from1 = (S.x >> 16) & 255, to0 = (S.x >> 24) & 255;
     const int slot = (S.y >> 8) & 255, create = (S.y >> 16) & 1, fa2mo = (S.y >> 17) & 1;
-    const int dg = A.poly_deg[4 * s + chrom];
+    const int dg = top ? 0 : A.poly_deg[4 * s + chrom];
     const int da = dg & 127, db = (dg >> 7) & 127, dc = (dg >> 14) & 127, de = (dg >> 21) & 127;
     if (type == 1 && da == 0) {   // offspring with a constant partial (leaves): scalar sums, M scaled in place
       const int off = from0, po = POFF(off), pc = PCAP(off), mo = MOFF(slot), mc = MCAP(slot);
@@ -1534,8 +1539,9 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
         const int f = A.ext_fam[q * T + threadIdx.x];
         double* co = wsl + (size_t)(A.poly_coef + q * A.poly_dcap) * T;
         int D;   // (the 10-state hoisting is compiled into the --denovo instantiation only: DN)
-        if constexpr (DN) D = I.denovo ? es_poly_hoist<10>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, wsl, T, co)
-                                       : es_poly_hoist<3>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, wsl, T, co);
+        const bool top = cfg == 0 && !A.vcf;   // the de novo monomorphism item: one evaluation at f = 1
+        if constexpr (DN) D = I.denovo ? es_poly_hoist<10>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, wsl, T, co, top)
+                                       : es_poly_hoist<3>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, wsl, T, co, top);
         else D = es_poly_hoist<3>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, wsl, T, co);
         co[(size_t)(A.poly_dcap - 1) * T] = (double)D;
       }
