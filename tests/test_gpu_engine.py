@@ -3,6 +3,8 @@ golden VCFs.  Marked gpu; run on an MI355X with `pytest -m gpu`."""
 import os
 import subprocess
 
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -273,3 +275,55 @@ def test_posterior_carry_matches_oracle(built, tmp_path):
         dos.append(ec["dosage"][0].copy())
         eng.close()
     assert (dos[0] != dos[1]).any()   # the first record's posteriors depend on the state
+
+
+@pytest.mark.parametrize("denovo", [0, 1])
+def test_headline_full_batch_properties(built, denovo):
+    """BASELINE config 3 at the bench's full batch (1000 quads x 262 144 sites, HBM-resident, k_synth), where
+    the oracle cannot follow: size-independent properties.  The same sites in one batch and in four batches
+    of 65 536 give bitwise-identical per-site results and section counters (no state leaks between sites or
+    batches); every site is called and counted once; the emitted sites are exactly the non-hom-ref calls."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    ped = bench.nuclear_pedigree(pm, 1000, 2)
+    B, np_ = 262144, ped.n_person
+    params = pm.Params.defaults(denovo=denovo)
+    big = pm.Engine(ped, params, max_batch=B)
+    d_pl, d_dm, d_ref = big.alloc(B * np_ * 10), big.alloc(B * np_ * 4), big.alloc(B)
+    big.synth(B, 7, 0, d_pl, d_dm, d_ref)
+    rsz = pm.engine.SITE_DTYPE.itemsize
+    d_res = big.alloc(B * rsz)
+    big.run_device(B, d_pl, d_dm, d_ref, d_res, None)
+    big.sync()
+    r_big = np.zeros(B, pm.engine.SITE_DTYPE)
+    big.to_host(r_big, d_res, B * rsz)
+    c_big = big.counters().as_array()
+    small = pm.Engine(ped, params, max_batch=B // 4)
+    r_small = np.zeros(B, pm.engine.SITE_DTYPE)
+    for k in range(4):   # the same device block, a quarter at a time (planar: site s at s * 10 * n_person)
+        off = k * (B // 4)
+        sub = lambda p, w: C.c_void_p(p.value + off * w)
+        part = np.zeros(B // 4, pm.engine.SITE_DTYPE)
+        d_r2 = small.alloc((B // 4) * rsz)
+        small.run_device(B // 4, sub(d_pl, np_ * 10), sub(d_dm, np_ * 4), sub(d_ref, 1), d_r2, None)
+        small.sync()
+        small.to_host(part, d_r2, (B // 4) * rsz)
+        small.free(d_r2)
+        r_small[off:off + B // 4] = part
+    c_small = small.counters().as_array()
+    for e, p in ((big, (d_pl, d_dm, d_ref, d_res)), (small, ())):
+        for x in p:
+            e.free(x)
+    big.close()
+    small.close()
+    keep = [f for f in pm.engine.SITE_DTYPE.names if f != "call_row"]   # row numbers restart per batch
+    assert all((r_big[f] == r_small[f]).all() for f in keep)
+    assert (c_big == c_small).all()
+    assert (r_big["status"] == 0).all() and int(c_big[:5].sum()) == B
+    # main.cpp:520-553: every site lands in exactly one filter count or one of homoRef / ts / tv / other / nocall
+    assert int(c_big[5:16].sum()) == B
+    emitted = r_big["emit"] != 0
+    if not denovo:   # records: the polymorphic calls past the posterior cutoff, one per ts / tv / other count
+        assert (r_big["maxidx"][emitted] >= 1).all()
+        assert int(emitted.sum()) == int(c_big[10:15].sum())
