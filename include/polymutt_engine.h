@@ -247,7 +247,8 @@ int pm_copy_to_device(pm_engine *eng, void *d_dst, const void *h_src, uint64_t b
 typedef struct {
   int64_t launches;      /* k_brent launches */
   double  kernel_ms;     /* summed k_brent time (HIP events on the engine stream) */
-  int64_t evals;         /* objective evaluations by Brent items */
+  int64_t evals;         /* objective evaluations computed by Brent items (OptimizeFrequency's f(a) and f(c),
+                            which Brent never reads, are counted in pm_site_result.evals but not computed) */
   int64_t fam_evals;     /* evals x families */
   int64_t items;         /* (site, configuration) work items evaluated */
   int64_t sites;         /* sites processed */

@@ -1232,7 +1232,9 @@ __device__ __forceinline__ void hoist_poly4_dn_pf(const DevArgs& A, const int* s
       if (u != 0) live |= 1u << (c0 + j);
       const uint8_t* W = cur + j * 10 * DN_PF_WIN;   // plane g of this slot at W[g * DN_PF_WIN + person - start]
       const int rel = u ? unit_first(u) - start_al[c0 + j] : 0;
-      uint32_t par[6];
+      // every PL byte of the slot first (one LDS round trip), then every table lookup (a second), then the
+      // arithmetic: a byte -> lk[byte] -> fma chain per genotype costs two LDS latencies per term otherwise
+      uint32_t par[6], kb[2][10];
 #pragma unroll
       for (int q = 0; q < 2; q++) {
         const int pp = rel + (q < nn ? q : 0);
@@ -1240,23 +1242,36 @@ __device__ __forceinline__ void hoist_poly4_dn_pf(const DevArgs& A, const int* s
         par[3 * q + 1] = W[I.g12 * DN_PF_WIN + pp];
         par[3 * q + 2] = W[I.g22 * DN_PF_WIN + pp];
       }
+      const int dnv = I.denovo;   // uniform per item
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const int pk = rel + (q + 2 < nn ? q + 2 : 0);
+        if (dnv) {
+#pragma unroll
+          for (int g = 0; g < 10; g++) kb[q][g] = W[g * DN_PF_WIN + pk];
+        } else {   // cfg-7 items: likelihoodONEKid's autosomal terms need the item's three planes only
+          kb[q][0] = W[I.g11 * DN_PF_WIN + pk]; kb[q][1] = W[I.g12 * DN_PF_WIN + pk]; kb[q][2] = W[I.g22 * DN_PF_WIN + pk];
+#pragma unroll
+          for (int g = 3; g < 10; g++) kb[q][g] = 0;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);   // (the scheduler would sink each byte read back into its chain)
       double kids[9];
 #pragma unroll
       for (int k = 0; k < 9; k++) kids[k] = 1.0;
 #pragma unroll
       for (int q = 0; q < 2; q++) {
-        const int pk = rel + (q + 2 < nn ? q + 2 : 0);
         double D11 = 0.0, D12 = 0.0, D22 = 0.0;
-        if (I.denovo) {   // uniform per item
+        if (dnv) {
 #pragma unroll
           for (int g = 0; g < 10; g++) {
-            const double pg = lk[W[g * DN_PF_WIN + pk]];
+            const double pg = lk[kb[q][g]];
             D11 = fma(M[r11 + g], pg, D11);
             D12 = fma(M[r12 + g], pg, D12);
             D22 = fma(M[r22 + g], pg, D22);
           }
-        } else {   // cfg-7 items: likelihoodONEKid's autosomal terms
-          D11 = lk[W[I.g11 * DN_PF_WIN + pk]]; D12 = lk[W[I.g12 * DN_PF_WIN + pk]]; D22 = lk[W[I.g22 * DN_PF_WIN + pk]];
+        } else {
+          D11 = lk[kb[q][0]]; D12 = lk[kb[q][1]]; D22 = lk[kb[q][2]];
         }
         const bool isKid = q + 2 < nn;
 #pragma unroll
@@ -1353,9 +1368,16 @@ __device__ __forceinline__ void lane_poly_r(double r, double g4, const double (*
 template <int CTRL, int ROWMASK>
 __device__ __forceinline__ void dpp_prod_step(double& m, int& e) {
   const int lo = __double2loint(m), hi = __double2hiint(m);
-  const int olo = __builtin_amdgcn_update_dpp(0, lo, CTRL, ROWMASK, 0xF, false);
-  const int ohi = __builtin_amdgcn_update_dpp(0x3FF00000, hi, CTRL, ROWMASK, 0xF, false);
-  const int oe = __builtin_amdgcn_update_dpp(0, e, CTRL, ROWMASK, 0xF, false);
+  int olo, ohi, oe;
+  if constexpr (ROWMASK == 0xF) {   // every row written: no identity `old` operand (saves its two v_mov per step)
+    olo = __builtin_amdgcn_mov_dpp(lo, CTRL, 0xF, 0xF, false);
+    ohi = __builtin_amdgcn_mov_dpp(hi, CTRL, 0xF, 0xF, false);
+    oe = __builtin_amdgcn_update_dpp(0, e, CTRL, ROWMASK, 0xF, false);   // (folds into one v_add_u32_dpp)
+  } else {
+    olo = __builtin_amdgcn_update_dpp(0, lo, CTRL, ROWMASK, 0xF, false);
+    ohi = __builtin_amdgcn_update_dpp(0x3FF00000, hi, CTRL, ROWMASK, 0xF, false);
+    oe = __builtin_amdgcn_update_dpp(0, e, CTRL, ROWMASK, 0xF, false);
+  }
   m = m * __hiloint2double(ohi, olo);   // no renormalisation: 64 factors in [1/16, 1) stay >= 2^-256
   e += oe;
 }
@@ -1560,8 +1582,12 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
     const double tol = A.precision;
     double a = 0.0001, b = 0.9999, c = 0.5;
     double mn = 0, fmin = 0, w = 0, v = 0, fw = 0, fv = 0, delta = 0.0, d = 0.0;
-    double x = single ? ((cfg == 0) ? 1.0 : 0.5) : a;   // MonomorphismLogLikelihood_denovo / single nuclear family at 0.5
-    int phase = 0, iter = 0, nev = 0;
+    // OptimizeFrequency (NucFamGenotypeLikelihood.cpp:432-441) evaluates fa = f(a), fb = f(b), fc = f(c) and
+    // calls Brent, which reads only fb (MathGold.cpp:85-93: a < c, so fa and fc are never swapped in or read).
+    // f(a) and f(c) are therefore counted (pm_site_result.evals keeps the reference's count) but not computed.
+    double x = single ? ((cfg == 0) ? 1.0 : 0.5) : b;   // MonomorphismLogLikelihood_denovo / single nuclear family at 0.5
+    int phase = single ? 0 : 1, iter = 0, nev = single ? 0 : 1;   // nev: f(a) counted
+    int skipped = single ? 0 : 2;
     bool ok = false;
     for (;;) {
       double tot;
@@ -1626,10 +1652,10 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
       nev++;
       if (single) { mn = 0.0; fmin = -tot; ok = true; break; }
       const double fx = -tot;
-      if (phase == 0) { phase = 1; x = b; continue; }
-      if (phase == 1) { fmin = fx; phase = 2; x = c; continue; }
-      if (phase == 2) { phase = 3; mn = b; w = b; v = b; fw = fmin; fv = fmin; }   // min = b, fmin = fb
-      else {
+      if (phase == 1) {   // fb; then f(c), counted only (see above); Brent: min = b, fmin = fb (MathGold.cpp:91-93)
+        fmin = fx; nev++;
+        phase = 3; mn = b; w = b; v = b; fw = fmin; fv = fmin;
+      } else {
         const double u = x, fu = fx;
         if (fu <= fmin) {
           if (u >= mn) a = mn; else c = mn;
@@ -1673,7 +1699,7 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
       raw[cfg] = -fmin;
       A.minv[site * 8 + cfg] = mn;
       A.evals[site * 8 + cfg] = nev;
-      if (!single) ev_acc += nev;
+      if (!single) ev_acc += nev - skipped;   // objective evaluations computed
       if (!ok) atomicExch(&A.counts[5], 1);
     }
   }

@@ -26,7 +26,16 @@ step trace 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/tra
 step trace1 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace1" -o run -- $BENCH --engines 1
 # BASELINE config 4 shape (200 ext10 pedigrees, Elston-Stewart peeling), one engine
 step trace_ext10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_ext10" -o run -- $BENCH --engines 1 --shape ext10 --families 200 --batch 16384 --no-denovo --steps 8
+# BASELINE config 5 shape (2000 mixed families, --in_vcf engine mode), one engine
+step trace_cfg5 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_cfg5" -o run -- $BENCH --engines 1 --shape mixed --families 2000 --vcf --no-denovo --batch 65536 --steps 12
 step pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- $BENCH --engines 1 --steps 4 --warmup 1 --calib-steps 0
 step pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- $BENCH --engines 1 --steps 4 --warmup 1 --calib-steps 0
 step pmc_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmc_sq" -o run -- $BENCH --engines 1 --steps 4 --warmup 1 --calib-steps 0
+# the other BASELINE configs' bench lines (default three engines)
+B="python3 $R/bench.py --no-cpu-baseline"
+step cfg2 300 $B --shape trio --families 1000 --no-denovo --steps 100
+step cfg4 300 $B --shape ext10 --families 200 --no-denovo --batch 16384 --steps 30
+step cfg4dn 300 $B --shape ext10 --families 200 --batch 4096 --steps 20
+step cfg5 300 $B --shape mixed --families 2000 --vcf --no-denovo --batch 65536 --steps 60
+step cfg3plain 300 $B --no-denovo --steps 200
 echo done >&2
