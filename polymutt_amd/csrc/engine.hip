@@ -1263,12 +1263,15 @@ __device__ __forceinline__ void hoist_poly4_dn_pf(const DevArgs& A, const int* s
       for (int q = 0; q < 2; q++) {
         double D11 = 0.0, D12 = 0.0, D22 = 0.0;
         if (dnv) {
+          double pg[10];   // the kid's ten table lookups in flight together
+#pragma unroll
+          for (int g = 0; g < 10; g++) pg[g] = lk[kb[q][g]];
+          __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int g = 0; g < 10; g++) {
-            const double pg = lk[kb[q][g]];
-            D11 = fma(M[r11 + g], pg, D11);
-            D12 = fma(M[r12 + g], pg, D12);
-            D22 = fma(M[r22 + g], pg, D22);
+            D11 = fma(M[r11 + g], pg[g], D11);
+            D12 = fma(M[r12 + g], pg[g], D12);
+            D22 = fma(M[r22 + g], pg[g], D22);
           }
         } else {
           D11 = lk[kb[q][0]]; D12 = lk[kb[q][1]]; D22 = lk[kb[q][2]];
