@@ -1259,23 +1259,33 @@ __device__ __forceinline__ void hoist_poly4_dn_pf(const DevArgs& A, const int* s
       double kids[9];
 #pragma unroll
       for (int k = 0; k < 9; k++) kids[k] = 1.0;
+      double DK[2][3];   // (D11, D12, D22) per kid
+      if (dnv) {
+        double pg[2][10];   // both kids' twenty table lookups in flight together
+#pragma unroll
+        for (int q = 0; q < 2; q++)
+#pragma unroll
+          for (int g = 0; g < 10; g++) pg[q][g] = lk[kb[q][g]];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 2; q++) DK[q][0] = DK[q][1] = DK[q][2] = 0.0;
+#pragma unroll
+        for (int g = 0; g < 10; g++) {   // each mutation-matrix entry read once for both kids (same per-kid order)
+          const double m11 = M[r11 + g], m12 = M[r12 + g], m22 = M[r22 + g];
+#pragma unroll
+          for (int q = 0; q < 2; q++) {
+            DK[q][0] = fma(m11, pg[q][g], DK[q][0]);
+            DK[q][1] = fma(m12, pg[q][g], DK[q][1]);
+            DK[q][2] = fma(m22, pg[q][g], DK[q][2]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 2; q++) { DK[q][0] = lk[kb[q][0]]; DK[q][1] = lk[kb[q][1]]; DK[q][2] = lk[kb[q][2]]; }
+      }
 #pragma unroll
       for (int q = 0; q < 2; q++) {
-        double D11 = 0.0, D12 = 0.0, D22 = 0.0;
-        if (dnv) {
-          double pg[10];   // the kid's ten table lookups in flight together
-#pragma unroll
-          for (int g = 0; g < 10; g++) pg[g] = lk[kb[q][g]];
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int g = 0; g < 10; g++) {
-            D11 = fma(M[r11 + g], pg[g], D11);
-            D12 = fma(M[r12 + g], pg[g], D12);
-            D22 = fma(M[r22 + g], pg[g], D22);
-          }
-        } else {
-          D11 = lk[kb[q][0]]; D12 = lk[kb[q][1]]; D22 = lk[kb[q][2]];
-        }
+        const double D11 = DK[q][0], D12 = DK[q][1], D22 = DK[q][2];
         const bool isKid = q + 2 < nn;
 #pragma unroll
         for (int k = 0; k < 9; k++) kids[k] *= isKid ? d_one_kid_dn(k, D11, D12, D22) : 1.0;
@@ -1406,14 +1416,21 @@ __device__ __forceinline__ void wave_prod(double& m, int& e) {
 // atanh series (truncation < 3e-17 relative).  Absolute error <= ~7e-17 (OCML's double-double log10:
 // ~3e-17), far below the ~1e-12 ulp of the objective it is added to; ~25 instructions instead of ~85.
 #define PM_INV_LN10 0x1.bcb7b1526e50ep-2
+__device__ __forceinline__ double sgpr_const(double c) {
+  asm volatile("" : "+s"(c));
+  return c;
+}
 __device__ __forceinline__ double log10_mant(double m, int e) {
   if (m == 0.0) return -INFINITY;   // an underflowed family product: log10(0), as the reference
   if (m < 0.70710678118654752440) { m *= 2.0; e -= 1; }
   const double t = (m - 1.0) / (m + 1.0);
   const double t2 = t * t;
-  double p = 2.0 / 21;
-  p = fma(p, t2, 2.0 / 19); p = fma(p, t2, 2.0 / 17); p = fma(p, t2, 2.0 / 15); p = fma(p, t2, 2.0 / 13);
-  p = fma(p, t2, 2.0 / 11); p = fma(p, t2, 2.0 / 9); p = fma(p, t2, 2.0 / 7); p = fma(p, t2, 2.0 / 5); p = fma(p, t2, 2.0 / 3);
+  // series coefficients as SGPR operands materialised at their use (otherwise the compiler keeps ten of
+  // them in VGPRs across the Brent loop, next to the 5 x S hoisted coefficients)
+  double p = sgpr_const(2.0 / 21);
+  p = fma(p, t2, sgpr_const(2.0 / 19)); p = fma(p, t2, sgpr_const(2.0 / 17)); p = fma(p, t2, sgpr_const(2.0 / 15));
+  p = fma(p, t2, sgpr_const(2.0 / 13)); p = fma(p, t2, sgpr_const(2.0 / 11)); p = fma(p, t2, sgpr_const(2.0 / 9));
+  p = fma(p, t2, sgpr_const(2.0 / 7)); p = fma(p, t2, sgpr_const(2.0 / 5)); p = fma(p, t2, sgpr_const(2.0 / 3));
   const double ln = fma(t * t2, p, 2.0 * t);
   const double de = (double)e;
   return ln * PM_INV_LN10 + (de * PM_LOG10_2_HI + de * PM_LOG10_2_LO);
