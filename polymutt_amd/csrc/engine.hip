@@ -2099,22 +2099,26 @@ __device__ __forceinline__ int8_t d_vcf_label(int chrom, int membersex) {
 // k (c_gq_thr[k], decreasing in k); a float log10 guesses k and at most a step or two against the thresholds
 // makes it exact.  Identical to the reference's glibc result for every double pb.
 __constant__ double c_gq_thr[101];
-__device__ __forceinline__ int d_gq(double pb) {
+// (thr: the block's LDS copy of c_gq_thr -- the lookups' index diverges, so they are not scalar loads)
+__device__ __forceinline__ int d_gq(double pb, const double* thr) {
   if (pb > 0.9999999999) return 100;
   const double q = 1. - pb;
   int k = (int)(-10.0f * __log10f((float)q) + 0.5f);
   k = k < 0 ? 0 : k > 100 ? 100 : k;
-  while (k < 100 && q < c_gq_thr[k]) k++;
-  while (k > 0 && q >= c_gq_thr[k - 1]) k--;
+  while (k < 100 && q < thr[k]) k++;
+  while (k > 0 && q >= thr[k - 1]) k--;
   return k;
+}
+__device__ __forceinline__ void load_gq_thr(double* s_gq) {
+  for (int i = threadIdx.x; i < 101; i += blockDim.x) s_gq[i] = c_gq_thr[i];
 }
 
 // one person's genotype row entry: pm_geno_call (16 B), or in vcf_mode the 4-B pm_vcf_call (best, GQ, label:
 // FamilyLikelihoodSeq_VCF::OutputVCF prints no dosage), a quarter of the bytes of the row stream
-__device__ __forceinline__ void d_emit_call(const DevArgs& A, size_t idx, const double* post, int best, int8_t label,
-                                            double dosage) {
+__device__ __forceinline__ void d_emit_call(const DevArgs& A, const double* s_gq, size_t idx, const double* post, int best,
+                                            int8_t label, double dosage) {
   const double pb = post[best];
-  const int gq = d_gq(pb);
+  const int gq = d_gq(pb, s_gq);
   if (A.vcf) {
     pm_vcf_call c;
     c.best = (int8_t)best; c.gq = (int8_t)gq; c.label = label; c.pad = 0;
@@ -2188,14 +2192,94 @@ __device__ void d_kid_geno(int chrom, const uint8_t* pl, int np, const double* l
   out[0] = G11; out[1] = G12; out[2] = G22;
 }
 
+// LEAN nuclear family (autosome, <= 4 persons, not de novo): every PL lookup of the family is issued first (one
+// memory round trip instead of one per stage), then the arithmetic of hoist_nuc, CalcParentMarginal and
+// KidJointGenoLikelihood below in the same operation order -- the same values bit for bit
+__device__ __forceinline__ void lean_nuc_post(const DevArgs& A, const double* s_lk, const double* s_gq, const uint8_t* pl,
+                                              size_t out, int p0, int n, int g11, int g12, int g22, double freq, int is_mono) {
+  const int np = A.n_person;
+  double lF[3], lM[3], kl[2][3];
+  lF[0] = s_lk[PLB(pl, np, p0, g11)]; lF[1] = s_lk[PLB(pl, np, p0, g12)]; lF[2] = s_lk[PLB(pl, np, p0, g22)];
+  lM[0] = s_lk[PLB(pl, np, p0 + 1, g11)]; lM[1] = s_lk[PLB(pl, np, p0 + 1, g12)]; lM[2] = s_lk[PLB(pl, np, p0 + 1, g22)];
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    const int pi = p0 + 2 + (2 + i < n ? i : 0);
+    kl[i][0] = s_lk[PLB(pl, np, pi, g11)]; kl[i][1] = s_lk[PLB(pl, np, pi, g12)]; kl[i][2] = s_lk[PLB(pl, np, pi, g22)];
+  }
+  double kids[9];
+#pragma unroll
+  for (int k = 0; k < 9; k++) kids[k] = 1.0;
+#pragma unroll
+  for (int i = 0; i < 2; i++) {   // hoist_nuc's kid loop, j = 2 .. n-1
+    if (2 + i >= n) break;
+#pragma unroll
+    for (int k = 0; k < 9; k++) kids[k] *= d_one_kid(k, PM_CHR_AUTO, 0, kl[i][0], kl[i][1], kl[i][2]);
+  }
+  double pp[9];
+  d_parent_prior((!A.n_fam_gt1 && !is_mono) ? PR_TRIO : PR_AUTO, freq, pp);
+  double m[9], wk[9];
+#pragma unroll
+  for (int a = 0; a < 3; a++)
+#pragma unroll
+    for (int b = 0; b < 3; b++) {
+      const double pg = lF[a] * lM[b];
+      m[3 * a + b] = (kids[3 * a + b] * pg) * pp[3 * a + b];   // cond[k] * pp[k]
+      wk[3 * a + b] = pg * pp[3 * a + b];
+    }
+#pragma unroll
+  for (int j = 0; j < 2; j++) {   // CalcPostProb parents
+    double q11, q12, q22;
+    if (j == 0) { q11 = m[0] + m[1] + m[2]; q12 = m[3] + m[4] + m[5]; q22 = m[6] + m[7] + m[8]; }
+    else { q11 = m[0] + m[3] + m[6]; q12 = m[1] + m[4] + m[7]; q22 = m[2] + m[5] + m[8]; }
+    const double sum = q11 + q12 + q22;
+    double post[3] = {0, 0, 0};
+    if (sum != 0) { post[0] = q11 / sum; post[1] = q12 / sum; post[2] = q22 / sum; }
+    d_emit_call(A, s_gq, out + p0 + j, post, d_best3(q11, q12, q22), PM_LBL_VCF_DIPLOID, post[1] + post[2] * 2);
+  }
+#pragma unroll
+  for (int j = 2; j < 4; j++) {   // KidJointGenoLikelihood :798-835, autosomal
+    if (j >= n) break;
+    double g[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      double G[3] = {1.0, 1.0, 1.0};
+#pragma unroll
+      for (int i = 0; i < 2; i++) {
+        if (2 + i >= n) break;
+        const double l11 = kl[i][0], l12 = kl[i][1], l22 = kl[i][2];
+        double l, q11, q12, q22;
+        switch (k) {
+          case 0: l = l11; q11 = l11; q12 = q22 = 0; break;
+          case 1: case 3: l = 0.5 * (l11 + l12); q11 = l11 * 0.5; q12 = l12 * 0.5; q22 = 0; break;
+          case 2: case 6: l = l12; q11 = 0; q12 = l12; q22 = 0; break;
+          case 4: l = 0.25 * l11 + 0.5 * l12 + 0.25 * l22; q11 = l11 * 0.25; q12 = l12 * 0.5; q22 = l22 * 0.25; break;
+          case 5: case 7: l = 0.5 * (l12 + l22); q11 = 0; q12 = l12 * 0.5; q22 = l22 * 0.5; break;
+          default: l = l22; q11 = 0; q12 = 0; q22 = l22; break;
+        }
+        if (2 + i != j) { G[0] *= l; G[1] *= l; G[2] *= l; }
+        else { G[0] *= q11; G[1] *= q12; G[2] *= q22; }
+      }
+      const double w = wk[k];
+#pragma unroll
+      for (int t = 0; t < 3; t++) g[t] = (k == 0) ? G[t] * w : g[t] + G[t] * w;
+    }
+    const double sum = g[0] + g[1] + g[2];
+    double post[3] = {0, 0, 0};
+    if (sum != 0.0) { post[0] = g[0] / sum; post[1] = g[1] / sum; post[2] = g[2] / sum; }
+    d_emit_call(A, s_gq, out + p0 + j, post, d_best3(post[0], post[1], post[2]), PM_LBL_VCF_DIPLOID, post[1] + post[2] * 2);
+  }
+}
+
 // LEAN: autosome, no extended family, nuclear families of <= 4 persons (the common case): the chrX/Y/MT
 // branches fold away and the generic kid path is not compiled, so the kernel runs at a higher occupancy.
 template <bool DN, bool ES, bool LEAN = false>
 __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
   __shared__ double s_lk[256];
   __shared__ double s_M[100];
+  __shared__ double s_gq[101];
   for (int i = threadIdx.x; i < 256; i += blockDim.x) s_lk[i] = A.lktab[i];
   for (int i = threadIdx.x; i < 100; i += blockDim.x) s_M[i] = A.M[i];
+  load_gq_thr(s_gq);
   __syncthreads();
   const long long work = (long long)A.counts[3] * A.n_fam;
   const size_t gid_base = (size_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (size_t)gridDim.x * blockDim.x;
@@ -2239,12 +2323,13 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
           const int best = d_best3(m11, m12, m22);
           // label: own sex (non-de-novo sets member sex first); de novo leaves it stale (0)
           const int8_t lab = yf ? PM_LBL_DOT : d_vcf_label(chrom, dn ? 0 : sx);
-          d_emit_call(A, out + p, post, best, lab, post[1] + post[2] * 2);
+          d_emit_call(A, s_gq, out + p, post, best, lab, post[1] + post[2] * 2);
         }
         continue;
       }
       if (ES && (kind == PM_FAM_EXTENDED || (A.nuc_es && kind == PM_FAM_NUCLEAR))) continue;   // k_posterior_es
       if (kind != PM_FAM_NUCLEAR) continue;
+      if constexpr (LEAN && !DN) { lean_nuc_post(A, s_lk, s_gq, pl, out, p0, n, g11, g12, g22, freq, is_mono); continue; }
       // CalcParentMarginal(_denovo) at freq
       ItemCtx I;
       I.a1 = a1; I.a2 = a2; I.g11 = g11; I.g12 = g12; I.g22 = g22; I.denovo = dn; I.sex = msex; I.chrom = chrom;
@@ -2280,7 +2365,7 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
           if (sum != 0) { post[0] = q11 / sum; post[1] = q12 / sum; post[2] = q22 / sum; }
           const int best = d_best3(q11, q12, q22);
           const int8_t lab = dn ? (int8_t)PM_LBL_ALLELES : ((chrom == PM_CHR_Y && sx == FEMALE) ? (int8_t)PM_LBL_DOT : d_vcf_label(chrom, sx));
-          d_emit_call(A, out + p, post, best, lab, post[1] + post[2] * 2);
+          d_emit_call(A, s_gq, out + p, post, best, lab, post[1] + post[2] * 2);
         } else if (!dn && chrom == PM_CHR_AUTO && n <= 4) {   // KidJointGenoLikelihood :798-835, autosomal, <= 2 kids
           // d_kid_geno's autosomal branches with every kid's three likelihoods loaded once and k unrolled; the
           // products run over the kids in the same order from 1.0, so the values are d_kid_geno's bit for bit
@@ -2317,7 +2402,7 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
           const double sum = g[0] + g[1] + g[2];
           double post[3] = {0, 0, 0};
           if (sum != 0.0) { post[0] = g[0] / sum; post[1] = g[1] / sum; post[2] = g[2] / sum; }
-          d_emit_call(A, out + p, post, d_best3(post[0], post[1], post[2]), d_vcf_label(chrom, sx), post[1] + post[2] * 2);
+          d_emit_call(A, s_gq, out + p, post, d_best3(post[0], post[1], post[2]), d_vcf_label(chrom, sx), post[1] + post[2] * 2);
         } else if (LEAN) {   // (every nuclear family has <= 4 persons: the branch above took them)
         } else if (!dn) {   // KidJointGenoLikelihood :798-835
           double J[9][3];
@@ -2333,7 +2418,7 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
           if (sum != 0.0) { post[0] = g[0] / sum; post[1] = g[1] / sum; post[2] = g[2] / sum; }
           const int best = d_best3(post[0], post[1], post[2]);
           const int8_t lab = (chrom == PM_CHR_Y && sx == FEMALE) ? (int8_t)PM_LBL_DOT : d_vcf_label(chrom, sx);
-          d_emit_call(A, out + p, post, best, lab, post[1] + post[2] * 2);
+          d_emit_call(A, s_gq, out + p, post, best, lab, post[1] + post[2] * 2);
         } else {   // KidJointGenoLikelihood_denovo :838-868
           double gsum[10];
           for (int t = 0; t < 10; t++) gsum[t] = 0.0;
@@ -2374,7 +2459,7 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
           for (int t = 0; t < 10; t++) post[t] = (sum == 0.0) ? 0.0 : gsum[t] / sum;
           int best = 0; double mx = 0.0;
           for (int t = 0; t < 10; t++) if (mx < post[t]) { mx = post[t]; best = t; }
-          d_emit_call(A, out + p, post, best, PM_LBL_GENO10, 0.0);
+          d_emit_call(A, s_gq, out + p, post, best, PM_LBL_GENO10, 0.0);
         }
       }
     }
@@ -2391,7 +2476,9 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
 template <bool DN>
 __global__ void __launch_bounds__(256) k_posterior_es(DevArgs A) {
   __shared__ double s_lk[256];
+  __shared__ double s_gq[101];
   for (int i = threadIdx.x; i < 256; i += blockDim.x) s_lk[i] = A.lktab[i];
+  load_gq_thr(s_gq);
   __syncthreads();
   const long long work = (long long)A.counts[3] * A.n_es_pers;
   const size_t gid_base = (size_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (size_t)gridDim.x * blockDim.x;
@@ -2412,7 +2499,7 @@ __global__ void __launch_bounds__(256) k_posterior_es(DevArgs A) {
     if (!DN) {
       if (chrom == PM_CHR_Y && sx == FEMALE) {
         const double z[3] = {0, 0, 0};
-        d_emit_call(A, out + p, z, 0, PM_LBL_DOT, 0.0);
+        d_emit_call(A, s_gq, out + p, z, 0, PM_LBL_DOT, 0.0);
         continue;
       }
       const double l11 = d_es_lk<3>(A, f, pl, s_lk, g11, g12, g22, chrom, freq, j, g11, wsl, stride);
@@ -2421,7 +2508,7 @@ __global__ void __launch_bounds__(256) k_posterior_es(DevArgs A) {
       const double sum = l11 + l12 + l22;
       double post[3] = {0, 0, 0};
       if (sum != 0) { post[0] = l11 / sum; post[1] = l12 / sum; post[2] = l22 / sum; }
-      d_emit_call(A, out + p, post, d_best3(l11, l12, l22), d_vcf_label(chrom, sx), post[1] + post[2] * 2);
+      d_emit_call(A, s_gq, out + p, post, d_best3(l11, l12, l22), d_vcf_label(chrom, sx), post[1] + post[2] * 2);
     } else {
       double lkv[10], sum = 0.0;
       for (int k = 0; k < 10; k++) lkv[k] = d_es_lk<10>(A, f, pl, s_lk, g11, g12, g22, chrom, freq, j, k, wsl, stride);
@@ -2430,7 +2517,7 @@ __global__ void __launch_bounds__(256) k_posterior_es(DevArgs A) {
       for (int k = 0; k < 10; k++) post[k] = (sum == 0) ? 0 : lkv[k] / sum;
       int b = 0; double mx = 0.0;
       for (int k = 0; k < 10; k++) if (mx < lkv[k]) { mx = lkv[k]; b = k; }
-      d_emit_call(A, out + p, post, b, PM_LBL_GENO10, 0.0);
+      d_emit_call(A, s_gq, out + p, post, b, PM_LBL_GENO10, 0.0);
     }
   }
 }
