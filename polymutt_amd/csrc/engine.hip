@@ -2131,6 +2131,13 @@ __device__ __forceinline__ void d_emit_call(const DevArgs& A, const double* s_gq
   A.calls[idx] = c;
 }
 
+// vcf_mode row entry from post[best] alone (FamilyLikelihoodSeq_VCF::OutputVCF prints best and GQ, no dosage)
+__device__ __forceinline__ void d_emit_vcf(const DevArgs& A, const double* s_gq, size_t idx, double pb, int best, int8_t label) {
+  pm_vcf_call c;
+  c.best = (int8_t)best; c.gq = (int8_t)d_gq(pb, s_gq); c.label = label; c.pad = 0;
+  ((pm_vcf_call*)A.calls)[idx] = c;
+}
+
 // likelihoodKidGenotype, :1334-1443
 __device__ void d_kid_geno(int chrom, const uint8_t* pl, int np, const double* lk, int p0, int n, const int8_t* sexv, int g11, int g12,
                            int g22, int kid, int k, double* out) {
@@ -2232,6 +2239,12 @@ __device__ __forceinline__ void lean_nuc_post(const DevArgs& A, const double* s_
     if (j == 0) { q11 = m[0] + m[1] + m[2]; q12 = m[3] + m[4] + m[5]; q22 = m[6] + m[7] + m[8]; }
     else { q11 = m[0] + m[3] + m[6]; q12 = m[1] + m[4] + m[7]; q22 = m[2] + m[5] + m[8]; }
     const double sum = q11 + q12 + q22;
+    if (A.vcf) {   // one quotient: post[best]
+      const int best = d_best3(q11, q12, q22);
+      const double qb = best == 0 ? q11 : best == 1 ? q12 : q22;
+      d_emit_vcf(A, s_gq, out + p0 + j, sum != 0 ? qb / sum : 0.0, best, PM_LBL_VCF_DIPLOID);
+      continue;
+    }
     double post[3] = {0, 0, 0};
     if (sum != 0) { post[0] = q11 / sum; post[1] = q12 / sum; post[2] = q22 / sum; }
     d_emit_call(A, s_gq, out + p0 + j, post, d_best3(q11, q12, q22), PM_LBL_VCF_DIPLOID, post[1] + post[2] * 2);
@@ -2264,6 +2277,23 @@ __device__ __forceinline__ void lean_nuc_post(const DevArgs& A, const double* s_
       for (int t = 0; t < 3; t++) g[t] = (k == 0) ? G[t] * w : g[t] + G[t] * w;
     }
     const double sum = g[0] + g[1] + g[2];
+    if (A.vcf) {
+      // d_best3 over the quotients g[t] / sum (sum > 0, g >= 0: division is monotone) is the first t whose
+      // quotient equals the largest one, post[b] with b = d_best3(g); an earlier quotient can only equal it
+      // when its g is within a rounding of g[b], so the other divisions are done only then
+      const int b = d_best3(g[0], g[1], g[2]);
+      const double gb = b == 0 ? g[0] : b == 1 ? g[1] : g[2];
+      double pb = 0.0;
+      int best = b;
+      if (sum != 0.0) {
+        pb = gb / sum;
+        const double near = gb * (1.0 - 1e-12);
+        if (b >= 1 && g[0] >= near && g[0] / sum == pb) best = 0;
+        else if (b == 2 && g[1] >= near && g[1] / sum == pb) best = 1;
+      }
+      d_emit_vcf(A, s_gq, out + p0 + j, pb, best, PM_LBL_VCF_DIPLOID);
+      continue;
+    }
     double post[3] = {0, 0, 0};
     if (sum != 0.0) { post[0] = g[0] / sum; post[1] = g[1] / sum; post[2] = g[2] / sum; }
     d_emit_call(A, s_gq, out + p0 + j, post, d_best3(post[0], post[1], post[2]), PM_LBL_VCF_DIPLOID, post[1] + post[2] * 2);
