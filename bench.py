@@ -22,13 +22,19 @@ is the timed region's ops per wall second.  `roofline_hbm` is the HBM figure BAS
 (algorithmic bytes = each launch reads the PL block of every site it touches once), with `traffic` = the
 PMC-measured HBM bytes per k_brent dispatch from the committed rocprofv3 passes under profiles/.
 
-Multi-GPU: one process per GPU (torchrun); sites are sharded (weak scaling, no data-path collective);
-the section summary counters are combined with one RCCL all-reduce (polymutt_amd/shard.py).
+Multi-GPU: one process per GPU; sites are sharded (weak scaling, no data-path collective); the section
+summary counters are combined with one RCCL all-reduce (polymutt_amd/shard.py).  `--gpus N` with N > 1 and
+no WORLD_SIZE in the environment starts `torch.distributed.run --nproc-per-node N` on this script as a child
+process (before anything touches the GPU) and relays its exit code; the workers check WORLD_SIZE == N and
+the line records `rccl_world`, the world size the counter all-reduce actually ran over.  `--dry-run` runs the
+same launcher and collectives over gloo with no engine (tests/test_cpu_host.py).
 
-cpu_baseline: the reference itself (oracle/_ref/pm_ref, built from /root/reference sources by
-oracle/ref/Makefile; it travels to the GPU box as a built binary) on a bounded GLF sample of the same
-workload, timed on the host cores -- rank 0, N=1 only: best of 3 at 1 thread and at the box's CPU share
-(min(nproc, 16) threads; BASELINE.md's plan), with nproc and the CPU model recorded.
+cpu_baseline: the clean-room CPU restatement of the reference path (tests/native/build/cpu_polymutt: the
+product host driver over the serial oracle, one core) on bounded GLF slices of the same workload, timed on
+the box's host cores -- rank 0, N=1 only.  Two slice sizes give the steady per-site rate with start-up
+(pedigree load, GLF opens) subtracted.  The reference's own objects never travel to the box (license.txt:1);
+tools/cpu_calibrate.py measures the reference against the restatement in the build container
+(profiles/r03_cpu_calibration.json) and the line carries that ratio and the implied reference rate.
 """
 import argparse
 import glob
@@ -53,7 +59,10 @@ FP64_NONFMA_TOPS = 39.3       # mul/add issue rate = half the FMA-counted peak (
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (one process each); N > 1 without WORLD_SIZE starts torch.distributed.run itself")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher + collectives only (gloo, no engine, no GPU): checks the multi-process path")
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--families", type=int, default=1000)
@@ -70,9 +79,8 @@ def parse():
                     help="engine instances (each with its own HIP stream and work buffers) taking consecutive batches: "
                          "one batch's HBM-bound k_prep overlaps the previous batch's FP64-bound Brent kernel")
     ap.add_argument("--seed", type=int, default=7)
-    ap.add_argument("--cpu-sites", type=int, default=150)
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(nproc, 16)")
-    ap.add_argument("--cpu-repeats", type=int, default=3)
+    ap.add_argument("--cpu-sites", type=int, nargs=2, default=[100, 1000],
+                    help="the two GLF slice sizes of the cpu_baseline (steady rate = their difference over the time difference)")
     ap.add_argument("--calib-steps", type=int, default=12,
                     help="one-engine steps after the timed region that give k_brent's own kernel time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -116,43 +124,55 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(args):
-    """Reference binary (or the CPU port) on a bounded GLF sample of the same workload: best of
-    --cpu-repeats runs at 1 thread and at min(nproc, 16) threads (the box's CPU share), wall time incl. ingest."""
-    import polymutt_amd as pm
-    ref_bin = os.path.join(ROOT, "oracle", "_ref", "pm_ref")
-    port_bin = os.path.join(ROOT, "tests", "native", "build", "cpu_polymutt")
-    if os.path.exists(ref_bin):
-        exe, kind = ref_bin, "reference"
-    elif os.path.exists(port_bin):
-        exe, kind = port_bin, "port"
-    else:
+def cpu_calibration(args):
+    """The reference-vs-restatement ratio tools/cpu_calibrate.py measured in the build container on the
+    default workload (profiles/r*_cpu_calibration.json), or None."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_cpu_calibration.json")))
+    if not files or (args.shape, args.families, args.denovo, args.vcf) != ("quad", 1000, True, False):
         return None
-    nproc = os.cpu_count() or 1
-    nthr = args.cpu_threads or min(nproc, CPU_SHARE)
+    d = json.load(open(files[-1]))
+    return {"file": os.path.basename(files[-1]), "reference_1thread_over_port": d["reference_1thread_over_port"],
+            "reference_best_over_port": d["reference_best_over_port"], "reference_best": d["reference_best_threads"],
+            "build_container_nproc": d["nproc"]}
+
+
+def cpu_baseline(args):
+    """The clean-room CPU restatement (product host driver + serial oracle, one core) on two bounded GLF slices
+    of the same workload; value = the steady per-site rate (slice difference over time difference), so the
+    start-up (pedigree load, one GLF open per person) does not inflate the GPU/CPU ratio."""
+    import polymutt_amd as pm
+    exe = os.path.join(ROOT, "tests", "native", "build", "cpu_polymutt")
+    if not os.path.exists(exe):
+        return None
+    s1, s2 = sorted(args.cpu_sites)
     tmp = tempfile.mkdtemp(prefix="pm_cpu_", dir=os.environ.get("TMPDIR", "/tmp"))
     try:
-        pm.synth_write_dataset(tmp, args.shape, args.families, args.cpu_sites, args.seed)
-        best = {}
-        for t in sorted({1, nthr}):
+        secs = []
+        for s in (s1, s2):
+            d = os.path.join(tmp, str(s))
+            pm.synth_write_dataset(d, args.shape, args.families, s, args.seed)
             cmd = [exe, "-p", "test.ped", "-d", "test.dat", "-g", "test.gif", "--out_vcf", "out.vcf",
-                   "--nthreads", str(t)] + (["--denovo"] if args.denovo else [])
-            for _ in range(args.cpu_repeats):
-                t0 = time.perf_counter()
-                r = subprocess.run(cmd, cwd=tmp, capture_output=True, text=True, timeout=900,
-                                   env=dict(os.environ, OMP_NUM_THREADS=str(t)))
-                dt = time.perf_counter() - t0
-                if r.returncode != 0:
-                    return {"error": r.stdout[-500:]}
-                best[t] = min(best.get(t, dt), dt)
-        top = min(best, key=lambda t: best[t])   # the thread count the reference runs fastest with on this box
-        return {"value": args.cpu_sites / best[top], "unit": "sites/s", "cores": top, "kind": kind,
-                "value_1thread": args.cpu_sites / best[1], f"value_{nthr}threads": args.cpu_sites / best[nthr],
-                "nproc": nproc, "cpu_model": cpu_model(),
-                "sample": f"{args.families} synthetic {args.shape} families x {args.cpu_sites} sites (seed {args.seed}) "
-                          f"written as GLF, end-to-end wall time incl. GLF ingest, best of {args.cpu_repeats} at "
-                          f"--nthreads 1 and {nthr}; value = the faster" + (", --denovo" if args.denovo else ""),
-                "seconds": best[top], "seconds_1thread": best[1]}
+                   "--nthreads", "1"] + (["--denovo"] if args.denovo else [])
+            t0 = time.perf_counter()
+            r = subprocess.run(cmd, cwd=d, capture_output=True, text=True, timeout=900, env=dict(os.environ, OMP_NUM_THREADS="1"))
+            secs.append(time.perf_counter() - t0)
+            if r.returncode != 0:
+                return {"error": r.stdout[-500:]}
+            shutil.rmtree(d, ignore_errors=True)
+        steady = (s2 - s1) / (secs[1] - secs[0]) if secs[1] > secs[0] else s2 / secs[1]
+        out = {"value": steady, "unit": "sites/s", "cores": 1, "kind": "port",
+               "value_end_to_end": s2 / secs[1], "seconds": secs, "nproc": os.cpu_count(),
+               "cpu_share": CPU_SHARE, "cpu_model": cpu_model(),
+               "sample": f"{args.families} synthetic {args.shape} families (seed {args.seed}) x {s1} and x {s2} sites "
+                         f"written as GLF" + (", --denovo" if args.denovo else "") + "; the restatement "
+                         "(tests/native/build/cpu_polymutt) end to end incl. GLF ingest on 1 core; value = "
+                         f"({s2} - {s1}) sites / (t{s2} - t{s1})"}
+        cal = cpu_calibration(args)
+        if cal:   # what the reference itself would do on these cores, from the build container's ratio
+            out["calibration"] = cal
+            out["reference_equivalent_1thread"] = steady * cal["reference_1thread_over_port"]
+            out["reference_equivalent_best"] = steady * cal["reference_best_over_port"]
+        return out
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 
@@ -202,11 +222,49 @@ def measured_fp64_peak():
     return max(rates) if rates else None   # the faster of mul/add: the conservative (larger) peak
 
 
+def launch_workers(args):
+    """`bench.py --gpus N` (N > 1) run directly: one worker process per GPU under torch.distributed.run, started
+    as a child before this process touches the GPU; rank 0's JSON line reaches our stdout unchanged."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd, env=dict(os.environ, PYTHONUNBUFFERED="1")).returncode
+
+
+def dry_run(args, world, rank):
+    """The multi-process skeleton without an engine: gloo process group, barrier, counter all-reduce and
+    max-over-ranks timing, exactly as the GPU path does them; one JSON line from rank 0."""
+    import torch.distributed as dist
+    from polymutt_amd.shard import allreduce_counters, max_over_ranks
+    if world > 1:
+        dist.init_process_group("gloo")
+        dist.barrier()
+    t0 = time.perf_counter()
+    counters = allreduce_counters(np.full(16, rank + 1, np.int64))
+    elapsed = max_over_ranks(time.perf_counter() - t0)
+    rw = dist.get_world_size() if dist.is_initialized() else 1
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run", "value": None, "n_gpus": world, "rccl_world": rw,
+                          "backend": dist.get_backend() if dist.is_initialized() else None,
+                          "counter_sum": int(counters[0]), "elapsed": elapsed}), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        sys.exit(launch_workers(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is not None and args.gpus != world:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run:
+        return dry_run(args, world, rank)
     dev = None
     if world > 1:
         import torch
@@ -297,6 +355,11 @@ def main():
     for f, _ in ks._fields_:
         setattr(ks, f, sum(getattr(x, f) for x in kss))
     counters = allreduce_counters(sum(e.counters().as_array() for e in engines), dev)   # the single RCCL all-reduce
+    if world > 1:
+        import torch.distributed as dist
+        rccl_world, backend = dist.get_world_size(), dist.get_backend()
+    else:
+        rccl_world, backend = 1, None
 
     total_sites = B * args.steps * world
     value = total_sites / elapsed
@@ -337,7 +400,8 @@ def main():
     if rank == 0:
         out = {
             "metric": "sites/sec (whole node) + achieved HBM GB/s, 1000 quad families",
-            "value": value, "unit": "sites/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "value": value, "unit": "sites/s", "n_gpus": world, "rccl_world": rccl_world, "collective_backend": backend,
+            "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": f"{nf} {args.shape} families, synthetic GLF-shaped sites per SURVEY 8(d) generated in "

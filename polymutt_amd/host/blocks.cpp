@@ -1,6 +1,7 @@
 // blocks.cpp -- see blocks.h.
 #include "blocks.h"
 #include <algorithm>
+#include <climits>
 #include <cstring>
 
 namespace pmhost {
@@ -101,6 +102,7 @@ void BlockSiteSource::open(const std::string& path, int n_person) {
 
 bool BlockSiteSource::nextSection() {
   // skip what is left of the current section (the reference's NextSection skips the rest of the records)
+  if (inSection_) skipSection();
   while (inSection_) loadBlock();
   char tag[4];
   if (fread(tag, 1, 4, fh_) != 4 || memcmp(tag, "SECT", 4) != 0) return false;   // "PIDX": no more sections
@@ -113,7 +115,39 @@ bool BlockSiteSource::nextSection() {
   inSection_ = true;
   ended_ = false;
   n_ = cur_ = lastBegin_ = 0;
+  section_++;
+  sectionStart_ = (uint64_t)ftell(fh_);
+  rangeHi_ = INT64_MAX;
   return true;
+}
+
+uint64_t BlockSiteSource::sectionEnd() const {
+  const BlockIndexEntry* last = nullptr;
+  for (const auto& e : index_)
+    if ((int64_t)e.section == section_) last = &e;
+  if (!last) return sectionStart_;   // no blocks: the section's first record is its end marker
+  return last->offset + 8 + (uint64_t)last->n * (4 + 1 + 14 * (uint64_t)np_);
+}
+
+bool BlockSiteSource::seek(int64_t lo, int64_t hi) {
+  if (index_.empty() || !inSection_) return false;
+  rangeHi_ = hi;
+  uint64_t at = 0;
+  bool found = false;
+  for (const auto& e : index_)
+    if ((int64_t)e.section == section_ && (int64_t)e.last_pos >= lo) { at = e.offset; found = true; break; }
+  if (!found) at = sectionEnd();   // every block of the section lies below lo
+  if (fseek(fh_, (long)at, SEEK_SET) != 0) throw FatalError("block file " + path_ + ": seek failed\n");
+  n_ = cur_ = lastBegin_ = 0;
+  return true;
+}
+
+void BlockSiteSource::skipSection() {
+  if (index_.empty() || !inSection_) return;   // no index: nextSection reads the rest in order
+  if (fseek(fh_, (long)sectionEnd(), SEEK_SET) != 0) throw FatalError("block file " + path_ + ": seek failed\n");
+  n_ = cur_ = lastBegin_ = 0;
+  loadBlock();   // the "SEND" marker
+  ended_ = true;
 }
 
 bool BlockSiteSource::loadBlock() {
@@ -127,6 +161,7 @@ bool BlockSiteSource::loadBlock() {
     return false;
   }
   if (memcmp(tag, "BLK1", 4) != 0) throw FatalError(path_ + ": corrupt block\n");
+  blocksRead_++;
   uint32_t n;
   get(&n, 4);
   n_ = (int)n;
@@ -142,7 +177,15 @@ bool BlockSiteSource::loadBlock() {
 int BlockSiteSource::nextSites(int maxSites, int* pos, uint8_t* ref) {
   lastBegin_ = cur_;
   if (ended_) return 0;
-  if (cur_ == n_ && !loadBlock()) { ended_ = true; return 0; }
+  if (cur_ == n_) {
+    if (rangeHi_ != INT64_MAX) {   // the next block (index entries are in file order) starts past the range
+      const uint64_t at = (uint64_t)ftell(fh_);
+      auto it = std::lower_bound(index_.begin(), index_.end(), at,
+                                 [](const BlockIndexEntry& e, uint64_t o) { return e.offset < o; });
+      if (it != index_.end() && it->offset == at && (int64_t)it->first_pos >= rangeHi_) { ended_ = true; return 0; }
+    }
+    if (!loadBlock()) { ended_ = true; return 0; }
+  }
   const int k = std::min(maxSites, n_ - cur_);
   for (int i = 0; i < k; i++) { pos[i] = pos_[cur_ + i]; ref[i] = ref_[cur_ + i]; }
   cur_ += k;

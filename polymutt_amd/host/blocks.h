@@ -13,7 +13,10 @@
 //   end      "SEND" u64 sites_in_section
 //   index    "PIDX" u32 n_blocks, per block {u32 section, u32 n, i32 first_pos, i32 last_pos, u64 offset}
 //   trailer  u64 index_offset "PMBE"
-// The index gives random access to any block (e.g. one shard of a section per GPU).
+// The index gives random access to any block: a shard rank seeks to the first block of its position range
+// (BlockSiteSource::seek) and skips the rest of a section after its range (skipSection), so no rank reads
+// another rank's blocks.  The SEND marker of section s sits right after its last block, so its offset follows
+// from that block's index entry (offset + 8 + n (4 + 1 + 14 n_person)).
 #pragma once
 #include <cstdint>
 #include <cstdio>
@@ -61,9 +64,13 @@ class BlockSiteSource : public SiteStream {
   bool ended() const override { return ended_; }
   void fill(const int* rowOf, uint8_t* pl, uint32_t* dm) override;
   const std::vector<BlockIndexEntry>& index() const { return index_; }
+  bool seek(int64_t lo, int64_t hi) override;   // by the block index (see SiteStream::seek)
+  void skipSection() override;      // by the block index: straight to the section's end marker
+  long blocksRead() const override { return blocksRead_; }
 
  private:
   bool loadBlock();   // false at the section end marker
+  uint64_t sectionEnd() const;   // file offset of the current section's "SEND" (index required)
   void get(void* p, size_t n);
   FILE* fh_ = nullptr;
   std::string path_;
@@ -77,6 +84,10 @@ class BlockSiteSource : public SiteStream {
   std::vector<uint32_t> dm_;
   int n_ = 0, cur_ = 0, lastBegin_ = 0;
   std::vector<BlockIndexEntry> index_;
+  int64_t section_ = -1;        // the current section's number (the index's section field)
+  uint64_t sectionStart_ = 0;   // file offset of the current section's first block (or its "SEND")
+  long blocksRead_ = 0;
+  int64_t rangeHi_ = INT64_MAX;   // seek's hi: no block starting at or past it is read
 };
 
 // Converts the GLF site stream of `ped` (index file glfIndexFile) into a .pmb file; returns the site count.

@@ -267,6 +267,10 @@ int run_polymutt_sharded(const Options& opt, const Pedigree& ped, SiteEvaluator&
     const int64_t lo = mp * R / N, hi = (R == N - 1) ? INT64_MAX : mp * (R + 1) / N;
     const bool guess = earlier || R > 0;
     eval.set_posterior_carry(guess);
+    // Block input seeks straight to the shard's first block (blocks.h index); GLF input cannot be seeked, so a
+    // GLF shard reads and drops the sites below lo (multi-GPU runs should convert with --glf2blocks first).
+    const long blocks0 = src.blocksRead();
+    const bool seeked = N > 1 && src.seek(lo, hi);
     int64_t entries = 0, n_out = 0, n_rec = 0, first_end = -1;
     const int64_t start = ftell(fh);
     std::vector<uint8_t> fpl((size_t)np * 10);
@@ -313,6 +317,10 @@ int run_polymutt_sharded(const Options& opt, const Pedigree& ped, SiteEvaluator&
       if (past || src.ended()) break;
     }
     flush();
+    if (past) src.skipSection();   // the rest of the section belongs to later shards
+    if (getenv("PM_BLOCK_STATS") && blocks0 >= 0)
+      fprintf(stderr, "PM_BLOCK_STATS shard %d section %s: blocks read %ld%s\n", R, label.c_str(), src.blocksRead() - blocks0,
+              seeked ? " (seeked)" : "");
     pm_counters C;
     eval.counters(&C);
     static_assert(sizeof(pm_counters) == 16 * sizeof(int64_t), "counter layout");

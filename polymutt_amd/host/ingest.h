@@ -67,6 +67,15 @@ class SiteStream {
   virtual bool ended() const = 0;   // the current section has no more sites
   // Rows of the sites of the last nextSites call: site i -> row rowOf[i] (< 0: skipped).
   virtual void fill(const int* rowOf, uint8_t* pl, uint32_t* dm) = 0;
+  // Random access (shards): restrict the current section to the blocks that overlap the 0-based positions
+  // [lo, hi) -- skip to the first without reading what lies below lo, end the section before a block that
+  // starts at or past hi.  Sites outside [lo, hi) may still come (the edge blocks); the caller drops them.
+  // false: this source can only be read in order (GLF: an un-indexed, delta-coded gzip stream per person) and
+  // the caller reads and drops the sites outside the range.
+  virtual bool seek(int64_t lo, int64_t hi) { (void)lo; (void)hi; return false; }
+  // Skip the rest of the current section without reading it (used after a shard's range ends).
+  virtual void skipSection() {}
+  virtual long blocksRead() const { return -1; }   // blocks loaded so far (-1: not a block source)
 };
 
 class ParallelSiteSource : public SiteStream {

@@ -139,6 +139,31 @@ def test_shard_range_partitions():
             assert max(h - l for l, h in rs) - min(h - l for l, h in rs) <= 1
 
 
+@pytest.mark.parametrize("gpus", [1, 2, 3])
+def test_bench_gpus_flag_launches_that_many_ranks(gpus):
+    """`bench.py --gpus N` run directly (no WORLD_SIZE) starts N worker processes itself and the collective
+    sees all of them (dry run: gloo, no engine)."""
+    import json
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--dry-run"],
+                       capture_output=True, text=True, timeout=300, env=dict(env, OMP_NUM_THREADS="1"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = lines[0]
+    assert line["n_gpus"] == gpus and line["rccl_world"] == gpus
+    assert line["counter_sum"] == gpus * (gpus + 1) // 2   # every rank's counters reached the all-reduce
+
+
+def test_bench_rejects_world_mismatch():
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"))
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+
+
 def _free_port():
     import socket
     with socket.socket() as s:
@@ -193,6 +218,55 @@ def _sharded_case(tmp_path, case):
         pm.synth_write_dataset(d, "trio+late", 30, 400, 31)   # (trios: the last person is male, so the state matters)
         return d, ["-p", "test.ped", "-d", "test.dat", "-g", "test.gif", "--chrX", "1"]
     raise ValueError(case)
+
+
+@pytest.mark.parametrize("case,world,block_sites", [("example", 2, 5000), ("example", 2, 10127), ("example", 3, 7000), ("multi_all", 2, 64),
+                                                    ("multi_chr2process", 3, 50), ("late_chrX", 2, 37)])
+def test_sharded_blocks_seek_to_their_range(cpu_driver, tmp_path, case, world, block_sites):
+    """Block input (--in_blocks) under the multi-process driver: each rank seeks by the block index to the first
+    block of its position range and skips the rest of a section after it, so it reads exactly the blocks that
+    overlap its range (none wholly below lo, none wholly at or past hi), and the merged VCF and summaries equal
+    one process's."""
+    from polymutt_amd import blocks
+    cwd, args = _sharded_case(tmp_path, case)
+    pmb = str(tmp_path / "in.pmb")
+    r = subprocess.run([cpu_driver] + args + ["--glf2blocks", pmb, "--block_sites", str(block_sites)], cwd=cwd,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:]
+    i = args.index("-g")
+    bargs = args[:i] + ["--in_blocks", pmb] + args[i + 2:]
+    one = str(tmp_path / "one.vcf")
+    r1 = subprocess.run([cpu_driver] + bargs + ["--out_vcf", one], cwd=cwd, capture_output=True, text=True, timeout=600)
+    assert r1.returncode == 0, r1.stdout[-2000:]
+    sh = str(tmp_path / "sharded.vcf")
+    lib = os.path.join(ROOT, "tests", "native", "build", "libpm_cpu_driver.so")
+    os.environ["PM_BLOCK_STATS"] = "1"
+    try:
+        r2 = run_sharded(cwd, bargs + ["--out_vcf", sh], world, lib=lib)
+    finally:
+        del os.environ["PM_BLOCK_STATS"]
+    assert r2.returncode == 0, r2.stdout[-3000:] + r2.stderr[-3000:]
+    assert vcf_body(sh) == vcf_body(one)
+    assert summary_lines(r2.stdout) == summary_lines(r1.stdout) and summary_lines(r1.stdout)
+    # blocks each rank read, per section, against the index
+    got = {}
+    for m in re.finditer(r"PM_BLOCK_STATS shard (\d+) section (\S+): blocks read (\d+)", r2.stderr):
+        got[(int(m.group(1)), m.group(2))] = int(m.group(3))
+    secs = blocks.read_sections(pmb)
+    index = blocks.read_index(pmb)
+    checked = 0
+    for s, (label, mp) in enumerate(secs):
+        ents = [e for e in index if e["section"] == s]
+        for R in range(world):
+            if (R, label) not in got:
+                continue   # section not analysed (--chr2process)
+            lo, hi = mp * R // world, (mp * (R + 1) // world if R < world - 1 else 1 << 62)
+            want = sum(1 for e in ents if e["last_pos"] >= lo and e["first_pos"] < hi)
+            assert got[(R, label)] == want, (R, label, got[(R, label)], want, lo, hi)
+            checked += 1
+    assert checked >= world
+    if case == "example":   # the later ranks read a fraction of the section, not its whole prefix
+        assert got[(world - 1, "1")] <= len(index) // world + 1
 
 
 @pytest.mark.parametrize("case,world", [("example", 2), ("ragged", 2), ("quad_chrX", 2), ("late_chrX", 2),
