@@ -213,6 +213,16 @@ def pmc_traffic():
     return None, os.path.basename(files[-1])
 
 
+def phase_split(st):
+    """k_brent's in-kernel hoisting / evaluation split (PM_PHASE_TIMING=1 at engine creation; else None): wave
+    time per item in each phase, from lane 0's 100 MHz clock."""
+    if not st.timed_items:
+        return None
+    h, e = st.hoist_wave_ns / st.timed_items, st.eval_wave_ns / st.timed_items
+    return {"hoist_us_per_item": h / 1e3, "eval_us_per_item": e / 1e3, "hoist_frac": h / (h + e) if h + e else 0.0,
+            "timed_items": st.timed_items}
+
+
 def measured_fp64_peak():
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_fp64_peak.json")))
     if not files:
@@ -421,6 +431,7 @@ def main():
                          "peak_measured_issue_rate": peak_meas,
                          "op_model": "SURVEY 8(d): evals x (19 nNuc + 17 + peel ops) + items x (18 nNuc + 36 kids)",
                          "peel_ops_per_eval": ext_ops, "evals": ks.evals, "items": ks.items,
+                         "phase_split": phase_split(ref_st),
                          "ops_per_site": ops / max(1, ks.sites), "log10_per_s": ks.evals * nf / elapsed},
             "roofline_hbm": {"bound": "hbm", "kernel": "k_brent", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,

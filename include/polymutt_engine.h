@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 3
+#define PM_ABI_VERSION 4
 #define PM_NCFG 7           /* varllk slots: 0 mono, 1 ref/ts, 2 ref/tv1, 3 ref/tv2, 4 ts/tv1, 5 ts/tv2, 6 tv1/tv2 */
 
 typedef enum { PM_OK = 0, PM_EINVAL = -1, PM_EHIP = -2, PM_ENOMEM = -3, PM_EBRENT = -4, PM_EPED = -5 } pm_status;
@@ -254,6 +254,10 @@ typedef struct {
   int64_t sites;         /* sites processed */
   int64_t site_visits;   /* sum over k_brent launches of the distinct sites each launch touched (each visit
                             reads that site's PL block once: the launch's algorithmic HBM bytes) */
+  int64_t hoist_wave_ns; /* with PM_PHASE_TIMING set at engine creation (else 0): k_brent wave time spent hoisting
+                            the frequency-independent family terms, summed over the items' blocks (lane 0's clock) */
+  int64_t eval_wave_ns;  /* ... and in the Brent loop (objective evaluations + updates) */
+  int64_t timed_items;   /* items the two fields above cover */
 } pm_kernel_stats;
 int pm_engine_kernel_stats(pm_engine *eng, pm_kernel_stats *out, int32_t reset);
 

@@ -136,6 +136,7 @@ struct DevArgs {
   int* items[N_LISTS];
   int* counts;             // [0..2] list sizes, [3] rows, [4] first emitted site, [5] Brent stuck, [8]/[9] quick items/site visits
   unsigned long long* eval_total;
+  unsigned long long* phase;   // PM_PHASE_TIMING: [0] hoisting, [1] evaluations, [2] items -- k_brent wave time (100 MHz ticks)
   int* row_site;           // [n] emitted row -> site
   unsigned long long* counters;   // pm_counters as 16 x u64
   int carry_postprob;      // famlk[0].CalcPostProb ran in an earlier batch
@@ -1504,7 +1505,9 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
   const bool pf = PFK && A.pf_npad > 0;
   if (pf) prefetch_planes(A, items, vb, nItems, s_pf);
   unsigned long long ev_acc = 0;   // evaluation count of this block's items: one atomic per block, at exit
+  unsigned long long ph_h = 0, ph_e = 0, ph_n = 0, ph_t = 0;   // PM_PHASE_TIMING (A.phase): hoisting / evaluation split
   for (int it = vb; it < nItems; it += gridDim.x) {
+    if (A.phase) ph_t = wall_clock64();
     const int item = items[it];
     const int site = item >> 3, cfg = item & 7;
     const int r = A.ref[site];
@@ -1596,6 +1599,7 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
         for (int a = 0; a <= PDM; a++) ce[q][a] = a <= ed[q] ? co[(size_t)a * T] : 0.0;
       }
     }
+    if (A.phase) { const unsigned long long t = wall_clock64(); ph_h += t - ph_t; ph_t = t; }
     const bool single = !A.vcf && ((cfg == 0) || (A.single_nuclear && !A.unrelated));
     // One evaluation site for the objective: the three bracketing evaluations of OptimizeFrequency
     // (:432-444) and every Brent step (core/MathGold.cpp:81-177) run through the same loop body.
@@ -1722,8 +1726,10 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
       if (!single) ev_acc += nev - skipped;   // objective evaluations computed
       if (!ok) atomicExch(&A.counts[5], 1);
     }
+    if (A.phase) { ph_e += wall_clock64() - ph_t; ph_n++; }
   }
   if (threadIdx.x == 0 && ev_acc) atomicAdd(A.eval_total, ev_acc);
+  if (A.phase && threadIdx.x == 0) { atomicAdd(&A.phase[0], ph_h); atomicAdd(&A.phase[1], ph_e); atomicAdd(&A.phase[2], ph_n); }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2721,6 +2727,7 @@ struct pm_engine {
   int* d_items[N_LISTS] = {nullptr, nullptr, nullptr};
   int* d_counts = nullptr;
   unsigned long long* d_eval_total = nullptr;
+  unsigned long long* d_phase = nullptr;   // PM_PHASE_TIMING set at engine creation: k_brent hoisting / evaluation wave time
   int* d_row_site = nullptr;
   int* d_row_blk = nullptr;   // k_rows_count: written records per 1024-site block
   unsigned long long* d_counters = nullptr;
@@ -3254,6 +3261,10 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
   DALLOC(E->d_counters, 16);
   HIP_TRY(hipMemset(E->d_counters, 0, 16 * sizeof(unsigned long long)));
   HIP_TRY(hipMemset(E->d_eval_total, 0, sizeof(unsigned long long)));
+  if (getenv("PM_PHASE_TIMING")) {
+    DALLOC(E->d_phase, 3);
+    HIP_TRY(hipMemset(E->d_phase, 0, 3 * sizeof(unsigned long long)));
+  }
   int rc = pm_engine_begin_section(E, PM_CHR_AUTO);
   if (rc) { pm_engine_destroy(E); return rc; }
   *out = E;
@@ -3343,7 +3354,7 @@ static DevArgs make_args(pm_engine* E, int n, const uint8_t* pl, const uint32_t*
   A.n = n; A.pl = pl; A.dm = dm; A.ref = ref; A.res = res; A.calls = calls;
   A.raw = E->d_raw; A.minv = E->d_minv; A.evals = E->d_evals; A.mono_plain = E->d_mono;
   for (int l = 0; l < N_LISTS; l++) A.items[l] = E->d_items[l];
-  A.counts = E->d_counts; A.eval_total = E->d_eval_total; A.row_site = E->d_row_site; A.row_blk = E->d_row_blk; A.counters = E->d_counters;
+  A.counts = E->d_counts; A.eval_total = E->d_eval_total; A.phase = E->d_phase; A.row_site = E->d_row_site; A.row_blk = E->d_row_blk; A.counters = E->d_counters;
   A.carry_postprob = E->carry_postprob ? 1 : 0;
   A.mono_dn = mono_dn_in_prep(E) ? 1 : 0;
   return A;
@@ -3696,9 +3707,17 @@ int pm_engine_kernel_stats(pm_engine* E, pm_kernel_stats* out, int32_t reset) {
   *out = E->stats;
   out->evals = (int64_t)ev;
   out->fam_evals = (int64_t)ev * E->n_fam;
+  if (E->d_phase) {
+    unsigned long long ph[3];
+    HIP_TRY(hipMemcpy(ph, E->d_phase, sizeof(ph), hipMemcpyDeviceToHost));
+    out->hoist_wave_ns = (int64_t)ph[0] * 10;   // wall_clock64 runs at 100 MHz
+    out->eval_wave_ns = (int64_t)ph[1] * 10;
+    out->timed_items = (int64_t)ph[2];
+  }
   if (reset) {
     E->stats = pm_kernel_stats{};
     HIP_TRY(hipMemset(E->d_eval_total, 0, sizeof(ev)));
+    if (E->d_phase) HIP_TRY(hipMemset(E->d_phase, 0, 3 * sizeof(unsigned long long)));
   }
   return PM_OK;
 }

@@ -422,8 +422,7 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, c
     throw FatalError("glfListFile or input VCF file not provided for input!\n");
   if (opt.vcfOutFile.empty()) throw FatalError("vcfOutFile not provided for output!\n");
   if (!opt.vcfInFile.empty()) {   // main.cpp:238-246
-    if (sharded) throw FatalError("--in_vcf runs cannot be sharded over several processes\n");
-    return run_polymutt_vcf(opt, ped, eval);
+    return run_polymutt_vcf(opt, ped, eval, sharded ? comm : nullptr);
   }
   if (opt.denovo && opt.denovo_llr < 0) throw FatalError("denovo_min_LLR can only be greater than 0 !\n");
 

@@ -4,6 +4,8 @@
 // a field is missing when absent or empty).  The likelihood work runs on the SiteEvaluator in vcf_mode.
 #include "vcf_input.h"
 #include <zlib.h>
+#include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -15,14 +17,37 @@
 namespace pmhost {
 namespace {
 
-struct LineReader {   // plain or gzip text, lines of any length
+struct LineReader {   // plain or gzip text, lines of any length; offsets are in the uncompressed stream
   gzFile fh = nullptr;
+  std::string path;
   std::vector<char> buf = std::vector<char>(1 << 20);
   ~LineReader() { if (fh) gzclose(fh); }
   bool open(const std::string& p) {
+    path = p;
     fh = gzopen(p.c_str(), "rb");
     if (fh) gzbuffer(fh, 1 << 20);
     return fh != nullptr;
+  }
+  int64_t tell() const { return (int64_t)gztell(fh); }
+  void seek(int64_t off) {   // plain files: a file seek; gzip: zlib re-inflates up to off (no parsing)
+    if (gzseek(fh, (z_off_t)off, SEEK_SET) < 0) throw FatalError("VCF input " + path + ": seek failed\n");
+  }
+  int64_t size() {   // uncompressed bytes of the stream (gzip: one inflate pass), position kept
+    const int64_t here = tell();
+    int64_t n = 0;
+    if (gzdirect(fh)) {
+      FILE* f = fopen(path.c_str(), "rb");
+      if (!f || fseek(f, 0, SEEK_END) != 0) throw FatalError("VCF input " + path + ": cannot size\n");
+      n = (int64_t)ftell(f);
+      fclose(f);
+    } else {
+      seek(0);
+      int got;
+      while ((got = gzread(fh, buf.data(), (unsigned)buf.size())) > 0) n += got;
+      if (got < 0) throw FatalError("VCF input " + path + ": read error\n");
+    }
+    seek(here);
+    return n;
   }
   bool next(std::string& line) {
     line.clear();
@@ -111,9 +136,46 @@ std::string label_text(const pm_geno_call& c) {   // GetBestGenoLabel_vcfv4 (Nuc
 
 }  // namespace
 
-int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eval) {
+// One record's FORMAT bookkeeping as the reference keeps it across records (FamilyLikelihoodSeq_VCF
+// FillPenetrance :316-324): DP's index is looked up on every biallelic record until found; GL/PL once, on the first
+// biallelic record.
+struct FormatState {
+  int GL_idx = -1, PL_idx = -1, DP_index = -1;
+  bool frozen() const { return DP_index >= 0 && (GL_idx >= 0 || PL_idx >= 0); }
+};
+
+namespace {
+void copy_file_into(const std::string& path, FILE* out) {
+  FILE* in = fopen(path.c_str(), "rb");
+  if (!in) throw FatalError("VCF shard merge: " + path + " is missing\n");
+  std::vector<char> buf(1 << 20);
+  size_t got;
+  while ((got = fread(buf.data(), 1, buf.size(), in)) > 0) fwrite(buf.data(), 1, got, out);
+  fclose(in);
+}
+int64_t pack_call(const pm_geno_call& c) {
+  return (int64_t)(uint16_t)c.best | ((int64_t)(uint16_t)c.gq << 16) | ((int64_t)(uint8_t)c.label << 32);
+}
+pm_geno_call unpack_call(int64_t v) {
+  pm_geno_call c{0.0, (int16_t)(v & 0xFFFF), (int16_t)((v >> 16) & 0xFFFF), (int8_t)((v >> 32) & 0xFF), {0, 0, 0}};
+  return c;
+}
+double bits2d(int64_t v) { double d; memcpy(&d, &v, 8); return d; }
+int64_t d2bits(double d) { int64_t v; memcpy(&v, &d, 8); return v; }
+}  // namespace
+
+// Sharded (comm->world > 1): rank R analyses the records whose lines start in its slice of the body's bytes
+// (uncompressed offsets; gzip input is re-inflated up to the slice, never parsed) and writes their records to
+// <out>.part<R>.  Cross-record state is handed over explicitly: the FORMAT indices come from a pre-scan of the
+// records before the slice (normally just the first one), and the records a rank meets before its first
+// record with data -- printed by the reference with the previous computed record's QUAL, AF and genotypes
+// (PedVCF.cpp:113-122) -- are written after one all-gather that carries each rank's last computed state.
+// Rank 0 then writes the header and concatenates the parts; the result is byte-identical to one process.
+int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, const ShardComm* comm) {
   if (opt.vcfInFile == opt.vcfOutFile) throw FatalError("Input and output VCF files are the same!\n");
   if (opt.vcfOutFile.empty()) throw FatalError("vcfOutFile not provided for output!\n");
+  const bool sharded = comm && comm->world > 1;
+  const int R = sharded ? comm->rank : 0, N = sharded ? comm->world : 1;
   LineReader in;
   if (!in.open(opt.vcfInFile)) throw FatalError("Cannot open VCF file " + opt.vcfInFile + "\n");
 
@@ -134,6 +196,7 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
       break;
     }
   }
+  const int64_t body = in.tell();
   // included samples in VCF order (PedVCF.cpp:66-80); person index per VCF column (-1: not in the ped)
   std::vector<int> col_person(samples.size(), -1);
   std::vector<std::string> included;
@@ -142,24 +205,28 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
     if (it != pid2person.end()) { col_person[i] = it->second; included.push_back(samples[i]); }
   }
 
-  FILE* out = fopen(opt.vcfOutFile.c_str(), "w");
+  auto write_header = [&](FILE* out) {
+    std::string header = "#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT";
+    for (auto& s : included) header += "\t" + s;
+    fprintf(out, "##fileformat=VCFv4.1\n##Polymutt=%s\n", opt.cmd.c_str());
+    fprintf(out, "%s",
+            "##Note=VCF file modified by polymutt. Updated fileds include: QUAL, GT and GQ, AF and AC. NOTE: modification was "
+            "applied only to biallelic variants\n"
+            "##FILTER=<ID=LOWDP,Description=\"Low Depth filter when the average depth per sample is lessn than 1\">\n"
+            "##INFO=<ID=DP,Number=1,Type=Integer,Description=\"Total Read Depth\">\n"
+            "##INFO=<ID=AF,Number=A,Type=Float,Description=\"Alternative Allele Frequency\">\n"
+            "##INFO=<ID=AC,Number=1,Type=Integer,Description=\"Alternative Allele Count\">\n"
+            "##FORMAT=<ID=GT,Number=1,Type=String,Description=\"Genotype\">\n"
+            "##FORMAT=<ID=GQ,Number=1,Type=Integer,Description=\"Genotype Quality\">\n"
+            "##FORMAT=<ID=DP,Number=1,Type=Integer,Description=\"Read Depth\">\n"
+            "##FORMAT=<ID=PL,Number=3,Type=Integer,Description=\"Phred-scaled Genotype Likelihoods\">\n"
+            "##FORMAT=<ID=GL,Number=3,Type=Float,Description=\"Log10 Genotype Likelihoods\">\n");
+    fprintf(out, "%s\n", header.c_str());
+  };
+  const std::string part = opt.vcfOutFile + ".part" + std::to_string(R), lead_in = part + ".lead", lead_out = part + ".leadvcf";
+  FILE* out = fopen(sharded ? part.c_str() : opt.vcfOutFile.c_str(), "w");
   if (!out) throw FatalError("Open outpuf VCF file " + opt.vcfOutFile + " failed!\n");
-  std::string header = "#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT";
-  for (auto& s : included) header += "\t" + s;
-  fprintf(out, "##fileformat=VCFv4.1\n##Polymutt=%s\n", opt.cmd.c_str());
-  fprintf(out, "%s",
-          "##Note=VCF file modified by polymutt. Updated fileds include: QUAL, GT and GQ, AF and AC. NOTE: modification was "
-          "applied only to biallelic variants\n"
-          "##FILTER=<ID=LOWDP,Description=\"Low Depth filter when the average depth per sample is lessn than 1\">\n"
-          "##INFO=<ID=DP,Number=1,Type=Integer,Description=\"Total Read Depth\">\n"
-          "##INFO=<ID=AF,Number=A,Type=Float,Description=\"Alternative Allele Frequency\">\n"
-          "##INFO=<ID=AC,Number=1,Type=Integer,Description=\"Alternative Allele Count\">\n"
-          "##FORMAT=<ID=GT,Number=1,Type=String,Description=\"Genotype\">\n"
-          "##FORMAT=<ID=GQ,Number=1,Type=Integer,Description=\"Genotype Quality\">\n"
-          "##FORMAT=<ID=DP,Number=1,Type=Integer,Description=\"Read Depth\">\n"
-          "##FORMAT=<ID=PL,Number=3,Type=Integer,Description=\"Phred-scaled Genotype Likelihoods\">\n"
-          "##FORMAT=<ID=GL,Number=3,Type=Float,Description=\"Log10 Genotype Likelihoods\">\n");
-  fprintf(out, "%s\n", header.c_str());
+  if (!sharded) write_header(out);
 
   // GetPolyPrior() once, before any SetNonAutosomeFlags (PedVCF.cpp:103): autosomal; GetPolyPrior_indel()
   // returns the same `prior` (NucFamGenotypeLikelihood.cpp:313).  PedVCF's own tstv_ratio is 2.0 (:7).
@@ -174,14 +241,18 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
   std::vector<pm_site_result> res(B);
   std::vector<pm_geno_call> calls((size_t)B * np);
   std::vector<Pending> pend;
-  int nb = 0, cur_chrom = -1, GL_idx = -1, PL_idx = -1, DP_index = -1, n_samples_with_data = 0, bad_allele = 0;
-  bool first = true;
+  int nb = 0, cur_chrom = -1, n_samples_with_data = 0, bad_allele = 0;
+  FormatState fs;
+  bool first = R == 0;   // FillPenetrance's first-record banner (:270-282): rank 0 owns the file's first record
+  bool computed_any = false;
+  int64_t n_lead = 0;
+  FILE* lead = nullptr;   // sharded, R > 0: raw lines met before this rank's first record with data
   State st;
   st.calls.assign(np, pm_geno_call{0.0, 0, 0, PM_LBL_VCF_DIPLOID, {0, 0, 0}});
 
-  auto write_record = [&](const Pending& r, bool fresh, const pm_site_result* R, const pm_geno_call* C) {
+  auto write_record = [&](FILE* fo, const Pending& r, bool fresh, const pm_site_result* Rs, const pm_geno_call* C) {
     if (fresh) {   // mono/poly -> QUAL (PedVCF.cpp:136-152), with the reference's operator-precedence slip
-      const double mono = R->varllk[0], poly = R->varllk[1];
+      const double mono = Rs->varllk[0], poly = Rs->varllk[1];
       double llk_alt, llk_ref;
       if (!r.indel) {
         llk_alt = log10((prior * (is_ts(r.a1, r.a2) ? 1 : 0)) ? prior_ts : prior_tv) + poly;
@@ -195,7 +266,7 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
         const double posterior = 1 / (1 + pow(10, llk_ref - llk_alt));
         st.qual = -10 * log10(1 - posterior);
       }
-      st.min = R->af;
+      st.min = Rs->af;
       for (int p = 0; p < np; p++) st.calls[p] = C[p];
     }
     // OutputVCF (FamilyLikelihoodSeq_VCF.cpp:412-521)
@@ -207,73 +278,64 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
       if (col_person[i] < 0) continue;
       AC += st.calls[col_person[i]].best;
       int dp = 0;
-      if (DP_index > 0) {
-        missing = get_field(L, r.cols[9 + i], DP_index, f);
+      if (fs.DP_index > 0) {
+        missing = get_field(L, r.cols[9 + i], fs.DP_index, f);
         dp = missing ? 0 : atoi(L.c_str() + f.b);
       }
       if (missing) continue;
       totalDepth += dp;
     }
     auto fld = [&](int k) { return L.substr(r.cols[k].b, r.cols[k].e - r.cols[k].b); };
-    fprintf(out, "%s\t%s\t%s\t%s\t%s\t%.2f\t%s\tAF=%.2f;AC=%d;DP=%d\t%s", fld(0).c_str(), fld(1).c_str(), fld(2).c_str(),
+    fprintf(fo, "%s\t%s\t%s\t%s\t%s\t%.2f\t%s\tAF=%.2f;AC=%d;DP=%d\t%s", fld(0).c_str(), fld(1).c_str(), fld(2).c_str(),
             fld(3).c_str(), fld(4).c_str(), st.qual, fld(6).c_str(), 1 - st.min, AC, totalDepth,
-            PL_idx > 0 ? "GT:GQ:DP:PL" : "GT:GQ:DP:GL");
+            fs.PL_idx > 0 ? "GT:GQ:DP:PL" : "GT:GQ:DP:GL");
     for (size_t i = 0; i < samples.size(); i++) {
       const int p = col_person[i];
       if (p < 0) continue;
       const pm_geno_call& c = st.calls[p];
       const std::string lab = label_text(c);
-      fprintf(out, "\t%s:%d:", (c.gq > 0 || lab == ".") ? lab.c_str() : "./.", (int)c.gq);
+      fprintf(fo, "\t%s:%d:", (c.gq > 0 || lab == ".") ? lab.c_str() : "./.", (int)c.gq);
       std::string dps = ".";
-      if (DP_index > 0) {
-        missing = get_field(L, r.cols[9 + i], DP_index, f);
+      if (fs.DP_index > 0) {
+        missing = get_field(L, r.cols[9 + i], fs.DP_index, f);
         if (!missing) dps = L.substr(f.b, f.e - f.b);
       }
-      fprintf(out, "%s:", missing ? "." : dps.c_str());
-      missing = get_field(L, r.cols[9 + i], PL_idx > 0 ? PL_idx : GL_idx, f);
-      fprintf(out, "%s", missing ? "." : L.substr(f.b, f.e - f.b).c_str());
+      fprintf(fo, "%s:", missing ? "." : dps.c_str());
+      missing = get_field(L, r.cols[9 + i], fs.PL_idx > 0 ? fs.PL_idx : fs.GL_idx, f);
+      fprintf(fo, "%s", missing ? "." : L.substr(f.b, f.e - f.b).c_str());
     }
-    fprintf(out, "\n");
+    fprintf(fo, "\n");
   };
 
   auto flush = [&]() {
     int rows = 0;
     if (nb > 0) eval.run(nb, pl.data(), dm.data(), ref.data(), res.data(), calls.data(), &rows);
     for (auto& r : pend) {
-      if (r.computed) write_record(r, true, &res[r.slot], calls.data() + (size_t)res[r.slot].call_row * np);
-      else write_record(r, false, nullptr, nullptr);
+      if (r.computed) write_record(out, r, true, &res[r.slot], calls.data() + (size_t)res[r.slot].call_row * np);
+      else write_record(out, r, false, nullptr, nullptr);
     }
     pend.clear();
     nb = 0;
   };
 
+  // parses a record's columns and its biallelic / allele / FORMAT-index bookkeeping (:296-324); false: not output
   std::string refS, altS;
-  Span f;
-  while (in.next(line)) {
-    if (line.empty() || line[0] == '#') continue;
-    Pending r;
-    r.line.swap(line);
+  auto classify = [&](Pending& r) {
     split(r.line, '\t', r.cols);
     if (r.cols.size() < 9) throw FatalError("Malformed VCF record (fewer than 9 columns)\n");
     const std::string& L = r.line;
     auto fld = [&](int k) { return L.substr(r.cols[k].b, r.cols[k].e - r.cols[k].b); };
-    if (first) {   // FillPenetrance on the first record (:270-282), then VarCallFromVCF's banner (:117)
-      for (size_t i = 0; i < samples.size(); i++) {
-        if (col_person[i] < 0) { printf("Sample ID \"%s\" not included in the analysis!\n", samples[i].c_str()); continue; }
-        n_samples_with_data++;
-      }
-    }
     refS = fld(3); altS = fld(4);
     bool biallelic = refS != altS && altS.find(',') == std::string::npos;
     if (biallelic) {
       r.indel = refS.size() > 1 || altS.size() > 1;
       r.a1 = r.indel ? 1 : allele2int(refS);
       r.a2 = r.indel ? 2 : allele2int(altS);
-      if (DP_index < 0) DP_index = format_index(L, r.cols[8], "DP");
-      if (GL_idx < 0 && PL_idx < 0) {
-        GL_idx = format_index(L, r.cols[8], "GL");
-        PL_idx = format_index(L, r.cols[8], "PL");
-        if (GL_idx < 0 && PL_idx < 0) {
+      if (fs.DP_index < 0) fs.DP_index = format_index(L, r.cols[8], "DP");
+      if (fs.GL_idx < 0 && fs.PL_idx < 0) {
+        fs.GL_idx = format_index(L, r.cols[8], "GL");
+        fs.PL_idx = format_index(L, r.cols[8], "PL");
+        if (fs.GL_idx < 0 && fs.PL_idx < 0) {
           fprintf(stderr, "NO GL or PL field was found. Please check the vcf file at chr:%s and position:%d", fld(0).c_str(),
                   atoi(fld(1).c_str()));
           exit(1);
@@ -282,10 +344,51 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
       }
       // non-ACGT single-base alleles index the genotype tables out of range in the reference (undefined
       // behaviour); a case-only REF/ALT difference gives a degenerate pair: both are skipped here
-      if (r.a1 == 0 || r.a2 == 0 || r.a1 == r.a2) { bad_allele++; biallelic = false; }
+      if (r.a1 == 0 || r.a2 == 0 || r.a1 == r.a2) return -1;
     }
-    if (first) { printf("Total samples in both VCF and PED files: %d\n\n", n_samples_with_data); first = false; }
-    if (!biallelic) continue;   // OutputVCF returns at once for these records (:419)
+    return biallelic ? 1 : 0;
+  };
+
+  int64_t lo = body, hi = INT64_MAX;
+  if (sharded) {
+    const int64_t total = in.size();
+    lo = body + (total - body) * R / N;
+    if (R < N - 1) hi = body + (total - body) * (R + 1) / N;
+    if (R > 0) {
+      // FORMAT indices as the records before the slice leave them (normally fixed by the first record)
+      while (!fs.frozen() && in.tell() < lo && in.next(line)) {
+        if (line.empty() || line[0] == '#') continue;
+        Pending r;
+        r.line.swap(line);
+        classify(r);
+      }
+      in.seek(lo - 1);   // the first line starting at or after lo: skip the rest of the line holding byte lo - 1
+      in.next(line);
+      lead = fopen(lead_in.c_str(), "w+b");
+      if (!lead) throw FatalError("Open outpuf VCF file " + opt.vcfOutFile + " failed!\n");
+    }
+  }
+
+  Span f;
+  for (;;) {
+    if (in.tell() >= hi || !in.next(line)) break;
+    if (line.empty() || line[0] == '#') continue;
+    Pending r;
+    r.line.swap(line);
+    if (first)   // FillPenetrance on the first record (:270-282) ...
+      for (size_t i = 0; i < samples.size(); i++) {
+        if (col_person[i] < 0) { printf("Sample ID \"%s\" not included in the analysis!\n", samples[i].c_str()); continue; }
+        n_samples_with_data++;
+      }
+    const int kind = classify(r);
+    const std::string& L = r.line;
+    auto fld = [&](int k) { return L.substr(r.cols[k].b, r.cols[k].e - r.cols[k].b); };
+    if (first) {   // ... then VarCallFromVCF's banner (:117)
+      printf("Total samples in both VCF and PED files: %d\n\n", n_samples_with_data);
+      first = false;
+    }
+    if (kind < 0) bad_allele++;
+    if (kind <= 0) continue;   // OutputVCF returns at once for these records (:419)
 
     // penetrances / log-likelihoods of the record (:318-366) into a dense block row
     const int slot = nb;
@@ -296,7 +399,7 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
     for (size_t i = 0; i < samples.size(); i++) {
       const int p = col_person[i];
       if (p < 0) continue;
-      if (get_field(L, r.cols[9 + i], GL_idx > 0 ? GL_idx : PL_idx, f)) break;   // missing: the reference returns (:332-343)
+      if (get_field(L, r.cols[9 + i], fs.GL_idx > 0 ? fs.GL_idx : fs.PL_idx, f)) break;   // missing: the reference returns (:332-343)
       double v[3];
       int nv = 0, b = f.b;
       for (int q = f.b; q <= f.e; q++)
@@ -310,7 +413,7 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
       if (v[0] != 0.0 || v[1] != 0.0 || v[2] != 0.0) withdata++;
       const int gix[3] = {g0, g1, g2};
       for (int k = 0; k < 3; k++) {
-        const int phred = (int)(PL_idx > 0 ? v[k] : -10 * v[k]);   // PL2LK(int(...)) (:361-363, :57-63)
+        const int phred = (int)(fs.PL_idx > 0 ? v[k] : -10 * v[k]);   // PL2LK(int(...)) (:361-363, :57-63)
         if (phred < 0) throw FatalError("Phred-scaled likelihood " + std::to_string(phred) + " can not be negative\n");
         row[(size_t)p * 10 + gix[k]] = (uint8_t)(phred > 255 ? 255 : phred);
       }
@@ -319,9 +422,13 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
     const std::string chrom = fld(0);
     const int cls = chrom == opt.chrX ? PM_CHR_X : chrom == opt.chrY ? PM_CHR_Y : chrom == opt.MT ? PM_CHR_MT : PM_CHR_AUTO;
     if (withdata == 0) {   // written with the previous record's QUAL / AF / genotypes (:113)
-      pend.push_back(std::move(r));
+      if (lead && !computed_any) {   // ... which an earlier rank computed: written after the exchange
+        fprintf(lead, "%s\n", r.line.c_str());
+        n_lead++;
+      } else pend.push_back(std::move(r));
       continue;
     }
+    computed_any = true;
     if (cls != cur_chrom) {
       if (nb > 0) {   // the row is already packed in `slot`; move it to slot 0 after the flush
         std::vector<uint8_t> keep(row, row + (size_t)np * 10);
@@ -339,8 +446,69 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
     if (nb == B) flush();
   }
   flush();
+  if (!sharded) {
+    fclose(out);
+    if (bad_allele) fprintf(stderr, "%d biallelic records with non-ACGT alleles were skipped\n", bad_allele);
+    return 0;
+  }
+
+  // exchange: {computed any, QUAL, AF minimiser, skipped records, the genotype calls} of each rank's last computed record
+  const int K = 4 + np;
+  std::vector<int64_t> send(K), recv((size_t)N * K);
+  send[0] = computed_any; send[1] = d2bits(st.qual); send[2] = d2bits(st.min); send[3] = bad_allele;
+  for (int p = 0; p < np; p++) send[4 + p] = pack_call(st.calls[p]);
+  comm->allgather(send.data(), K, recv.data());
+  fflush(out);
   fclose(out);
-  if (bad_allele) fprintf(stderr, "%d biallelic records with non-ACGT alleles were skipped\n", bad_allele);
+  if (lead) {   // this rank's leading no-data records, with the state of the nearest earlier rank that computed one
+    State carried;
+    carried.calls.assign(np, pm_geno_call{0.0, 0, 0, PM_LBL_VCF_DIPLOID, {0, 0, 0}});
+    for (int q = R - 1; q >= 0; q--) {
+      const int64_t* v = recv.data() + (size_t)q * K;
+      if (!v[0]) continue;
+      carried.qual = bits2d(v[1]);
+      carried.min = bits2d(v[2]);
+      for (int p = 0; p < np; p++) carried.calls[p] = unpack_call(v[4 + p]);
+      break;
+    }
+    std::swap(st, carried);
+    FILE* lo_out = fopen(lead_out.c_str(), "wb");
+    if (!lo_out) throw FatalError("Open outpuf VCF file " + opt.vcfOutFile + " failed!\n");
+    LineReader lr;
+    fflush(lead);
+    fclose(lead);
+    if (!lr.open(lead_in)) throw FatalError("VCF shard: " + lead_in + " is missing\n");
+    for (int64_t k = 0; k < n_lead && lr.next(line); k++) {
+      Pending r;
+      r.line.swap(line);
+      split(r.line, '\t', r.cols);
+      write_record(lo_out, r, false, nullptr, nullptr);
+    }
+    fclose(lo_out);
+    remove(lead_in.c_str());
+  }
+  {   // every shard's files are complete before the lead concatenates them
+    int64_t one = 1;
+    std::vector<int64_t> all(N);
+    comm->allgather(&one, 1, all.data());
+  }
+  if (R != 0) return 0;
+  FILE* fin = fopen(opt.vcfOutFile.c_str(), "w");
+  if (!fin) throw FatalError("Open outpuf VCF file " + opt.vcfOutFile + " failed!\n");
+  write_header(fin);
+  int64_t bad = 0;
+  for (int q = 0; q < N; q++) {
+    const std::string pq = opt.vcfOutFile + ".part" + std::to_string(q);
+    if (q > 0) {
+      copy_file_into(pq + ".leadvcf", fin);
+      remove((pq + ".leadvcf").c_str());
+    }
+    copy_file_into(pq, fin);
+    remove(pq.c_str());
+    bad += recv[(size_t)q * K + 3];
+  }
+  fclose(fin);
+  if (bad) fprintf(stderr, "%lld biallelic records with non-ACGT alleles were skipped\n", (long long)bad);
   return 0;
 }
 

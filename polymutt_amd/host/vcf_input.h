@@ -7,7 +7,8 @@
 
 namespace pmhost {
 
-// Runs polymutt --in_vcf; returns the process exit code.
-int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eval);
+// Runs polymutt --in_vcf; returns the process exit code.  With comm->world > 1 the run is one shard: a
+// byte slice of the records per rank, merged by rank 0 (vcf_input.cpp).
+int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, const ShardComm* comm = nullptr);
 
 }  // namespace pmhost

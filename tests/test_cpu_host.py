@@ -286,3 +286,38 @@ def test_sharded_driver_matches_one_process_gloo(cpu_driver, tmp_path, case, wor
     assert summary_lines(r2.stdout) == summary_lines(r1.stdout) and summary_lines(r1.stdout)
     assert not [f for f in os.listdir(os.path.dirname(sh)) if ".part" in f]   # shard files merged and removed
     assert ("first record re-run" in r2.stderr) == (case == "late_chrX"), r2.stderr[-2000:]
+
+
+@pytest.mark.parametrize("case,world", [("golden", 2), ("golden", 3), ("edits", 2), ("nodata", 2), ("nodata", 3),
+                                        ("empty_rank", 3)])
+def test_sharded_vcf_input_matches_one_process_gloo(cpu_driver, tmp_path, case, world):
+    """--in_vcf over several processes (a byte slice of the records per rank, vcf_input.cpp) writes the same VCF as
+    one process: gzip and plain input, the record-kind edits, and records without data at every rank's start
+    (printed with the previous computed record's state, PedVCF.cpp:113-122, handed over from an earlier rank --
+    two ranks back when the rank between has no data at all)."""
+    from vcf_edits import write_edited_vcf, write_nodata_vcf
+    if case == "golden":
+        src = os.path.join(EXAMPLE, "testvcf.in.vcf.gz")
+    else:
+        src = str(tmp_path / "in.vcf")
+        if case == "edits":
+            write_edited_vcf(src)
+        elif case == "nodata":
+            write_nodata_vcf(src, worlds=(2, 3))
+        else:
+            write_nodata_vcf(src, worlds=(3,), empty_rank=(1, 3))
+    args = ["-p", "test.ped", "-d", "test.dat", "--in_vcf", src]
+    one = str(tmp_path / "one.vcf")
+    r1 = subprocess.run([cpu_driver] + args + ["--out_vcf", one], cwd=EXAMPLE, capture_output=True, text=True, timeout=600)
+    assert r1.returncode == 0, r1.stdout[-2000:] + r1.stderr[-2000:]
+    sh = str(tmp_path / "sharded.vcf")
+    lib = os.path.join(ROOT, "tests", "native", "build", "libpm_cpu_driver.so")
+    r2 = run_sharded(EXAMPLE, args + ["--out_vcf", sh], world, lib=lib)
+    assert r2.returncode == 0, r2.stdout[-3000:] + r2.stderr[-3000:]
+    assert vcf_body(sh) == vcf_body(one)
+    assert len(vcf_body(one)) > 8000
+    assert not [f for f in os.listdir(os.path.dirname(sh)) if ".part" in f]
+    if case == "golden":
+        import gzip
+        gold = gzip.open(os.path.join(EXAMPLE, "testvcf.out.vcf.body.gz"), "rt").read().splitlines()
+        assert vcf_body(sh)[1:] == gold[1:]

@@ -75,3 +75,64 @@ def check_edited_output(got, theta=0.001, n_founders=6):
             assert g[:4] == e[:4] and g[4] == EDITS[i][1] and g[5:] == e[5:], i
         else:
             assert got[j] == gold[i], f"record {i} differs:\n{got[j][:200]}\n{gold[i][:200]}"
+
+
+def _zero_pl(col):
+    """A sample column with its PL replaced by 0,0,0 (no data: withdata_cnt counts a sample only when one of
+    its three values is non-zero, FamilyLikelihoodSeq_VCF.cpp:345-350)."""
+    f = col.split(":")
+    f[-1] = "0,0,0"
+    return ":".join(f)
+
+
+def _drop_dp(cols):
+    """The record with its DP FORMAT key renamed (GT:GQ:DP:DS:PL -> GT:GQ:XD:DS:PL): DP is then absent, while PL
+    keeps the FORMAT index the first biallelic record fixes for the whole file (:316-324)."""
+    fmt = cols[8].split(":")
+    fmt[fmt.index("DP")] = "XD"
+    return cols[:8] + [":".join(fmt)] + cols[9:]
+
+
+def write_nodata_vcf(path, worlds=(2, 3), empty_rank=None):
+    """The example input edited so that the records a shard rank meets first carry no data (all PL 0,0,0): the
+    reference prints them with the previous computed record's QUAL, AF and genotypes (PedVCF.cpp:113-122), so a
+    sharded run must hand that state over from the rank before.  The first line of every rank's byte slice
+    (polymutt_amd/host/vcf_input.cpp) for each world size is blanked with its neighbours; the first three records
+    have no DP key (DP's FORMAT index is looked up per record until found, :316-324); empty_rank=(r, world)
+    blanks that rank's whole slice (the state then comes from two ranks back).  Returns the blanked record indices."""
+    lines = gzip.open(os.path.join(EXAMPLE, "testvcf.in.vcf.gz"), "rt").read().splitlines()
+    head = [l for l in lines if l.startswith("#")]
+    recs = [l.split("\t") for l in lines if not l.startswith("#")]
+    for i in range(3):
+        recs[i] = _drop_dp(recs[i])
+
+    def layout():
+        body = sum(len(l) + 1 for l in head)
+        starts, off = [], body
+        for r in recs:
+            starts.append(off)
+            off += len("\t".join(r)) + 1
+        return body, off, starts
+
+    blank = set()
+    body, total, starts = layout()   # blanking changes lengths: the slices are taken on the final file below
+    for _ in range(3):               # fixed point: blank, recompute the slices, blank again
+        for w in worlds:
+            for r in range(1, w):
+                lo = body + (total - body) * r // w
+                k = next(i for i, s in enumerate(starts) if s >= lo)
+                blank.update(range(max(0, k - 2), min(len(recs), k + 3)))
+        if empty_rank:
+            r, w = empty_rank
+            lo, hi = body + (total - body) * r // w, body + (total - body) * (r + 1) // w
+            blank.update(i for i, s in enumerate(starts) if lo <= s < hi)
+        for i in blank:
+            recs[i] = recs[i][:9] + [_zero_pl(c) for c in recs[i][9:]]
+        body, total, starts = layout()
+    for w in worlds:   # every rank's first record is blanked in the final layout
+        for r in range(1, w):
+            lo = body + (total - body) * r // w
+            assert next(i for i, s in enumerate(starts) if s >= lo) in blank, (w, r)
+    with open(path, "w") as fh:
+        fh.write("\n".join(head + ["\t".join(r) for r in recs]) + "\n")
+    return sorted(blank)
