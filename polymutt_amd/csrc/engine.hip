@@ -30,6 +30,7 @@
 #include <vector>
 #include "../../include/polymutt_engine.h"
 #include "synth_core.h"
+#include "es_jit.h"
 
 #define MALE 1
 #define FEMALE 2
@@ -101,6 +102,11 @@ struct DevArgs {
   const int* poly_lay;
   const int* poly_deg;
   int poly_coef, poly_dcap;
+  // k_es_hoist -> k_brent hand-over (EP): the D + 1 coefficients (+ D at poly_dcap - 1) of every (item, ES family) of
+  // the items [es_it0, es_it1) of a list at es_coef[(((it - es_it0) * max_ext + q) * poly_dcap + a) * T + lane]
+  double* es_coef;
+  int es_it0, es_it1, max_ext;
+  int hoist_ws, hoist_tmp;   // k_es_hoist LDS per wave (doubles): the family's layout workspace, the step temporaries
   // posteriors of peeled families: one work item per (row, person) of es_pers[n_es_pers] = family << 8 | member
   const int* es_pers;
   int n_es_pers;
@@ -462,295 +468,8 @@ __device__ __forceinline__ double d_es_lk(const DevArgs& A, int f, const uint8_t
 // Brent item on coefficient vectors; each objective evaluation is then one Horner pass over D + 1 non-negative
 // coefficients (no cancellation: relative error ~ (D + 2) ulp, the class of PM_NUM_POLY's nuclear quartics).
 // The reference-order numeric peel stays in d_es_lk (PM_NUM_PRODUCT / PM_NUM_EXACT, and the posteriors).
-// register tiles for the hoisting: a polynomial of degree <= PDM as PDM + 1 coefficients (zero above its degree)
+// register tiles of the evaluation: a polynomial of degree <= PDM as PDM + 1 coefficients (zero above its degree)
 #define PDM 8
-__device__ __forceinline__ void pl_load(const double* ws, size_t st, int o, int d, double* r) {
-#pragma unroll
-  for (int a = 0; a <= PDM; a++) r[a] = a <= d ? ws[(size_t)(o + a) * st] : 0.0;
-}
-__device__ __forceinline__ void pl_store(double* ws, size_t st, int o, int d, const double* r) {
-#pragma unroll
-  for (int a = 0; a <= PDM; a++)
-    if (a <= d) ws[(size_t)(o + a) * st] = r[a];
-}
-__device__ __forceinline__ void pl_mul(const double* x, const double* y, double* r) {   // degrees summing to <= PDM
-#pragma unroll
-  for (int a = PDM; a >= 0; a--) {
-    double s = 0;
-#pragma unroll
-    for (int b = 0; b <= a; b++) s += x[b] * y[a - b];
-    r[a] = s;
-  }
-}
-
-// top: only the f^D coefficient (the item is the de novo monomorphism, one evaluation at f = 1 where
-// L = c_D): every founder keeps just its top term and every step runs at degree 0 -- a numeric peel at f = 1.
-template <int NS>
-__device__ __forceinline__ int es_poly_hoist(const DevArgs& A, int f, const uint8_t* pl, const double* lk, int g11, int g12,
-                                             int g22, int chrom, double* ws, size_t st, double* out, bool top = false) {
-  const int p0 = A.fam_start[f], n = A.fam_start[f + 1] - p0, nf = A.fam_founders[f];
-  const bool X = chrom == PM_CHR_X, Y = chrom == PM_CHR_Y, MT = chrom == PM_CHR_MT;
-  const int* L = A.poly_lay + A.poly_start[f];
-  const int tof = L[1], D = top ? 0 : L[2 + chrom];
-  const size_t np = (size_t)A.n_person;
-#define WV(o) ws[(size_t)(o) * st]
-#define POFF(i) (L[6 + (i)] & 0xFFFFFF)
-#define PCAP(i) (L[6 + (i)] >> 24)
-#define MOFF(m) (L[6 + n + (m)] & 0xFFFFFF)
-#define MCAP(m) (L[6 + n + (m)] >> 24)
-  for (int i = 0; i < n; i++) {   // InitializePartials(_BA) x SetFounderPriors(_BA)
-    const int sx = A.sex[p0 + i];
-    const bool fo = A.is_founder[p0 + i] != 0 && i < nf;
-    const uint8_t* R = pl + p0 + i;
-    const int o = POFF(i), cap = PCAP(i);
-    const bool yf = Y && sx == FEMALE;
-    const int dfull = !fo ? 0 : (Y && sx == FEMALE) ? 0 : ((X || Y) && sx == MALE) || MT ? 1 : 2;
-    const int d = top ? 0 : dfull;
-    const int gidx[3] = {g11, g12, g22};
-    for (int j = 0; j < NS; j++) {
-      for (int a = 0; a <= d; a++) WV(o + j * cap + a) = 0.0;
-      if (NS == 3) {
-        const double pen = lk[R[gidx[j] * np]];
-        if (yf) { WV(o + j * cap) = 1.0; continue; }   // BA chrY females: partial 1.0 (:1449-1465)
-        if (!fo) { WV(o + j * cap) = pen; continue; }
-        if (top) { if (j == 0) WV(o + j * cap) = pen; continue; }       // the f^d term: f^2 or f
-        if (d == 2) WV(o + j * cap + 2 - j) = j == 1 ? 2 * pen : pen;   // f^2, 2fg, g^2
-        else if (j != 1) WV(o + j * cap + (j == 0 ? 1 : 0)) = pen;      // f, 0, g
-      } else {
-        const double pen = lk[R[j * np]];
-        if (!fo) { WV(o + j * cap) = pen; continue; }
-        const int q = j == g11 ? 0 : j == g12 ? 1 : j == g22 ? 2 : 3;
-        if (q == 3) continue;
-        if (top && dfull > 0) { if (q == 0) WV(o + j * cap) = pen; continue; }   // the f^d term
-        if (d == 2) WV(o + j * cap + 2 - q) = q == 1 ? 2 * pen : pen;
-        else if (d == 1) { if (q != 1) WV(o + j * cap + (q == 0 ? 1 : 0)) = pen; }
-        else WV(o + j * cap) = pen;   // chrY female founder: q = 1, 1, 1
-      }
-    }
-  }
-  const int s0 = A.peel_start[f], s1 = A.peel_start[f + 1];
-  for (int s = s0; s < s1; s++) {
-    const int2 S = A.steps[s];
-    const int type = S.x & 255, from0 = (S.x >> 8) & 255, from1 = (S.x >> 16) & 255, to0 = (S.x >> 24) & 255;
-    const int slot = (S.y >> 8) & 255, create = (S.y >> 16) & 1, fa2mo = (S.y >> 17) & 1;
-    const int dg = top ? 0 : A.poly_deg[4 * s + chrom];
-    const int da = dg & 127, db = (dg >> 7) & 127, dc = (dg >> 14) & 127, de = (dg >> 21) & 127;
-    if (type == 1 && da == 0) {   // offspring with a constant partial (leaves): scalar sums, M scaled in place
-      const int off = from0, po = POFF(off), pc = PCAP(off), mo = MOFF(slot), mc = MCAP(slot);
-      const int csex = A.sex[p0 + off];
-      double pk[NS];
-#pragma unroll
-      for (int k = 0; k < NS; k++) pk[k] = WV(po + k * pc);
-      for (int i = 0; i < NS; i++)
-        for (int j = 0; j < NS; j++) {
-          double sum = 0;
-#pragma unroll
-          for (int k = 0; k < NS; k++) sum += ((NS == 3) ? d_tba(i, j, k, chrom, csex) : A.T10dn[(i * 10 + j) * 10 + k]) * pk[k];
-          const int e0 = mo + (i * NS + j) * mc;
-          if (create) WV(e0) = sum;
-          else
-            for (int a = 0; a <= db; a++) WV(e0 + a) *= sum;
-        }
-    } else if (NS == 3 && type == 1 && da + db <= PDM) {   // BA, register tiles
-      const int off = from0, po = POFF(off), pc = PCAP(off), mo = MOFF(slot), mc = MCAP(slot);
-      const int csex = A.sex[p0 + off];
-      double P[3][PDM + 1];
-#pragma unroll
-      for (int k = 0; k < 3; k++) pl_load(ws, st, po + k * pc, da, P[k]);
-      for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++) {
-          double S[PDM + 1], M[PDM + 1], R[PDM + 1];
-#pragma unroll
-          for (int a = 0; a <= PDM; a++) S[a] = 0.0;
-#pragma unroll
-          for (int k = 0; k < 3; k++) {
-            const double t = d_tba(i, j, k, chrom, csex);
-#pragma unroll
-            for (int a = 0; a <= PDM; a++) S[a] += t * P[k][a];
-          }
-          const int e0 = mo + (i * 3 + j) * mc;
-          if (create) { pl_store(ws, st, e0, da, S); continue; }
-          pl_load(ws, st, e0, db, M);
-          pl_mul(M, S, R);
-          pl_store(ws, st, e0, da + db, R);
-        }
-    } else if (NS == 10 && type == 1 && da <= 2 && da + db <= PDM) {   // 10 states, register tiles (offspring degree <= 2)
-      const int off = from0, po = POFF(off), pc = PCAP(off), mo = MOFF(slot), mc = MCAP(slot);
-      double P[10][3];
-#pragma unroll
-      for (int k = 0; k < 10; k++)
-#pragma unroll
-        for (int a = 0; a < 3; a++) P[k][a] = a <= da ? WV(po + k * pc + a) : 0.0;
-      for (int i = 0; i < 10; i++)
-        for (int j = 0; j < 10; j++) {
-          double S[PDM + 1], M[PDM + 1], R[PDM + 1];
-#pragma unroll
-          for (int a = 0; a <= PDM; a++) S[a] = 0.0;
-#pragma unroll
-          for (int k = 0; k < 10; k++) {
-            const double t = A.T10dn[(i * 10 + j) * 10 + k];
-#pragma unroll
-            for (int a = 0; a < 3; a++) S[a] += t * P[k][a];
-          }
-          const int e0 = mo + (i * 10 + j) * mc;
-          if (create) { pl_store(ws, st, e0, da, S); continue; }
-          pl_load(ws, st, e0, db, M);
-          pl_mul(M, S, R);
-          pl_store(ws, st, e0, da + db, R);
-        }
-    } else if (NS == 10 && type == 2 && da <= 2 && da + db + dc <= PDM) {   // 10 states, register tiles (from degree <= 2)
-      const int sf = from0, stt = to0, fo_ = POFF(sf), fc = PCAP(sf), to_ = POFF(stt), tc = PCAP(stt);
-      const int mo = slot == 255 ? 0 : MOFF(slot), mc = slot == 255 ? 0 : MCAP(slot);
-      double P[10][3];
-#pragma unroll
-      for (int j = 0; j < 10; j++)
-#pragma unroll
-        for (int a = 0; a < 3; a++) P[j][a] = a <= da ? WV(fo_ + j * fc + a) : 0.0;
-      for (int i = 0; i < 10; i++) {
-        double S[PDM + 1], M[PDM + 1], R[PDM + 1];
-#pragma unroll
-        for (int a = 0; a <= PDM; a++) S[a] = 0.0;
-#pragma unroll
-        for (int j = 0; j < 10; j++) {
-          if (slot == 255) {
-#pragma unroll
-            for (int a = 0; a < 3; a++) S[a] += P[j][a];
-          } else {
-            pl_load(ws, st, mo + (fa2mo ? j * 10 + i : i * 10 + j) * mc, db, M);
-#pragma unroll
-            for (int a = 0; a <= PDM; a++) {   // R = P[j] (degree <= 2) x M
-              double acc = 0;
-#pragma unroll
-              for (int b = 0; b < 3; b++)
-                if (a - b >= 0) acc += P[j][b] * M[a - b];
-              R[a] = acc;
-            }
-#pragma unroll
-            for (int a = 0; a <= PDM; a++) S[a] += R[a];
-          }
-        }
-        pl_load(ws, st, to_ + i * tc, dc, M);
-        pl_mul(M, S, R);
-        pl_store(ws, st, to_ + i * tc, da + db + dc, R);
-      }
-    } else if (NS == 3 && type == 2 && da + db + dc <= PDM) {   // BA, register tiles
-      const int sf = from0, stt = to0, fo_ = POFF(sf), fc = PCAP(sf), to_ = POFF(stt), tc = PCAP(stt);
-      const int mo = slot == 255 ? 0 : MOFF(slot), mc = slot == 255 ? 0 : MCAP(slot);
-      double P[3][PDM + 1];
-#pragma unroll
-      for (int j = 0; j < 3; j++) pl_load(ws, st, fo_ + j * fc, da, P[j]);
-      for (int i = 0; i < 3; i++) {
-        double S[PDM + 1], M[PDM + 1], R[PDM + 1];
-#pragma unroll
-        for (int a = 0; a <= PDM; a++) S[a] = 0.0;
-#pragma unroll
-        for (int j = 0; j < 3; j++) {
-          if (slot == 255) {
-#pragma unroll
-            for (int a = 0; a <= PDM; a++) S[a] += P[j][a];
-          } else {
-            pl_load(ws, st, mo + (fa2mo ? j * 3 + i : i * 3 + j) * mc, db, M);
-            pl_mul(P[j], M, R);
-#pragma unroll
-            for (int a = 0; a <= PDM; a++) S[a] += R[a];
-          }
-        }
-        pl_load(ws, st, to_ + i * tc, dc, M);
-        pl_mul(M, S, R);
-        pl_store(ws, st, to_ + i * tc, da + db + dc, R);
-      }
-    } else if (type == 1) {   // offspring -> parents: M(i, j) *= sum_k T(i, j, k) P_off[k]   (da = deg P_off, db = deg M)
-      const int off = from0, po = POFF(off), pc = PCAP(off), mo = MOFF(slot), mc = MCAP(slot);
-      const int csex = A.sex[p0 + off];
-      if (create)
-        for (int e = 0; e < NS * NS; e++) WV(mo + e * mc) = 1.0;
-      for (int i = 0; i < NS; i++)
-        for (int j = 0; j < NS; j++) {
-          for (int a = 0; a <= da; a++) {
-            double sum = 0;
-            for (int k = 0; k < NS; k++) {
-              const double t = (NS == 3) ? d_tba(i, j, k, chrom, csex) : A.T10dn[(i * 10 + j) * 10 + k];
-              sum += t * WV(po + k * pc + a);
-            }
-            WV(tof + a) = sum;
-          }
-          const int e0 = mo + (i * NS + j) * mc;
-          for (int a = db + da; a >= 0; a--) {   // in place, highest coefficient first
-            double acc = 0;
-            for (int c = max(0, a - da); c <= min(a, db); c++) acc += WV(e0 + c) * WV(tof + a - c);
-            WV(e0 + a) = acc;
-          }
-        }
-    } else if (type == 2) {   // spouse -> spouse: P_to[i] *= sum_j P_from[j] M(j, i)   (da from, db M, dc to)
-      const int sf = from0, stt = to0, fo_ = POFF(sf), fc = PCAP(sf), to_ = POFF(stt), tc = PCAP(stt);
-      const int mo = slot == 255 ? 0 : MOFF(slot), mc = slot == 255 ? 0 : MCAP(slot);
-      for (int i = 0; i < NS; i++) {
-        for (int a = 0; a <= da + db; a++) {
-          double sum = 0;
-          for (int j = 0; j < NS; j++) {
-            if (slot == 255) { sum += a <= da ? WV(fo_ + j * fc + a) : 0.0; continue; }
-            const int e0 = mo + (fa2mo ? j * NS + i : i * NS + j) * mc;
-            for (int u = max(0, a - db); u <= min(a, da); u++) sum += WV(fo_ + j * fc + u) * WV(e0 + a - u);
-          }
-          WV(tof + a) = sum;
-        }
-        const int e0 = to_ + i * tc, ds = da + db;
-        for (int a = dc + ds; a >= 0; a--) {
-          double acc = 0;
-          for (int c = max(0, a - ds); c <= min(a, dc); c++) acc += WV(e0 + c) * WV(tof + a - c);
-          WV(e0 + a) = acc;
-        }
-      }
-    } else {   // parents -> only offspring: P_off[k] *= sum_ij P_fa[i] M(i, j) P_mo[j] T(i, j, k)   (da fa, db M, dc mo, de off)
-      const int fa = from0, mo_ = from1, off = to0;
-      const int fao = POFF(fa), fac = PCAP(fa), moo = POFF(mo_), moc = PCAP(mo_), oo = POFF(off), oc = PCAP(off);
-      const int mo = slot == 255 ? 0 : MOFF(slot), mc = slot == 255 ? 0 : MCAP(slot);
-      const int csex = A.sex[p0 + off];
-      const int dw = da + db + dc, w = tof + NS * (dw + 1);   // S_k at tof + k (dw + 1), W(i, j) at w
-      for (int e = 0; e < NS * (dw + 1); e++) WV(tof + e) = 0.0;
-      for (int i = 0; i < NS; i++)
-        for (int j = 0; j < NS; j++) {
-          for (int a = 0; a <= dw; a++) {
-            double acc = 0;
-            for (int u = 0; u <= da; u++)
-              for (int v = 0; v <= db; v++) {
-                const int r = a - u - v;
-                if (r < 0 || r > dc) continue;
-                const double m = slot == 255 ? 1.0 : WV(mo + (i * NS + j) * mc + v);
-                acc += WV(fao + i * fac + u) * m * WV(moo + j * moc + r);
-              }
-            WV(w + a) = acc;
-          }
-          for (int k = 0; k < NS; k++) {
-            double t;
-            if (NS == 3) t = d_tba(i, j, k, chrom, csex);
-            else t = (slot == 255) ? A.T10dn[(i * 10 + j) * 10 + k] : A.T10[(i * 10 + j) * 10 + k];   // quirk :1391
-            for (int a = 0; a <= dw; a++) WV(tof + k * (dw + 1) + a) += t * WV(w + a);
-          }
-        }
-      for (int k = 0; k < NS; k++) {
-        const int e0 = oo + k * oc;
-        for (int a = de + dw; a >= 0; a--) {
-          double acc = 0;
-          for (int c = max(0, a - dw); c <= min(a, de); c++) acc += WV(e0 + c) * WV(tof + k * (dw + 1) + a - c);
-          WV(e0 + a) = acc;
-        }
-      }
-    }
-  }
-  const int fin = (A.steps[s1 - 1].x >> 24) & 255, fo_ = POFF(fin), fc = PCAP(fin);
-  for (int a = 0; a <= D; a++) {
-    double sum = 0.0;
-    for (int i = 0; i < NS; i++) sum += WV(fo_ + i * fc + a);
-    out[(size_t)a * st] = sum;
-  }
-#undef WV
-#undef POFF
-#undef PCAP
-#undef MOFF
-#undef MCAP
-  return D;
-}
 
 // L(f) from the coefficients: g^D sum_a c_a t^a (t = f / g <= 1) or f^D sum_a c_a s^(D - a) (s = g / f < 1)
 __device__ __forceinline__ double es_poly_eval(const double* c, size_t st, int D, double x) {
@@ -1460,13 +1179,256 @@ __device__ __forceinline__ double block_logprod(double m, int e, double* red, in
 // ES=true additionally peels the lane's extended families (instantiated only for pedigrees that have them).
 // Occupancy target (waves per SIMD) of a Brent flavour: the lean polynomial kernel keeps 5 doubles per
 // family, so even at S=16 two items fit on a SIMD if the hoisting phase is kept from spreading out.
+
+// ------------------------------------------------------------------------------------------------
+// k_es_hoist: the polynomial-form peel for one (Brent item, extended family) per wave, ahead of
+// the item's k_brent (EP), which then reads the coefficients instead of peeling.  The family's schedule is
+// wave-uniform (scalar control flow), its partials and marriage partials live in this wave's LDS slice, and each
+// step runs as phases whose output elements -- a (state, coefficient) or (state pair, coefficient) each -- are
+// spread over the lanes, with a wave-level barrier between phases (LDS ops of one wave complete in order).  Same
+// steps and degrees as FamilyLikelihoodES.cpp :1105-1395 (plain `transmission` at :1391);
+// every phase writes out of place (temporaries after the layout) and copies back.
+// A wave's LDS: hoist_ws (the family layout of poly_layout) + hoist_tmp (the largest step's temporaries).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ double lds_tba(const double* tba, int i, int j, int k, int chrom, int child_sex) {   // d_tba on LDS
+  const int o = i * 9 + j * 3 + k;
+  double t = tba[o];
+  if (chrom == PM_CHR_X) t = (child_sex == MALE) ? tba[2 * 27 + o] : tba[27 + o];
+  if (chrom == PM_CHR_Y) t = (child_sex == MALE) ? tba[3 * 27 + o] : 1.0;
+  if (chrom == PM_CHR_MT) t = tba[4 * 27 + o];
+  return t;
+}
+
+template <int NS>
+__device__ __forceinline__ void wave_poly_peel(const DevArgs& A, int f, const uint8_t* pl, const double* lk, const double* tba,
+                                               const double* T10, const double* T10dn, int g11, int g12, int g22, int chrom,
+                                               bool top, double* ws, int lane, double* out, int ostride) {
+  const int p0 = A.fam_start[f], n = A.fam_start[f + 1] - p0, nf = A.fam_founders[f];
+  const bool X = chrom == PM_CHR_X, Y = chrom == PM_CHR_Y, MT = chrom == PM_CHR_MT;
+  const int* L = A.poly_lay + A.poly_start[f];
+  const int D = top ? 0 : L[2 + chrom];
+  const size_t np = (size_t)A.n_person;
+  double* TB = ws + A.hoist_ws;   // step temporaries
+#define WV(o) ws[(o)]
+#define POFF(i) (L[6 + (i)] & 0xFFFFFF)
+#define PCAP(i) (L[6 + (i)] >> 24)
+#define MOFF(m) (L[6 + n + (m)] & 0xFFFFFF)
+#define MCAP(m) (L[6 + n + (m)] >> 24)
+  for (int x = lane; x < n * NS; x += 64) {   // InitializePartials(_BA) x SetFounderPriors(_BA)
+    const int i = x / NS, j = x - i * NS;
+    const int sx = A.sex[p0 + i];
+    const bool fo = A.is_founder[p0 + i] != 0 && i < nf;
+    const uint8_t* R = pl + p0 + i;
+    const int o = POFF(i) + j * PCAP(i);
+    const bool yf = Y && sx == FEMALE;
+    const int dfull = !fo ? 0 : (Y && sx == FEMALE) ? 0 : ((X || Y) && sx == MALE) || MT ? 1 : 2;
+    const int d = top ? 0 : dfull;
+    for (int a = 0; a <= d; a++) WV(o + a) = 0.0;
+    if (NS == 3) {
+      const int gj = j == 0 ? g11 : j == 1 ? g12 : g22;
+      const double pen = lk[R[gj * np]];
+      if (yf) WV(o) = 1.0;                          // BA chrY females: partial 1.0 (:1449-1465)
+      else if (!fo) WV(o) = pen;
+      else if (top) { if (j == 0) WV(o) = pen; }    // the f^d term: f^2 or f
+      else if (d == 2) WV(o + 2 - j) = j == 1 ? 2 * pen : pen;   // f^2, 2fg, g^2
+      else if (j != 1) WV(o + (j == 0 ? 1 : 0)) = pen;          // f, 0, g
+    } else {
+      const double pen = lk[R[j * np]];
+      const int q = j == g11 ? 0 : j == g12 ? 1 : j == g22 ? 2 : 3;
+      if (!fo) WV(o) = pen;
+      else if (q != 3) {
+        if (top && dfull > 0) { if (q == 0) WV(o) = pen; }   // the f^d term
+        else if (d == 2) WV(o + 2 - q) = q == 1 ? 2 * pen : pen;
+        else if (d == 1) { if (q != 1) WV(o + (q == 0 ? 1 : 0)) = pen; }
+        else WV(o) = pen;   // chrY female founder: q = 1, 1, 1
+      }
+    }
+  }
+  wave_sync();
+  const int s0 = A.peel_start[f], s1 = A.peel_start[f + 1];
+  for (int s = s0; s < s1; s++) {
+    const int2 S = A.steps[s];
+    const int type = S.x & 255, from0 = (S.x >> 8) & 255, from1 = (S.x >> 16) & 255, to0 = (S.x >> 24) & 255;
+    const int slot = (S.y >> 8) & 255, create = (S.y >> 16) & 1, fa2mo = (S.y >> 17) & 1;
+    const int dg = top ? 0 : A.poly_deg[4 * s + chrom];
+    const int da = dg & 127, db = (dg >> 7) & 127, dc = (dg >> 14) & 127, de = (dg >> 21) & 127;
+    if (type == 1) {   // offspring -> parents: M(i, j) *= sum_k T(i, j, k) P_off[k]   (da = deg P_off, db = deg M)
+      const int off = from0, po = POFF(off), pc = PCAP(off), mo = MOFF(slot), mc = MCAP(slot);
+      const int csex = A.sex[p0 + off];
+      const int wa = da + 1;
+      for (int x = lane; x < NS * NS * wa; x += 64) {   // S(e, a)
+        const int e = x / wa, a = x - e * wa, i = e / NS, j = e - i * NS;
+        double sum = 0;
+#pragma unroll
+        for (int k = 0; k < NS; k++) {
+          const double t = (NS == 3) ? lds_tba(tba, i, j, k, chrom, csex) : T10dn[(i * 10 + j) * 10 + k];
+          sum += t * WV(po + k * pc + a);
+        }
+        if (create) WV(mo + e * mc + a) = sum;
+        else TB[x] = sum;
+      }
+      wave_sync();
+      if (!create) {
+        const int w = da + db + 1;
+        double* TM = TB + NS * NS * wa;
+        for (int x = lane; x < NS * NS * w; x += 64) {   // (M S)(e, a)
+          const int e = x / w, a = x - e * w;
+          double acc = 0;
+          for (int c = max(0, a - da); c <= min(a, db); c++) acc += WV(mo + e * mc + c) * TB[e * wa + a - c];
+          TM[x] = acc;
+        }
+        wave_sync();
+        for (int x = lane; x < NS * NS * w; x += 64) {
+          const int e = x / w, a = x - e * w;
+          WV(mo + e * mc + a) = TM[x];
+        }
+        wave_sync();
+      }
+    } else if (type == 2) {   // spouse -> spouse: P_to[i] *= sum_j P_from[j] M(j, i)   (da from, db M, dc to)
+      const int sf = from0, stt = to0, fo_ = POFF(sf), fc = PCAP(sf), to_ = POFF(stt), tc = PCAP(stt);
+      const int mo = slot == 255 ? 0 : MOFF(slot), mc = slot == 255 ? 0 : MCAP(slot);
+      const int ds = da + db, ws1 = ds + 1;
+      for (int x = lane; x < NS * ws1; x += 64) {   // S(i, a)
+        const int i = x / ws1, a = x - i * ws1;
+        double sum = 0;
+        for (int j = 0; j < NS; j++) {
+          if (slot == 255) { if (a <= da) sum += WV(fo_ + j * fc + a); continue; }
+          const int e0 = mo + (fa2mo ? j * NS + i : i * NS + j) * mc;
+          for (int u = max(0, a - db); u <= min(a, da); u++) sum += WV(fo_ + j * fc + u) * WV(e0 + a - u);
+        }
+        TB[x] = sum;
+      }
+      wave_sync();
+      const int w = dc + ds + 1;
+      double* TM = TB + NS * ws1;
+      for (int x = lane; x < NS * w; x += 64) {   // P_to S
+        const int i = x / w, a = x - i * w;
+        double acc = 0;
+        for (int c = max(0, a - ds); c <= min(a, dc); c++) acc += WV(to_ + i * tc + c) * TB[i * ws1 + a - c];
+        TM[x] = acc;
+      }
+      wave_sync();
+      for (int x = lane; x < NS * w; x += 64) {
+        const int i = x / w, a = x - i * w;
+        WV(to_ + i * tc + a) = TM[x];
+      }
+      wave_sync();
+    } else {   // parents -> only offspring: P_off[k] *= sum_ij P_fa[i] M(i, j) P_mo[j] T(i, j, k)   (da fa, db M, dc mo, de off)
+      const int fa = from0, mo_ = from1, off = to0;
+      const int fao = POFF(fa), fac = PCAP(fa), moo = POFF(mo_), moc = PCAP(mo_), oo = POFF(off), oc = PCAP(off);
+      const int mo = slot == 255 ? 0 : MOFF(slot), mc = slot == 255 ? 0 : MCAP(slot);
+      const int csex = A.sex[p0 + off];
+      const int dw = da + db + dc, ww = dw + 1;
+      for (int x = lane; x < NS * NS * ww; x += 64) {   // W(e, a) = P_fa[i] M(i, j) P_mo[j]
+        const int e = x / ww, a = x - e * ww, i = e / NS, j = e - i * NS;
+        double acc = 0;
+        for (int u = 0; u <= da; u++)
+          for (int v = 0; v <= db; v++) {
+            const int r = a - u - v;
+            if (r < 0 || r > dc) continue;
+            const double m = slot == 255 ? 1.0 : WV(mo + e * mc + v);
+            acc += WV(fao + i * fac + u) * m * WV(moo + j * moc + r);
+          }
+        TB[x] = acc;
+      }
+      wave_sync();
+      double* TS = TB + NS * NS * ww;
+      for (int x = lane; x < NS * ww; x += 64) {   // S(k, a) = sum_e T(i, j, k) W(e, a)
+        const int k = x / ww, a = x - k * ww;
+        double sum = 0;
+        for (int e = 0; e < NS * NS; e++) {
+          const int i = e / NS, j = e - i * NS;
+          double t;
+          if (NS == 3) t = lds_tba(tba, i, j, k, chrom, csex);
+          else t = (slot == 255) ? T10dn[(i * 10 + j) * 10 + k] : T10[(i * 10 + j) * 10 + k];   // quirk :1391
+          sum += t * TB[e * ww + a];
+        }
+        TS[x] = sum;
+      }
+      wave_sync();
+      const int w = de + dw + 1;
+      double* TM = TS + NS * ww;
+      for (int x = lane; x < NS * w; x += 64) {   // P_off S
+        const int k = x / w, a = x - k * w;
+        double acc = 0;
+        for (int c = max(0, a - dw); c <= min(a, de); c++) acc += WV(oo + k * oc + c) * TS[k * ww + a - c];
+        TM[x] = acc;
+      }
+      wave_sync();
+      for (int x = lane; x < NS * w; x += 64) {
+        const int k = x / w, a = x - k * w;
+        WV(oo + k * oc + a) = TM[x];
+      }
+      wave_sync();
+    }
+  }
+  const int fin = (A.steps[s1 - 1].x >> 24) & 255, fo_ = POFF(fin), fc = PCAP(fin);
+  for (int a = lane; a <= D; a += 64) {
+    double sum = 0.0;
+    for (int i = 0; i < NS; i++) sum += WV(fo_ + i * fc + a);
+    out[(size_t)a * ostride] = sum;
+  }
+  if (lane == 0) out[(size_t)(A.poly_dcap - 1) * ostride] = (double)D;
+  wave_sync();   // the next unit reuses the slice
+#undef WV
+#undef POFF
+#undef PCAP
+#undef MOFF
+#undef MCAP
+}
+
+// grid: persistent, 4 waves per block (tables shared, one LDS slice per wave); units (item, ES family slot e = q T + lane
+// of the lane plan) with the family fastest, so a block's waves share the item's site block in the caches.
+template <bool DN>
+__global__ void __launch_bounds__(256) k_es_hoist(DevArgs A, int list) {
+  __shared__ double s_lk[256];
+  __shared__ double s_tba[5 * 27];
+  __shared__ double s_T10[DN ? 1000 : 1], s_T10dn[DN ? 1000 : 1];
+  extern __shared__ double s_hw[];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) s_lk[i] = A.lktab[i];
+  for (int i = threadIdx.x; i < 5 * 27; i += blockDim.x) s_tba[i] = (&c_TBA[0][0])[i];
+  if constexpr (DN)
+    for (int i = threadIdx.x; i < 1000; i += blockDim.x) { s_T10[i] = A.T10[i]; s_T10dn[i] = A.T10dn[i]; }
+  __syncthreads();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  double* ws = s_hw + (size_t)wave * (A.hoist_ws + A.hoist_tmp);
+  const int nItems = min(A.counts[list], A.es_it1);
+  if (nItems <= A.es_it0) return;
+  const int nslots = A.max_ext * A.T;
+  const long long units = (long long)(nItems - A.es_it0) * nslots;
+  const int waves = gridDim.x * (blockDim.x >> 6);
+  for (long long u = (long long)blockIdx.x * (blockDim.x >> 6) + wave; u < units; u += waves) {
+    const int it = A.es_it0 + (int)(u / nslots), e = (int)(u % nslots);
+    const int f = __builtin_amdgcn_readfirstlane(A.ext_fam[e]);
+    if (f < 0) continue;
+    const int item = __builtin_amdgcn_readfirstlane(A.items[list][it]);
+    const int site = item >> 3, cfg = item & 7;
+    const int r = A.ref[site];
+    int a1, a2;
+    item_alleles(A, site, cfg, r, &a1, &a2);
+    const int g11 = d_gi(a1, a1), g12 = d_gi(a1, a2), g22 = d_gi(a2, a2);
+    const bool denovo = A.denovo && cfg != 7;
+    const bool top = DN && cfg == 0 && !A.vcf;   // the de novo monomorphism item: one evaluation at f = 1
+    const uint8_t* pl = A.pl + (size_t)site * A.n_person * 10;
+    const int q = e / A.T, l = e - q * A.T;
+    double* out = A.es_coef + ((size_t)(it - A.es_it0) * A.max_ext + q) * A.poly_dcap * A.T + l;
+    if (DN && denovo) wave_poly_peel<10>(A, f, pl, s_lk, s_tba, s_T10, s_T10dn, g11, g12, g22, A.chrom, top, ws, lane, out, A.T);
+    else wave_poly_peel<3>(A, f, pl, s_lk, s_tba, s_T10, s_T10dn, g11, g12, g22, A.chrom, top, ws, lane, out, A.T);
+  }
+}
+
 template <int T, int S, int NUM, bool GEN>
 constexpr int brent_waves() { return (NUM == PM_NUM_POLY && !GEN && (T == 64 || T == 128) && S >= 8) ? PM_POLY_WAVES : 1; }
 
 // DN: lean polynomial kernel for autosomal --denovo (instantiated separately so the common kernel carries
 // no de novo hoisting code or register pressure).
 // PF: lean kernel whose items' genotype planes are prefetched into LDS (prefetch_planes); no other hoisting path.
-// EP: extended families in polynomial form (es_poly_hoist once per item, es_poly_eval per evaluation); the
+// EP: extended families in polynomial form (coefficients from k_es_hoist, es_poly_eval per evaluation); the
 // reference-order peel (d_es_lk) is compiled out, and the block asks for 2 waves per SIMD.
 template <int T, int S, int NUM, bool GEN, bool ES, bool DN = false, bool PF = false, bool EP = false>
 __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k_brent(DevArgs A, int list) {
@@ -1506,7 +1468,8 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
   if (pf) prefetch_planes(A, items, vb, nItems, s_pf);
   unsigned long long ev_acc = 0;   // evaluation count of this block's items: one atomic per block, at exit
   unsigned long long ph_h = 0, ph_e = 0, ph_n = 0, ph_t = 0;   // PM_PHASE_TIMING (A.phase): hoisting / evaluation split
-  for (int it = vb; it < nItems; it += gridDim.x) {
+  const int itEnd = min(nItems, A.es_it1);   // EP: this launch's chunk of the list [es_it0, es_it1)
+  for (int it = A.es_it0 + vb; it < itEnd; it += gridDim.x) {
     if (A.phase) ph_t = wall_clock64();
     const int item = items[it];
     const int site = item >> 3, cfg = item & 7;
@@ -1578,21 +1541,13 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
     constexpr int EPE = (EP && T == 64) ? PM_EPE : 0;
     double ce[EPE ? EPE : 1][EPE ? PDM + 1 : 1];
     int ed[EPE ? EPE : 1];
-    if constexpr (ES && EP) {   // polynomial form: the lane's extended families peeled once per item (es_poly_hoist)
+    // EP: the lane's extended families' coefficients, peeled for this item by k_es_hoist
+    const double* coef = (ES && EP) ? A.es_coef + (size_t)(it - A.es_it0) * A.max_ext * A.poly_dcap * T + threadIdx.x : nullptr;
+    if constexpr (ES && EP) {
       const int cnt = A.ext_count ? A.ext_count[threadIdx.x] : 0;
-      for (int q = 0; q < cnt; q++) {
-        const int f = A.ext_fam[q * T + threadIdx.x];
-        double* co = wsl + (size_t)(A.poly_coef + q * A.poly_dcap) * T;
-        int D;   // (the 10-state hoisting is compiled into the --denovo instantiation only: DN)
-        const bool top = cfg == 0 && !A.vcf;   // the de novo monomorphism item: one evaluation at f = 1
-        if constexpr (DN) D = I.denovo ? es_poly_hoist<10>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, wsl, T, co, top)
-                                       : es_poly_hoist<3>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, wsl, T, co, top);
-        else D = es_poly_hoist<3>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, wsl, T, co);
-        co[(size_t)(A.poly_dcap - 1) * T] = (double)D;
-      }
 #pragma unroll
       for (int q = 0; q < EPE; q++) {
-        const double* co = wsl + (size_t)(A.poly_coef + q * A.poly_dcap) * T;
+        const double* co = coef + (size_t)q * A.poly_dcap * T;
         ed[q] = q < cnt ? (int)co[(size_t)(A.poly_dcap - 1) * T] : -1;
         if (ed[q] > PDM) ed[q] = -1;
 #pragma unroll
@@ -1649,7 +1604,7 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
             if constexpr (EP) {
               if constexpr (EPE > 0)
                 if (q < EPE && ed[q] >= 0) continue;   // (evaluated from registers above)
-              const double* co = wsl + (size_t)(A.poly_coef + q * A.poly_dcap) * T;
+              const double* co = coef + (size_t)q * A.poly_dcap * T;
               v = es_poly_eval(co, T, (int)co[(size_t)(A.poly_dcap - 1) * T], x);
             } else {
               v = I.denovo  ? d_es_lk<10>(A, f, pl, s_lk, I.g11, I.g12, I.g22, I.chrom, x, -1, -1, wsl, T)
@@ -2509,17 +2464,23 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
 // families: one thread per (row, person), three (or ten) FillZeroPenetrance peels (:327-356) of the person's
 // family at the site's frequency, in the reference's operation order (d_es_lk).  Splitting the families'
 // persons over threads gives ten times the parallelism of a thread per (row, family).
-template <bool DN>
+// LDSWS: each thread's peel workspace (ws_per_lane doubles) in LDS, interleaved across the block's threads, instead
+// of the lane-interleaved HBM workspace: every partial / marriage-partial access of the 3 (10) peels per person
+// is then an LDS round trip (~100 cycles) rather than an HBM one (the HBM workspace of the whole grid does not fit
+// the caches: PMC showed 88% of wave cycles waiting).
+template <bool DN, bool LDSWS = false>
 __global__ void __launch_bounds__(256) k_posterior_es(DevArgs A) {
   __shared__ double s_lk[256];
   __shared__ double s_gq[101];
+  extern __shared__ double s_wsp[];
   for (int i = threadIdx.x; i < 256; i += blockDim.x) s_lk[i] = A.lktab[i];
   load_gq_thr(s_gq);
   __syncthreads();
   const long long work = (long long)A.counts[3] * A.n_es_pers;
-  const size_t gid_base = (size_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (size_t)gridDim.x * blockDim.x;
-  double* wsl = A.ws + gid_base;
-  for (long long gid = (long long)gid_base; gid < work; gid += (long long)stride) {
+  const size_t gid_base = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t stride = LDSWS ? (size_t)blockDim.x : (size_t)gridDim.x * blockDim.x;   // workspace stride
+  double* wsl = LDSWS ? s_wsp + threadIdx.x : A.ws + gid_base;
+  for (long long gid = (long long)gid_base; gid < work; gid += (long long)gridDim.x * blockDim.x) {
     const int row = (int)(gid / A.n_es_pers), e = A.es_pers[gid % A.n_es_pers];
     const int f = e >> 8, j = e & 255;
     const int site = A.row_site[row];
@@ -2708,10 +2669,20 @@ struct pm_engine {
   int *d_fam_founders = nullptr, *d_peel_start = nullptr, *d_ext_count = nullptr, *d_ext_fam = nullptr;
   int8_t* d_is_founder = nullptr;
   int2* d_steps = nullptr;
-  double *d_T10 = nullptr, *d_T10dn = nullptr, *d_ws = nullptr;
+  double *d_T10 = nullptr, *d_T10dn = nullptr, *d_ws = nullptr, *d_tba = nullptr;
   // ES polynomial form (PM_NUM_POLY): per-family layouts and per-step degrees (poly_layout)
   bool es_poly = false;
   int poly_ws = 0, poly_coef = 0, poly_dcap = 0;
+  int hoist_tmp = 0, hoist_waves = 4, es_chunk = 0;   // k_es_hoist: step temporaries per wave, waves per block, items per launch
+  double* d_es_coef = nullptr;                        // [es_chunk][max_ext][poly_dcap][T] hoisted coefficients
+  // the schedule compiler (es_jit.h): per plan (0, 1) and chromosome class, built on first use (0 untried, 1 ok, -1 failed)
+  std::vector<int> ext_fam_h, ext_fam1_h, peel_start_h;
+  std::vector<int2> steps_h;
+  std::vector<int8_t> founder_h;
+  std::vector<int> fam_founders_h;
+  pmjit::Kernel jit[2][4];
+  int jit_state[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+  int* d_jit_slots[2][4] = {{nullptr, nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr, nullptr}};   // e | sig | p0
   int *d_poly_start = nullptr, *d_poly_lay = nullptr, *d_poly_deg = nullptr;
   int *d_es_pers = nullptr, *d_es_pers1 = nullptr;   // (family << 8 | member) of peeled families: plan 0 / plan 1
   int n_es_pers = 0, n_es_pers1 = 0;
@@ -2804,45 +2775,10 @@ static bool plan_units(const pm_pedigree* ped, int T, int S, std::vector<int4>& 
   return true;
 }
 
-// Packs one extended family's ES_Peeling schedule for d_es_lk: marriage-partial slots are resolved the
-// way the reference's partial map behaves (created by the first type-1 step of a couple, looked up by
-// later type-2/3 steps, absent before that).  Returns the workspace doubles the family needs, -1 if it
-// cannot be packed (family larger than 255 members).
-static int pack_steps(const pm_pedigree* ped, int f, int ns, std::vector<int2>& out) {
-  const int p0 = ped->fam_start[f], n = ped->fam_start[f + 1] - p0;
-  if (n > 255 || !ped->peel_start || !ped->steps) return -1;
-  std::vector<std::pair<int, int>> keys;
-  auto find = [&](int a, int b) {
-    for (size_t i = 0; i < keys.size(); i++) if (keys[i].first == a && keys[i].second == b) return (int)i;
-    return -1;
-  };
-  for (int k = ped->peel_start[f]; k < ped->peel_start[f + 1]; k++) {
-    const pm_peel_step& S = ped->steps[k];
-    int slot = 255, create = 0, fa2mo = 0;
-    if (S.type == 1) {
-      int i = find(S.to0, S.to1);
-      if (i < 0) { i = (int)keys.size(); keys.push_back({S.to0, S.to1}); create = 1; }
-      slot = i;
-    } else if (S.type == 2) {
-      int a, b;
-      if (ped->sex[p0 + S.from0] == FEMALE) { a = S.to0; b = S.from0; fa2mo = 0; } else { a = S.from0; b = S.to0; fa2mo = 1; }
-      const int i = find(a, b);
-      slot = i < 0 ? 255 : i;
-    } else if (S.type == 3) {
-      const int i = find(S.from0, S.from1);
-      slot = i < 0 ? 255 : i;
-    } else return -1;
-    if (keys.size() > 254) return -1;
-    int2 e;
-    e.x = (S.type & 255) | ((S.from0 & 255) << 8) | ((S.from1 & 255) << 16) | ((S.to0 & 255) << 24);
-    e.y = (S.to1 & 255) | (slot << 8) | (create << 16) | (fa2mo << 17);
-    out.push_back(e);
-  }
-  if (ped->peel_start[f + 1] == ped->peel_start[f]) return -1;
-  return n * ns + (int)keys.size() * ns * ns;
-}
+// pack_steps: es_jit.cpp (pmjit::pack_steps), shared with the schedule compiler.
+using pmjit::pack_steps;
 
-// Layout of one family's peel in polynomial form (es_poly_hoist): for every chromosome class the degree each
+// Layout of one family's peel in polynomial form (k_es_hoist / wave_poly_peel): for every chromosome class the degree each
 // step combines (founders: 2; 1 for chrX/Y males and chrMT; 0 for chrY females), per slot the coefficient
 // capacity (largest degree + 1 over the classes), a temp region, and the likelihood's degree D.  Appends the
 // family's layout ints to lay and its steps' degree words to deg; returns the workspace doubles, -1 if a degree
@@ -2941,12 +2877,14 @@ void pm_engine_destroy(pm_engine* E) {
   if (!E) return;
   hipSetDevice(E->device);
   void* bufs[] = {E->d_units1, E->d_ext_count1, E->d_ext_fam1, E->d_fam_founders, E->d_peel_start, E->d_ext_count, E->d_ext_fam, E->d_is_founder, E->d_steps, E->d_T10,
-                  E->d_T10dn, E->d_ws, E->d_units_q, E->d_poly_start, E->d_poly_lay, E->d_poly_deg, E->d_es_pers, E->d_es_pers1,
+                  E->d_T10dn, E->d_ws, E->d_tba, E->d_units_q, E->d_poly_start, E->d_poly_lay, E->d_poly_deg, E->d_es_coef, E->d_es_pers, E->d_es_pers1,
                   E->d_fam_start, E->d_fam_kind, E->d_fa, E->d_mo, E->d_sex, E->d_units, E->d_lktab, E->d_M, E->d_syn,
                   E->d_pl, E->d_stage, E->d_ref, E->d_dm, E->d_res, E->d_calls, E->d_raw, E->d_minv, E->d_mono, E->d_evals,
                   E->d_items[0], E->d_items[1], E->d_items[2], E->d_counts, E->d_eval_total, E->d_row_site,
                   E->d_counters, E->d_row_blk};
   for (void* b : bufs) if (b) hipFree(b);
+  for (auto& pl : E->d_jit_slots)
+    for (int* b : pl) if (b) hipFree(b);
   for (auto& pr : E->brent_events) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
   if (E->ev0) hipEventDestroy(E->ev0);
   if (E->ev1) hipEventDestroy(E->ev1);
@@ -3113,6 +3051,26 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
       for (int c = 0; c < 4; c++) poly_d = std::max(poly_d, poly_lay[poly_start[f] + 2 + c]);
     }
     poly_start[ped->n_fam] = (int)poly_lay.size();
+    if (E->es_poly) {   // k_es_hoist temporaries: the largest step's out-of-place phases (wave_poly_peel)
+      const int ns = par->denovo ? 10 : 3;
+      for (size_t s = 0; s < steps.size(); s++)
+        for (int cls = 0; cls < 4; cls++) {
+          const int dg = poly_deg[s * 4 + cls], type = steps[s].x & 255;
+          const int a = dg & 127, b = (dg >> 7) & 127, c = (dg >> 14) & 127, e = (dg >> 21) & 127;
+          int need;
+          if (type == 1) need = ns * ns * (a + 1) + ns * ns * (a + b + 1);
+          else if (type == 2) need = ns * (a + b + 1) + ns * (a + b + c + 1);
+          else need = ns * ns * (a + b + c + 1) + ns * (a + b + c + 1) + ns * (a + b + c + e + 1);
+          E->hoist_tmp = std::max(E->hoist_tmp, need);
+        }
+      // 4 waves per block when their LDS slices fit, else fewer; none: the reference-order peel per evaluation
+      const size_t stat = (256 + 5 * 27 + (par->denovo ? 2000 : 2)) * sizeof(double);
+      const size_t per_wave = (size_t)(poly_w + E->hoist_tmp) * sizeof(double);
+      E->hoist_waves = 0;
+      for (int w = 4; w >= 1 && !E->hoist_waves; w--)
+        if (stat + per_wave * w <= 150 * 1024) E->hoist_waves = w;
+      if (!E->hoist_waves) E->es_poly = false;
+    }
     const int T = E->T;
     E->max_ext = (E->n_ext + T - 1) / T;
     std::vector<int> ext_count(T, 0), ext_fam((size_t)std::max(1, E->max_ext) * T, -1);
@@ -3141,6 +3099,11 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
     DALLOC(E->d_is_founder, ped->n_person);
     DALLOC(E->d_peel_start, ped->n_fam + 1);
     DALLOC(E->d_steps, std::max<size_t>(1, steps.size()));
+    E->ext_fam_h = ext_fam;
+    E->peel_start_h = peel_start;
+    E->steps_h = steps;
+    E->founder_h.assign(ped->is_founder, ped->is_founder + ped->n_person);
+    E->fam_founders_h = founders;
     DALLOC(E->d_ext_count, T);
     DALLOC(E->d_ext_fam, ext_fam.size());
     DALLOC(E->d_T10, 1000);
@@ -3154,6 +3117,8 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
     HIP_TRY(hipMemcpy(E->d_T10, T10.data(), sizeof(double) * 1000, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(E->d_T10dn, T10dn.data(), sizeof(double) * 1000, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_TBA), kTBA, sizeof(kTBA)));
+    DALLOC(E->d_tba, 5 * 27);
+    HIP_TRY(hipMemcpy(E->d_tba, kTBA, sizeof(kTBA), hipMemcpyHostToDevice));
     {   // GQ thresholds (d_gq): smallest double q in (0, 1] with int(-10 log10(q) + 0.5) <= k, by bisection on the
         // bit patterns of positive doubles (ordered like their values), with the host's glibc log10
       double thr[101];
@@ -3191,6 +3156,7 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
         int q1 = 0;
         for (int f = 0; f < ped->n_fam; f++)
           if (ped->fam_kind[f] != PM_FAM_FOUNDERS) { const int lane = q1 % E->T1; e1[(size_t)c1[lane]++ * E->T1 + lane] = f; q1++; }
+        E->ext_fam1_h = e1;
         DALLOC(E->d_units1, u1.size());
         DALLOC(E->d_ext_count1, E->T1);
         DALLOC(E->d_ext_fam1, e1.size());
@@ -3212,12 +3178,16 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
       HIP_TRY(hipMemcpy(E->d_poly_start, poly_start.data(), sizeof(int) * poly_start.size(), hipMemcpyHostToDevice));
       if (!poly_lay.empty()) HIP_TRY(hipMemcpy(E->d_poly_lay, poly_lay.data(), sizeof(int) * poly_lay.size(), hipMemcpyHostToDevice));
       if (!poly_deg.empty()) HIP_TRY(hipMemcpy(E->d_poly_deg, poly_deg.data(), sizeof(int) * poly_deg.size(), hipMemcpyHostToDevice));
+      // hoisted coefficients of a chunk of items: <= 1 GiB, at most every item a batch can enqueue in one list (4 per site)
+      const size_t per_item = (size_t)std::max({E->max_ext * E->T, E->max_ext1 * std::max(1, E->T1), 1}) * E->poly_dcap * sizeof(double);
+      E->es_chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)4 * std::max(1, max_batch), ((size_t)1 << 30) / per_item));
+      DALLOC(E->d_es_coef, (size_t)E->es_chunk * per_item / sizeof(double));
     }
     // workspace: the Brent grids and the posterior grid are capped so each needs <= 1 GiB
     E->grid_post = E->n_cu * 8;
     if (wsmax > 0) {
       const size_t cap = (size_t)1 << 30, per_lane = (size_t)wsmax * sizeof(double);
-      const size_t per_lane_b = (size_t)std::max(wsmax, E->es_poly ? E->poly_ws : 0) * sizeof(double);   // Brent grids
+      const size_t per_lane_b = (size_t)wsmax * sizeof(double);   // Brent grids (EP kernels use no workspace: k_es_hoist)
       E->grid_brent = (int)std::max<size_t>(E->n_cu, std::min<size_t>(E->grid_brent, cap / (per_lane_b * T)));
       E->grid_brent -= E->grid_brent % 8;   // keep the XCD-aware item order exact
       if (E->T1) {
@@ -3330,6 +3300,8 @@ static DevArgs make_args(pm_engine* E, int n, const uint8_t* pl, const uint32_t*
   A.es_poly = 0;   // set per Brent launch (launch_brent)
   A.poly_start = E->d_poly_start; A.poly_lay = E->d_poly_lay; A.poly_deg = E->d_poly_deg;
   A.poly_coef = E->poly_coef; A.poly_dcap = E->poly_dcap;
+  A.es_coef = E->d_es_coef; A.es_it0 = 0; A.es_it1 = INT_MAX; A.max_ext = E->use_plan1 ? E->max_ext1 : E->max_ext;
+  A.hoist_ws = E->poly_coef; A.hoist_tmp = E->hoist_tmp;
   A.es_pers = E->use_plan1 ? E->d_es_pers1 : E->d_es_pers;
   A.n_es_pers = E->use_plan1 ? E->n_es_pers1 : E->n_es_pers;
   A.theta_one = 1.0;
@@ -3405,6 +3377,44 @@ static BrentFn brent_kernel(int T, int S, int num, bool gen, bool es, bool dn = 
   return nullptr;
 }
 
+// The schedule compiler's kernels for the current plan and chromosome class (es_jit.h), built on first use; nullptr
+// when it is off (PM_NO_JIT) or failed to build (then the generic k_es_hoist / k_posterior_es run).
+static const pmjit::Kernel* jit_kernel(pm_engine* E) {
+  const int plan = E->use_plan1 ? 1 : 0, cls = E->chrom;
+  if (!E->es_poly || getenv("PM_NO_JIT")) return nullptr;
+  int& st = E->jit_state[plan][cls];
+  if (st == 0) {
+    st = -1;
+    const std::vector<int>& ef = plan ? E->ext_fam1_h : E->ext_fam_h;
+    std::vector<pmjit::Family> fams;
+    for (size_t e = 0; e < ef.size(); e++) {
+      const int f = ef[e];
+      if (f < 0) continue;
+      pmjit::Family F;
+      F.e = (int)e;
+      F.p0 = E->fam_start_h[f];
+      F.n = E->fam_start_h[f + 1] - F.p0;
+      F.nf = E->fam_founders_h[f];
+      F.sex.assign(E->sex_h.begin() + F.p0, E->sex_h.begin() + F.p0 + F.n);
+      F.founder.assign(E->founder_h.begin() + F.p0, E->founder_h.begin() + F.p0 + F.n);
+      F.steps.assign(E->steps_h.begin() + E->peel_start_h[f], E->steps_h.begin() + E->peel_start_h[f + 1]);
+      fams.push_back(F);
+    }
+    std::string err;
+    pmjit::Kernel& K = E->jit[plan][cls];
+    if (!fams.empty() && pmjit::build(E->device, cls, fams, kTBA, E->par.denovo != 0, &K, &err)) {
+      const size_t ns = K.slot_e.size();
+      std::vector<int> tab(3 * ns);
+      for (size_t i = 0; i < ns; i++) { tab[i] = K.slot_e[i]; tab[ns + i] = K.slot_sig[i]; tab[2 * ns + i] = K.slot_p0[i]; }
+      if (dalloc(&E->d_jit_slots[plan][cls], tab.size()) == PM_OK &&
+          hipMemcpy(E->d_jit_slots[plan][cls], tab.data(), sizeof(int) * tab.size(), hipMemcpyHostToDevice) == hipSuccess)
+        st = 1;
+    } else if (!fams.empty())
+      fprintf(stderr, "polymutt: peeling-schedule compiler unavailable (%s); using the generic hoisting kernel\n", err.c_str());
+  }
+  return st == 1 ? &E->jit[plan][cls] : nullptr;
+}
+
 static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelated = false) {
   DevArgs A = A0;
   int T = E->T, S = E->S, grid = E->grid_brent;
@@ -3449,9 +3459,8 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
   // Elston-Stewart workspace in LDS: every partial / marriage-partial access of the peel becomes an LDS round
   // trip instead of an L2 one.  Blocks per CU follow from the LDS budget (160 KB per CU).
   A.ws_lds = 0;
-  if (ep) {   // polynomial-form peels (HBM workspace)
+  if (ep) {   // polynomial-form peels: coefficients from k_es_hoist, no workspace in k_brent
     A.es_poly = 1;
-    A.ws_per_lane = std::max(E->ws_per_lane, E->poly_ws);
   } else if (!unrelated && n_ext > 0 && !E->par.denovo) {   // BA peels (the 10-state one is too big)
     const size_t need = (size_t)E->ws_per_lane * T * sizeof(double);
     if (need > 0 && need <= 150 * 1024) {
@@ -3466,7 +3475,40 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
   HIP_TRY(hipEventCreate(&a));
   HIP_TRY(hipEventCreate(&b));
   HIP_TRY(hipEventRecord(a, E->stream));
-  hipLaunchKernelGGL(fn, dim3(grid), dim3(T), shmem, E->stream, A, list);
+  if (ep) {   // chunks of the list (the coefficient buffer holds es_chunk items): k_es_hoist, then the chunk's Brent items
+    void (*hoist)(DevArgs, int) = A.denovo ? k_es_hoist<true> : k_es_hoist<false>;
+    const size_t hlds = (size_t)E->hoist_waves * (E->poly_coef + E->hoist_tmp) * sizeof(double);
+    if (hlds > 64 * 1024) HIP_TRY(hipFuncSetAttribute((const void*)hoist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hlds));
+    const size_t stat = (256 + 5 * 27 + (A.denovo ? 2000 : 2)) * sizeof(double);
+    const int hgrid = E->n_cu * std::max(1, std::min(8, (int)((160 * 1024) / (hlds + stat))));
+    const int max_items = 4 * E->last_n;
+    const pmjit::Kernel* K = jit_kernel(E);
+    for (int it0 = 0; it0 < max_items; it0 += E->es_chunk) {
+      A.es_it0 = it0;
+      A.es_it1 = (int)std::min<long long>((long long)it0 + E->es_chunk, INT_MAX);
+      if (K) {   // compiled schedule: one thread (--denovo: one wave) per (item, family)
+        const int plan = E->use_plan1 ? 1 : 0, ns = (int)K->slot_e.size();
+        const int* tab = E->d_jit_slots[plan][E->chrom];
+        pmjit::Args J;
+        J.items = A.items[list]; J.counts = A.counts; J.ref = A.ref; J.res = (const int*)A.res; J.pl = A.pl; J.lktab = A.lktab;
+        J.coef = A.es_coef; J.slot_e = tab; J.slot_sig = tab + ns; J.slot_p0 = tab + 2 * ns;
+        J.T10 = E->d_T10; J.T10dn = E->d_T10dn; J.tba = E->d_tba;
+        J.list = list; J.it0 = A.es_it0; J.it1 = A.es_it1; J.nslots = ns; J.np = A.n_person; J.T = A.T; J.max_ext = A.max_ext;
+        J.dcap = A.poly_dcap; J.vcf = A.vcf; J.res_words = sizeof(pm_site_result) / 4;
+        J.res_a1 = offsetof(pm_site_result, allele1) / 4; J.res_a2 = offsetof(pm_site_result, allele2) / 4;
+        J.denovo = A.denovo;
+        void* params[] = {&J};
+        if (K->wave)
+          HIP_TRY(hipModuleLaunchKernel(K->fn, E->n_cu * std::max(1, 16 / K->wpb), 1, 1, 64 * K->wpb, 1, 1, 0, E->stream, params, nullptr));
+        else HIP_TRY(hipModuleLaunchKernel(K->fn, E->n_cu * 8, 1, 1, 256, 1, 1, 0, E->stream, params, nullptr));
+      } else hipLaunchKernelGGL(hoist, dim3(hgrid), dim3(64 * E->hoist_waves), hlds, E->stream, A, list);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(fn, dim3(grid), dim3(T), shmem, E->stream, A, list);
+      HIP_TRY(hipGetLastError());
+    }
+  } else {
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(T), shmem, E->stream, A, list);
+  }
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(b, E->stream));
   E->brent_events.push_back({a, b});
@@ -3531,9 +3573,36 @@ static int run_pipeline(pm_engine* E, int n, const uint8_t* pl, const uint32_t* 
     void (*post)(DevArgs) = E->par.denovo ? (es ? k_posterior<true, true> : k_posterior<true, false>)
                           : es ? k_posterior<false, true> : lean ? k_posterior<false, false, true> : k_posterior<false, false>;
     hipLaunchKernelGGL(post, dim3(E->grid_post), dim3(256), 0, E->stream, A);
-    if (es && A.n_es_pers > 0) {
+    const pmjit::Kernel* K = es && A.n_es_pers > 0 ? jit_kernel(E) : nullptr;
+    if (K && K->fn_post) {   // compiled schedule: one thread per (row, peeled family), all its persons' 3 peels in registers
       HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(E->par.denovo ? k_posterior_es<true> : k_posterior_es<false>, dim3(E->grid_post), dim3(256), 0, E->stream, A);
+      const int plan = E->use_plan1 ? 1 : 0, ns = (int)K->slot_e.size();
+      const int* tab = E->d_jit_slots[plan][E->chrom];
+      void* thr = nullptr;
+      HIP_TRY(hipGetSymbolAddress(&thr, HIP_SYMBOL(c_gq_thr)));
+      pmjit::PostArgs P;
+      P.counts = A.counts; P.row_site = A.row_site; P.res = (const char*)A.res; P.pl = A.pl; P.lktab = A.lktab;
+      P.gq_thr = (const double*)thr; P.calls = (void*)A.calls; P.fam_p0 = tab + 2 * ns; P.fam_sig = tab + ns;
+      P.nfams = ns; P.np = A.n_person; P.vcf = A.vcf; P.res_bytes = sizeof(pm_site_result);
+      P.off_a1 = offsetof(pm_site_result, allele1); P.off_a2 = offsetof(pm_site_result, allele2);
+      P.off_maxidx = offsetof(pm_site_result, maxidx); P.off_af = offsetof(pm_site_result, af);
+      P.theta = A.theta;
+      void* params[] = {&P};
+      HIP_TRY(hipModuleLaunchKernel(K->fn_post, E->n_cu * 8, 1, 1, 256, 1, 1, 0, E->stream, params, nullptr));
+    } else if (es && A.n_es_pers > 0) {
+      HIP_TRY(hipGetLastError());
+      // LDS workspace when a 64-thread block's share fits: the block size is the largest of 256/128/64 whose
+      // workspace stays within the 64 KB default dynamic-LDS limit
+      const size_t per = (size_t)E->ws_per_lane * sizeof(double);
+      int bt = 0;
+      for (int t : {256, 128, 64})
+        if (!bt && per * t <= 64 * 1024 && !getenv("PM_ES_POST_HBM")) bt = t;
+      if (bt) {
+        const int per_cu = std::max(1, (int)((160 * 1024) / (per * bt + 3 * 1024)));
+        void (*pe)(DevArgs) = E->par.denovo ? k_posterior_es<true, true> : k_posterior_es<false, true>;
+        hipLaunchKernelGGL(pe, dim3(E->n_cu * per_cu * 2), dim3(bt), per * bt, E->stream, A);
+      } else
+        hipLaunchKernelGGL(E->par.denovo ? k_posterior_es<true> : k_posterior_es<false>, dim3(E->grid_post), dim3(256), 0, E->stream, A);
     }
   }
   HIP_TRY(hipGetLastError());

@@ -1,0 +1,850 @@
+// es_jit.cpp -- see es_jit.h.
+#include "es_jit.h"
+#include <hip/hiprtc.h>
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include "../../include/polymutt_engine.h"
+
+namespace pmjit {
+namespace {
+
+constexpr int MALE = 1, FEMALE = 2;
+
+// A homogeneous polynomial in (f, g = 1 - f) of degree d: coefficient names c[a] of f^a g^(d - a) ("" = zero).
+struct Poly {
+  int d = 0;
+  std::vector<std::string> c;
+};
+
+std::string lit(double x) {   // exact hexadecimal literal
+  char b[64];
+  snprintf(b, sizeof b, "%a", x);
+  return b;
+}
+
+struct Gen {
+  std::string code;
+  int nv = 0;
+  std::map<std::string, std::string> memo;   // expression -> value: identical computations share one value
+  std::string def(const std::string& expr) {
+    auto it = memo.find(expr);
+    if (it != memo.end()) return it->second;
+    std::string v = "v" + std::to_string(nv++);
+    code += "  const double " + v + " = " + expr + ";\n";
+    memo[expr] = v;
+    return v;
+  }
+  // acc + x * y (acc empty: x * y); "1" factors elided
+  std::string mac(const std::string& acc, const std::string& x, const std::string& y) {
+    const bool x1 = x == "1.0", y1 = y == "1.0";
+    const std::string prod = x1 ? y : y1 ? x : "";
+    if (acc.empty()) return prod.empty() ? def(x + " * " + y) : prod;
+    if (!prod.empty()) return def(acc + " + " + prod);
+    return def("fma(" + x + ", " + y + ", " + acc + ")");
+  }
+  Poly zero(int d) { Poly p; p.d = d; p.c.assign(d + 1, ""); return p; }
+  Poly mul(const Poly& A, const Poly& B) {
+    Poly R = zero(A.d + B.d);
+    for (int a = 0; a <= R.d; a++)
+      for (int u = std::max(0, a - B.d); u <= std::min(a, A.d); u++)
+        if (!A.c[u].empty() && !B.c[a - u].empty()) R.c[a] = mac(R.c[a], A.c[u], B.c[a - u]);
+    return R;
+  }
+  // sum_t w_t P_t (all of degree d)
+  Poly lincomb(const std::vector<std::pair<double, const Poly*>>& terms, int d) {
+    Poly R = zero(d);
+    for (int a = 0; a <= d; a++)
+      for (auto& t : terms) {
+        if (t.first == 0.0 || t.second->c[a].empty()) continue;
+        R.c[a] = mac(R.c[a], t.first == 1.0 ? std::string("1.0") : lit(t.first), t.second->c[a]);
+      }
+    return R;
+  }
+  Poly add(const Poly& A, const Poly& B) {   // same degree
+    Poly R = zero(A.d);
+    for (int a = 0; a <= A.d; a++) {
+      if (A.c[a].empty()) R.c[a] = B.c[a];
+      else if (B.c[a].empty()) R.c[a] = A.c[a];
+      else R.c[a] = def(A.c[a] + " + " + B.c[a]);
+    }
+    return R;
+  }
+};
+
+// transmission_BA of the class for an offspring of sex csex (GetTransmissionProb_BA :1059-1075)
+double tba(const double (*T)[27], int chrom, int csex, int i, int j, int k) {
+  const int o = i * 9 + j * 3 + k;
+  if (chrom == PM_CHR_X) return csex == MALE ? T[2][o] : T[1][o];
+  if (chrom == PM_CHR_Y) return csex == MALE ? T[3][o] : 1.0;
+  if (chrom == PM_CHR_MT) return T[4][o];
+  return T[0][o];
+}
+
+// the shape key: everything the generated code depends on
+std::string shape_key(const Family& F) {
+  std::string k = std::to_string(F.n) + ":" + std::to_string(F.nf) + ":";
+  for (int i = 0; i < F.n; i++) {
+    k += F.founder[i] ? 'F' : 'o';
+    k += (char)('0' + F.sex[i]);   // (child sex of the X/Y transmission, chrY females)
+  }
+  for (auto& s : F.steps) k += ":" + std::to_string(s.x) + "," + std::to_string(s.y);
+  return k;
+}
+
+// One family shape's hoisting as a device function: the polynomial of FamilyLikelihoodES' BA peel in (f, g).
+std::string gen_family(const Family& F, int chrom, const double (*T)[27], const std::string& name) {
+  Gen G;
+  const int n = F.n;
+  const bool X = chrom == PM_CHR_X, Y = chrom == PM_CHR_Y, MT = chrom == PM_CHR_MT;
+  std::map<std::pair<int, int>, std::string> pen;   // (person, state) -> loaded likelihood
+  auto penv = [&](int i, int j) {
+    auto key = std::make_pair(i, j);
+    auto it = pen.find(key);
+    if (it != pen.end()) return it->second;
+    static const char* plane[3] = {"P11", "P12", "P22"};
+    std::string v = G.def(std::string("lk[") + plane[j] + "[p0 + " + std::to_string(i) + "]]");
+    pen[key] = v;
+    return v;
+  };
+  // InitializePartials_BA x SetFounderPriors_BA (:1449-1465, :666-687)
+  std::vector<std::vector<Poly>> P(n, std::vector<Poly>(3));
+  for (int i = 0; i < n; i++) {
+    const int sx = F.sex[i];
+    const bool fo = F.founder[i] && i < F.nf;
+    const bool yf = Y && sx == FEMALE;
+    const int d = !fo ? 0 : yf ? 0 : (((X || Y) && sx == MALE) || MT) ? 1 : 2;
+    for (int j = 0; j < 3; j++) {
+      Poly p = G.zero(d);
+      if (yf) p.c[0] = "1.0";
+      else if (!fo) p.c[0] = penv(i, j);
+      else if (d == 2) p.c[2 - j] = j == 1 ? G.def("2.0 * " + penv(i, j)) : penv(i, j);   // f^2, 2fg, g^2
+      else if (j != 1) p.c[j == 0 ? 1 : 0] = penv(i, j);                                    // f, 0, g
+      P[i][j] = p;
+    }
+  }
+  std::map<int, std::vector<Poly>> M;   // marriage partials by slot: [i * 3 + j]
+  int fin = -1;
+  for (const int2& S : F.steps) {
+    const int type = S.x & 255, from0 = (S.x >> 8) & 255, from1 = (S.x >> 16) & 255, to0 = (S.x >> 24) & 255;
+    const int slot = (S.y >> 8) & 255, create = (S.y >> 16) & 1, fa2mo = (S.y >> 17) & 1;
+    fin = to0;
+    if (type == 1) {   // peelOffspring2Parents_BA (:1105-1130): M(i, j) *= sum_k T(i, j, k) P_off[k]
+      const int off = from0, csex = F.sex[off], da = P[off][0].d;
+      std::vector<Poly> Sij(9);
+      for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+          std::vector<std::pair<double, const Poly*>> t;
+          for (int k = 0; k < 3; k++) t.push_back({tba(T, chrom, csex, i, j, k), &P[off][k]});
+          Sij[i * 3 + j] = G.lincomb(t, da);
+        }
+      if (create || !M.count(slot)) M[slot] = Sij;
+      else
+        for (int e = 0; e < 9; e++) M[slot][e] = G.mul(M[slot][e], Sij[e]);
+    } else if (type == 2) {   // peelSpouse2Spouse_BA (:1182-1230): P_to[i] *= sum_j P_from[j] M(j, i)
+      const int sf = from0, stt = to0;
+      for (int i = 0; i < 3; i++) {
+        Poly sum;
+        bool first = true;
+        for (int j = 0; j < 3; j++) {
+          Poly term = slot == 255 ? P[sf][j] : G.mul(P[sf][j], M[slot][fa2mo ? j * 3 + i : i * 3 + j]);
+          sum = first ? term : G.add(sum, term);
+          first = false;
+        }
+        P[stt][i] = G.mul(P[stt][i], sum);
+      }
+    } else {   // peelParents2Offspring_BA (:1260-1286): P_off[k] *= sum_ij P_fa[i] M(i, j) P_mo[j] T(i, j, k)
+      const int fa = from0, mo = from1, off = to0, csex = F.sex[off];
+      std::vector<Poly> W(9);
+      for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+          const Poly fm = slot == 255 ? P[fa][i] : G.mul(P[fa][i], M[slot][i * 3 + j]);
+          W[i * 3 + j] = G.mul(fm, P[mo][j]);
+        }
+      for (int k = 0; k < 3; k++) {
+        std::vector<std::pair<double, const Poly*>> t;
+        for (int e = 0; e < 9; e++) t.push_back({tba(T, chrom, csex, e / 3, e % 3, k), &W[e]});
+        const Poly Sk = G.lincomb(t, W[0].d);
+        P[off][k] = G.mul(P[off][k], Sk);
+      }
+    }
+  }
+  // CalculateLikelihood_BA (:1013-1032): the final person's partials summed
+  Poly L = G.add(G.add(P[fin][0], P[fin][1]), P[fin][2]);
+  std::string out = "__device__ __attribute__((noinline)) void " + name +
+                    "(const unsigned char* __restrict__ P11, const unsigned char* __restrict__ P12, "
+                    "const unsigned char* __restrict__ P22, int p0, const double* __restrict__ lk, double* __restrict__ out, "
+                    "int os, int dcap) {\n" + G.code;
+  for (int a = 0; a <= L.d; a++) out += "  out[" + std::to_string(a) + " * os] = " + (L.c[a].empty() ? "0.0" : L.c[a]) + ";\n";
+  out += "  out[(dcap - 1) * os] = " + std::to_string(L.d) + ".0;\n}\n";
+  return out;
+}
+
+const char* kPrologue = R"(
+typedef unsigned char uint8_t;
+struct Args {
+  const int* items; const int* counts; const uint8_t* ref; const int* res; const uint8_t* pl; const double* lktab;
+  double* coef; const int* slot_e; const int* slot_sig; const int* slot_p0;
+  const double* T10; const double* T10dn; const double* tba;
+  int list, it0, it1, nslots, np, T, max_ext, dcap, vcf, res_words, res_a1, res_a2, denovo;
+};
+__device__ __forceinline__ int gi(int b1, int b2) {
+  return b1 < b2 ? (b1 - 1) * (10 - b1) / 2 + (b2 - b1) : (b2 - 1) * (10 - b2) / 2 + (b1 - b2);
+}
+__device__ __forceinline__ void cfg_alleles(int cfg, int r, int* a1, int* a2) {   // main.cpp:458-529, PedigreeGLF.h:14-53
+  const int ts = r == 1 ? 3 : r == 2 ? 4 : r == 3 ? 1 : 2, tv1 = (r == 1 || r == 3) ? 2 : 1, tv2 = (r == 1 || r == 3) ? 4 : 3;
+  switch (cfg) {
+    case 0: *a1 = r; *a2 = (r == 4) ? 3 : r + 1; break;
+    case 1: *a1 = r; *a2 = ts; break;
+    case 2: *a1 = r; *a2 = tv1; break;
+    case 3: *a1 = r; *a2 = tv2; break;
+    case 4: *a1 = ts; *a2 = tv1; break;
+    case 5: *a1 = ts; *a2 = tv2; break;
+    default: *a1 = tv1; *a2 = tv2; break;
+  }
+}
+)";
+
+std::string gen_kernel(const std::vector<std::string>& shapes) {
+  std::string s = R"(
+extern "C" __global__ void __launch_bounds__(256) es_hoist_jit(Args A) {
+  __shared__ double lk[256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) lk[i] = A.lktab[i];
+  __syncthreads();
+  const int nItems = min(A.counts[A.list], A.it1);
+  if (nItems <= A.it0) return;
+  const long long units = (long long)(nItems - A.it0) * A.nslots;
+  for (long long u = (long long)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += (long long)gridDim.x * blockDim.x) {
+    const int uq = (int)(u / A.nslots), k = (int)(u - (long long)uq * A.nslots);
+    const int it = A.it0 + uq;
+    const int item = A.items[it];
+    const int site = item >> 3, cfg = item & 7, r = A.ref[site];
+    int a1, a2;
+    if (A.vcf) { a1 = r & 15; a2 = r >> 4; }
+    else if (cfg == 7) { a1 = A.res[(size_t)site * A.res_words + A.res_a1]; a2 = A.res[(size_t)site * A.res_words + A.res_a2]; }
+    else cfg_alleles(cfg, r, &a1, &a2);
+    const uint8_t* pl = A.pl + (size_t)site * A.np * 10;
+    const uint8_t* P11 = pl + (size_t)gi(a1, a1) * A.np;
+    const uint8_t* P12 = pl + (size_t)gi(a1, a2) * A.np;
+    const uint8_t* P22 = pl + (size_t)gi(a2, a2) * A.np;
+    const int e = A.slot_e[k], q = e / A.T;
+    double* out = A.coef + ((size_t)uq * A.max_ext + q) * A.dcap * A.T + (e - q * A.T);
+    switch (A.slot_sig[k]) {
+)";
+  for (size_t i = 0; i < shapes.size(); i++)
+    s += "      case " + std::to_string(i) + ": " + shapes[i] + "(P11, P12, P22, A.slot_p0[k], lk, out, A.T, A.dcap); break;\n";
+  s += "    }\n  }\n}\n";
+  return s;
+}
+
+
+// ---------------------------------------------------------------------------------------------------------------
+// Genotype posteriors of one family shape (CalcPostProb_SingleExtendedPed_BA, FamilyLikelihoodSeq.cpp:171-216): for
+// every person j and genotype s, the reference-order numeric BA peel at freq with j's penetrances zeroed but for s
+// (FillZeroPenetrance :327-356).  The operations and their order are d_es_lk<3>'s (engine.hip), hence the
+// reference's, term by term; folding x * 1 -> x, dropping + 0 and 0-products (every value is finite and >= 0) keeps
+// every bit.  Computations that do not depend on j's zeroed penetrance are generated once (Gen::def memo), so the 3n
+// peels of a family share their common prefix.
+struct NumPeel {
+  Gen& G;
+  explicit NumPeel(Gen& g) : G(g) {}
+  static bool is0(const std::string& x) { return x == "0.0"; }
+  std::string mul(const std::string& x, const std::string& y) {
+    if (is0(x) || is0(y)) return "0.0";
+    if (x == "1.0") return y;
+    if (y == "1.0") return x;
+    return G.def(x + " * " + y);
+  }
+  std::string add(const std::string& acc, const std::string& x) {   // acc + x, acc "" = the sum's 0.0 start
+    if (acc.empty()) return x;
+    if (is0(x)) return acc;
+    if (is0(acc)) return x;
+    return G.def(acc + " + " + x);
+  }
+};
+
+std::string gen_post_family(const Family& F, int chrom, const double (*T)[27], const std::string& name) {
+  Gen G;
+  NumPeel N(G);
+  const int n = F.n;
+  const bool X = chrom == PM_CHR_X, Y = chrom == PM_CHR_Y, MT = chrom == PM_CHR_MT;
+  static const char* plane[3] = {"P11", "P12", "P22"};
+  std::string body;
+  // founder priors (d_es_lk: pr[] per founder, same expressions)
+  const std::string q0 = G.def("fq * fq"), q1 = G.def("2 * fq * (1 - fq)"), q2 = G.def("(1 - fq) * (1 - fq)");
+  const std::string h0 = "fq", h2 = G.def("1 - fq");
+  std::vector<std::vector<std::string>> pen(n, std::vector<std::string>(3));
+  for (int i = 0; i < n; i++)
+    for (int s = 0; s < 3; s++) pen[i][s] = G.def(std::string("lk[") + plane[s] + "[p0 + " + std::to_string(i) + "]]");
+  auto peel = [&](int zp, int zs) {
+    std::vector<std::vector<std::string>> P(n, std::vector<std::string>(3));
+    for (int i = 0; i < n; i++) {
+      const int sx = F.sex[i];
+      const bool fo = F.founder[i] != 0;
+      std::string pr[3] = {"0.0", "0.0", "0.0"};
+      if (i < F.nf) {
+        pr[0] = q0; pr[1] = q1; pr[2] = q2;
+        if (X && sx == MALE) { pr[0] = h0; pr[1] = "0.0"; pr[2] = h2; }
+        if (Y) { if (sx == MALE) { pr[0] = h0; pr[1] = "0.0"; pr[2] = h2; } else { pr[0] = pr[1] = pr[2] = "1.0"; } }
+        if (MT) { pr[0] = h0; pr[1] = "0.0"; pr[2] = h2; }
+      }
+      for (int s = 0; s < 3; s++) {
+        const std::string pe = (zp == i && s != zs) ? std::string("0.0") : pen[i][s];
+        P[i][s] = (Y && sx == FEMALE) ? std::string("1.0") : (fo ? N.mul(pr[s], pe) : pe);
+      }
+    }
+    std::map<int, std::vector<std::string>> M;
+    int fin = -1;
+    for (const int2& S : F.steps) {
+      const int type = S.x & 255, from0 = (S.x >> 8) & 255, from1 = (S.x >> 16) & 255, to0 = (S.x >> 24) & 255;
+      const int slot = (S.y >> 8) & 255, create = (S.y >> 16) & 1, fa2mo = (S.y >> 17) & 1;
+      fin = to0;
+      if (type == 1) {
+        const int off = from0, csex = F.sex[off];
+        if (create || !M.count(slot)) M[slot].assign(9, "1.0");
+        for (int i = 0; i < 3; i++)
+          for (int j = 0; j < 3; j++) {
+            std::string sum;
+            for (int k = 0; k < 3; k++) {
+              const double t = tba(T, chrom, csex, i, j, k);
+              sum = N.add(sum, t == 0.0 ? std::string("0.0") : N.mul(t == 1.0 ? std::string("1.0") : lit(t), P[off][k]));
+            }
+            M[slot][i * 3 + j] = N.mul(M[slot][i * 3 + j], sum.empty() ? std::string("0.0") : sum);
+          }
+      } else if (type == 2) {
+        const int sf = from0, stt = to0;
+        for (int i = 0; i < 3; i++) {
+          std::string sum;
+          for (int j = 0; j < 3; j++) {
+            if (slot == 255) sum = N.add(sum, P[sf][j]);
+            else sum = N.add(sum, N.mul(P[sf][j], M[slot][fa2mo ? j * 3 + i : i * 3 + j]));
+          }
+          P[stt][i] = N.mul(P[stt][i], sum.empty() ? std::string("0.0") : sum);
+        }
+      } else {
+        const int fa = from0, mo = from1, off = to0, csex = F.sex[off];
+        std::string sum[3];
+        for (int i = 0; i < 3; i++)
+          for (int j = 0; j < 3; j++) {
+            const std::string w = slot == 255 ? N.mul(P[fa][i], P[mo][j]) : N.mul(N.mul(P[fa][i], M[slot][i * 3 + j]), P[mo][j]);
+            for (int k = 0; k < 3; k++) {
+              const double t = tba(T, chrom, csex, i, j, k);
+              sum[k] = N.add(sum[k], t == 0.0 ? std::string("0.0") : N.mul(t == 1.0 ? std::string("1.0") : lit(t), w));
+            }
+          }
+        for (int k = 0; k < 3; k++) P[off][k] = N.mul(P[off][k], sum[k].empty() ? std::string("0.0") : sum[k]);
+      }
+    }
+    std::string L;
+    for (int i = 0; i < 3; i++) L = N.add(L, P[fin][i]);
+    return L.empty() ? std::string("0.0") : L;
+  };
+  for (int j = 0; j < n; j++) {
+    const int sx = F.sex[j];
+    if (Y && sx == FEMALE) {   // CalcPostProb_SingleExtendedPed_BA: chrY females get no posterior ('.')
+      body += "  emit(calls, out0 + p0 + " + std::to_string(j) + ", 0.0, 0.0, 0.0, " + std::to_string((int)PM_LBL_DOT) +
+              ", thr, vcf, 1);\n";
+      continue;
+    }
+    const std::string l0 = peel(j, 0), l1 = peel(j, 1), l2 = peel(j, 2);
+    const int lab = (Y || MT || (X && sx == MALE)) ? PM_LBL_VCF_HAPLOID : PM_LBL_VCF_DIPLOID;   // d_vcf_label
+    body += "  emit(calls, out0 + p0 + " + std::to_string(j) + ", " + l0 + ", " + l1 + ", " + l2 + ", " + std::to_string(lab) +
+            ", thr, vcf, 0);\n";
+  }
+  return "__device__ __attribute__((noinline)) void " + name +
+         "(const unsigned char* __restrict__ P11, const unsigned char* __restrict__ P12, const unsigned char* __restrict__ P22, "
+         "int p0, const double* __restrict__ lk, double fq, const double* __restrict__ thr, void* calls, size_t out0, int vcf) {\n" +
+         G.code + body + "}\n";
+}
+
+const char* kPostPrologue = R"(
+struct PostArgs {
+  const int* counts; const int* row_site; const char* res; const uint8_t* pl; const double* lktab; const double* gq_thr;
+  void* calls; const int* fam_p0; const int* fam_sig;
+  int nfams, np, vcf, res_bytes, off_a1, off_a2, off_maxidx, off_af;
+  double theta;
+};
+struct GenoCall { double dosage; short best; short gq; signed char label; signed char pad[3]; };
+struct VcfCall { signed char best; signed char gq; signed char label; signed char pad; };
+// d_gq (engine.hip): GQ of OutputVCF :1818-1820 from the host's glibc thresholds, exact for every double
+__device__ __forceinline__ int gq_of(double pb, const double* thr) {
+  if (pb > 0.9999999999) return 100;
+  const double q = 1. - pb;
+  int k = (int)(-10.0f * log10f((float)q) + 0.5f);
+  k = k < 0 ? 0 : k > 100 ? 100 : k;
+  while (k < 100 && q < thr[k]) k++;
+  while (k > 0 && q >= thr[k - 1]) k--;
+  return k;
+}
+// k_posterior_es's tail: post = l / sum, best = d_best3(l), GQ of post[best], DS = post12 + 2 post22
+__device__ __forceinline__ void emit(void* calls, size_t idx, double l11, double l12, double l22, int label, const double* thr,
+                                     int vcf, int zero) {
+  double post[3] = {0.0, 0.0, 0.0};
+  int best = 0;
+  if (!zero) {
+    const double sum = l11 + l12 + l22;
+    if (sum != 0) { post[0] = l11 / sum; post[1] = l12 / sum; post[2] = l22 / sum; }
+    double m = l11;
+    if (l12 > m) { m = l12; best = 1; }
+    if (l22 > m) { m = l22; best = 2; }
+  }
+  const int gq = gq_of(post[best], thr);
+  if (vcf) {
+    VcfCall c; c.best = (signed char)best; c.gq = (signed char)gq; c.label = (signed char)label; c.pad = 0;
+    ((VcfCall*)calls)[idx] = c;
+    return;
+  }
+  GenoCall c; c.dosage = post[1] + post[2] * 2; c.best = (short)best; c.gq = (short)gq; c.label = (signed char)label;
+  c.pad[0] = c.pad[1] = c.pad[2] = 0;
+  ((GenoCall*)calls)[idx] = c;
+}
+)";
+
+std::string gen_post_kernel(const std::vector<std::string>& shapes) {
+  std::string s = R"(
+extern "C" __global__ void __launch_bounds__(256) es_post_jit(PostArgs A) {
+  __shared__ double lk[256];
+  __shared__ double thr[101];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) lk[i] = A.lktab[i];
+  for (int i = threadIdx.x; i < 101; i += blockDim.x) thr[i] = A.gq_thr[i];
+  __syncthreads();
+  const long long work = (long long)A.counts[3] * A.nfams;
+  for (long long u = (long long)blockIdx.x * blockDim.x + threadIdx.x; u < work; u += (long long)gridDim.x * blockDim.x) {
+    const int row = (int)(u / A.nfams), k = (int)(u - (long long)row * A.nfams);
+    const int site = A.row_site[row];
+    const char* R = A.res + (size_t)site * A.res_bytes;
+    const int a1 = *(const int*)(R + A.off_a1), a2 = *(const int*)(R + A.off_a2);
+    const double fq = (*(const int*)(R + A.off_maxidx) == 0) ? 1 - A.theta : *(const double*)(R + A.off_af);   // main.cpp:576-587
+    const uint8_t* pl = A.pl + (size_t)site * A.np * 10;
+    const uint8_t* P11 = pl + (size_t)gi(a1, a1) * A.np;
+    const uint8_t* P12 = pl + (size_t)gi(a1, a2) * A.np;
+    const uint8_t* P22 = pl + (size_t)gi(a2, a2) * A.np;
+    const size_t out0 = (size_t)row * A.np;
+    switch (A.fam_sig[k]) {
+)";
+  for (size_t i = 0; i < shapes.size(); i++)
+    s += "      case " + std::to_string(i) + ": " + shapes[i] + "(P11, P12, P22, A.fam_p0[k], lk, fq, thr, A.calls, out0, A.vcf); break;\n";
+  s += "    }\n  }\n}\n";
+  return s;
+}
+
+
+// ---------------------------------------------------------------------------------------------------------------
+// Wave-cooperative hoisting (--denovo engines: 10-state peels, whose marriage partials -- 100 entries x coefficients
+// -- do not fit one thread's registers).  One (item, family) per wave, as engine.hip's generic k_es_hoist, but
+// compiled per family shape: the workspace layout, every step's degrees and every loop bound are constants, so a
+// phase is a few unrolled multiply-adds per lane between wave-level barriers, with no schedule or layout loads
+// and no run-time divisions.  Variants per shape: 10-state (de novo items), bi-allelic (cfg-7 items), and "top"
+// (the de novo monomorphism item: the f^D coefficient only, every degree 0).
+struct WaveGen {
+  std::string code;
+  void loop(int N, const std::string& body) {   // lanes over N elements x, then a wave barrier
+    code += "  for (int x = lane; x < " + std::to_string(N) + "; x += 64) {\n" + body + "  }\n  wave_sync();\n";
+  }
+};
+
+std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const std::string& name, int* ws_doubles) {
+  const int n = F.n;
+  const bool X = chrom == PM_CHR_X, Y = chrom == PM_CHR_Y, MT = chrom == PM_CHR_MT;
+  // degrees through the peel (poly_layout's rule), capacities, temporaries (type 3 only: the W(i, j) products)
+  std::vector<int> d0(n), dP(n), capP(n);
+  for (int i = 0; i < n; i++) {
+    const bool fo = F.founder[i] && i < F.nf;
+    const int sx = F.sex[i];
+    const int dfull = !fo ? 0 : (Y && sx == FEMALE) ? 0 : (((X || Y) && sx == MALE) || MT) ? 1 : 2;
+    d0[i] = dP[i] = top ? 0 : dfull;
+    capP[i] = dP[i] + 1;
+  }
+  std::map<int, int> dM, capM;
+  int tmp = 1;
+  struct StepDeg { int a, b, c, e; };
+  std::vector<StepDeg> sd;
+  for (const int2& S : F.steps) {
+    const int type = S.x & 255, from0 = (S.x >> 8) & 255, from1 = (S.x >> 16) & 255, to0 = (S.x >> 24) & 255;
+    const int slot = (S.y >> 8) & 255, create = (S.y >> 16) & 1;
+    StepDeg g{0, 0, 0, 0};
+    if (type == 1) {
+      g.a = dP[from0]; g.b = create ? 0 : dM[slot];
+      dM[slot] = g.a + g.b;
+      capM[slot] = std::max(capM[slot], dM[slot] + 1);
+    } else if (type == 2) {
+      g.a = dP[from0]; g.b = slot == 255 ? 0 : dM[slot]; g.c = dP[to0];
+      dP[to0] = g.a + g.b + g.c;
+      capP[to0] = std::max(capP[to0], dP[to0] + 1);
+    } else {
+      g.a = dP[from0]; g.b = slot == 255 ? 0 : dM[slot]; g.c = dP[from1]; g.e = dP[to0];
+      dP[to0] = g.a + g.b + g.c + g.e;
+      capP[to0] = std::max(capP[to0], dP[to0] + 1);
+      tmp = std::max(tmp, NS * NS * (g.a + g.b + g.c + 1));
+    }
+    sd.push_back(g);
+  }
+  std::vector<int> po(n);
+  int off = 0;
+  for (int i = 0; i < n; i++) { po[i] = off; off += NS * capP[i]; }
+  std::map<int, int> mo;
+  for (auto& m : capM) { mo[m.first] = off; off += NS * NS * m.second; }
+  const int TB = off;
+  *ws_doubles = off + tmp;
+  auto S = [](long v) { return std::to_string(v); };
+  const std::string nsS = S(NS), nsq = S(NS * NS), R = S((NS * NS + 63) / 64);
+  std::string code;
+  // InitializePartials x SetFounderPriors, one person at a time (lanes over its states)
+  for (int i = 0; i < n; i++) {
+    const bool fo = F.founder[i] && i < F.nf;
+    const int sx = F.sex[i];
+    const bool yf = NS == 3 && Y && sx == FEMALE;
+    const int dfull = !fo ? 0 : (Y && sx == FEMALE) ? 0 : (((X || Y) && sx == MALE) || MT) ? 1 : 2;
+    const int d = d0[i];
+    std::string b = "    const int o = " + S(po[i]) + " + x * " + S(capP[i]) + ";\n";
+    for (int a = 0; a <= d; a++) b += "    W[o + " + S(a) + "] = 0.0;\n";
+    if (NS == 3) {
+      b += "    const double pen = lk[(x == 0 ? P11 : x == 1 ? P12 : P22)[p0 + " + S(i) + "]];\n";
+      if (yf) b += "    W[o] = 1.0;\n";
+      else if (!fo) b += "    W[o] = pen;\n";
+      else if (top) b += "    if (x == 0) W[o] = pen;\n";
+      else if (d == 2) b += "    W[o + 2 - x] = x == 1 ? 2 * pen : pen;\n";
+      else b += "    if (x != 1) W[o + (x == 0 ? 1 : 0)] = pen;\n";
+    } else {
+      b += "    const double pen = lk[pl[(size_t)x * np + p0 + " + S(i) + "]];\n";
+      b += "    const int q = x == g11 ? 0 : x == g12 ? 1 : x == g22 ? 2 : 3;\n";
+      if (!fo) b += "    W[o] = pen;\n";
+      else if (top && dfull > 0) b += "    if (q == 0) W[o] = pen;\n";
+      else if (d == 2) b += "    if (q != 3) W[o + 2 - q] = q == 1 ? 2 * pen : pen;\n";
+      else if (d == 1) b += "    if (q == 0 || q == 2) W[o + (q == 0 ? 1 : 0)] = pen;\n";
+      else b += "    if (q != 3) W[o] = pen;\n";
+    }
+    code += "  for (int x = lane; x < " + nsS + "; x += 64) {\n" + b + "  }\n";
+  }
+  code += "  wave_sync();\n";
+  // T(e = i NS + j, k) of an offspring: 10-state rows of the lane's pair(s) in registers (trow, the de novo
+  // transmission), the plain transmission (quirk :1391) and the bi-allelic class tables in LDS
+  auto tt = [&](int csex, const std::string& e, const std::string& k, bool plain) -> std::string {
+    if (NS == 10) return plain ? "t10[(" + e + ") * 10 + " + k + "]" : "t10dn[(" + e + ") * 10 + " + k + "]";
+    const int t = chrom == PM_CHR_X ? (csex == MALE ? 2 : 1) : chrom == PM_CHR_Y ? (csex == MALE ? 3 : 5) : chrom == PM_CHR_MT ? 4 : 0;
+    return "tb[" + S(t * 27) + " + (" + e + ") * 3 + " + k + "]";
+  };
+  size_t si = 0;
+  int fin = -1;
+  for (const int2& St : F.steps) {
+    const StepDeg g = sd[si++];
+    const int type = St.x & 255, from0 = (St.x >> 8) & 255, from1 = (St.x >> 16) & 255, to0 = (St.x >> 24) & 255;
+    const int slot = (St.y >> 8) & 255, create = (St.y >> 16) & 1, fa2mo = (St.y >> 17) & 1;
+    fin = to0;
+    if (type == 1) {   // lanes over the pairs e: S(e) = sum_k T(e, k) P_off[k] in registers, then M(e) *= S(e) in place
+      const int off_ = from0, csex = F.sex[off_], pcap = capP[off_], mcap = capM[slot], MO = mo[slot];
+      std::string b = "#pragma unroll\n  for (int r = 0; r < " + R + "; r++) {\n    const int e = lane + 64 * r;\n    if (e < " + nsq + ") {\n";
+      b += "      double s[" + S(g.a + 1) + "];\n";
+      for (int a = 0; a <= g.a; a++) {
+        b += "      s[" + S(a) + "] = 0.0;\n";
+        b += "#pragma unroll\n      for (int k = 0; k < " + nsS + "; k++) s[" + S(a) + "] = fma(" +
+             (NS == 10 ? std::string("(r == 0 ? tr0[k] : tr1[k])") : tt(csex, "e", "k", false)) + ", W[" + S(po[off_]) + " + k * " +
+             S(pcap) + " + " + S(a) + "], s[" + S(a) + "]);\n";
+      }
+      const std::string me = S(MO) + " + e * " + S(mcap);
+      if (create) {
+        for (int a = 0; a <= g.a; a++) b += "      W[" + me + " + " + S(a) + "] = s[" + S(a) + "];\n";
+      } else {
+        b += "      double m[" + S(g.b + 1) + "];\n";
+        for (int c = 0; c <= g.b; c++) b += "      m[" + S(c) + "] = W[" + me + " + " + S(c) + "];\n";
+        for (int a = 0; a <= g.a + g.b; a++) {
+          std::string acc;
+          for (int c = std::max(0, a - g.a); c <= std::min(a, g.b); c++)
+            acc = acc.empty() ? "m[" + S(c) + "] * s[" + S(a - c) + "]" : "fma(m[" + S(c) + "], s[" + S(a - c) + "], " + acc + ")";
+          b += "      W[" + me + " + " + S(a) + "] = " + acc + ";\n";
+        }
+      }
+      b += "    }\n  }\n  wave_sync();\n";
+      code += b;
+    } else if (type == 2) {   // lanes over i: S(i) = sum_j P_from[j] M(j, i) in registers, then P_to[i] *= S(i) in place
+      const int sf = from0, stt = to0, fcap = capP[sf], tcap = capP[stt];
+      const int ds = g.a + g.b;
+      std::string b = "  for (int i = lane; i < " + nsS + "; i += 64) {\n    double s[" + S(ds + 1) + "];\n";
+      for (int a = 0; a <= ds; a++) b += "    s[" + S(a) + "] = 0.0;\n";
+      if (slot == 255) {
+        for (int a = 0; a <= ds; a++)
+          b += "#pragma unroll\n    for (int j = 0; j < " + nsS + "; j++) s[" + S(a) + "] += W[" + S(po[sf]) + " + j * " + S(fcap) + " + " +
+               S(a) + "];\n";
+      } else {
+        const int mcap = capM[slot], MO = mo[slot];
+        const std::string me = fa2mo ? "(j * " + nsS + " + i)" : "(i * " + nsS + " + j)";
+        b += "#pragma unroll\n    for (int j = 0; j < " + nsS + "; j++) {\n";
+        for (int u = 0; u <= g.a; u++) b += "      const double f" + S(u) + " = W[" + S(po[sf]) + " + j * " + S(fcap) + " + " + S(u) + "];\n";
+        for (int v = 0; v <= g.b; v++) b += "      const double g" + S(v) + " = W[" + S(MO) + " + " + me + " * " + S(mcap) + " + " + S(v) + "];\n";
+        for (int u = 0; u <= g.a; u++)
+          for (int v = 0; v <= g.b; v++) b += "      s[" + S(u + v) + "] = fma(f" + S(u) + ", g" + S(v) + ", s[" + S(u + v) + "]);\n";
+        b += "    }\n";
+      }
+      b += "    double t[" + S(g.c + 1) + "];\n";
+      for (int c = 0; c <= g.c; c++) b += "    t[" + S(c) + "] = W[" + S(po[stt]) + " + i * " + S(tcap) + " + " + S(c) + "];\n";
+      for (int a = 0; a <= g.c + ds; a++) {
+        std::string acc;
+        for (int c = std::max(0, a - ds); c <= std::min(a, g.c); c++)
+          acc = acc.empty() ? "t[" + S(c) + "] * s[" + S(a - c) + "]" : "fma(t[" + S(c) + "], s[" + S(a - c) + "], " + acc + ")";
+        b += "    W[" + S(po[stt]) + " + i * " + S(tcap) + " + " + S(a) + "] = " + acc + ";\n";
+      }
+      b += "  }\n  wave_sync();\n";
+      code += b;
+    } else {   // W(e) = P_fa[i] M(e) P_mo[j] -> LDS; lanes over k: S(k) = sum_e T(e, k) W(e), P_off[k] *= S(k) in place
+      const int fa = from0, mo_ = from1, off_ = to0, csex = F.sex[off_];
+      const int dw = g.a + g.b + g.c, ww = dw + 1;
+      std::string b = "#pragma unroll\n  for (int r = 0; r < " + R + "; r++) {\n    const int e = lane + 64 * r;\n    if (e < " + nsq + ") {\n"
+                      "      const int i = e / " + nsS + ", j = e - i * " + nsS + ";\n      double w[" + S(ww) + "];\n";
+      for (int a = 0; a <= dw; a++) b += "      w[" + S(a) + "] = 0.0;\n";
+      for (int u = 0; u <= g.a; u++)
+        for (int v = 0; v <= g.b; v++)
+          for (int c = 0; c <= g.c; c++) {
+            const std::string m = slot == 255 ? "" : " * W[" + S(mo[slot]) + " + e * " + S(capM[slot]) + " + " + S(v) + "]";
+            b += "      w[" + S(u + v + c) + "] = fma(W[" + S(po[fa]) + " + i * " + S(capP[fa]) + " + " + S(u) + "]" + m + ", W[" +
+                 S(po[mo_]) + " + j * " + S(capP[mo_]) + " + " + S(c) + "], w[" + S(u + v + c) + "]);\n";
+          }
+      for (int a = 0; a <= dw; a++) b += "      W[" + S(TB) + " + e * " + S(ww) + " + " + S(a) + "] = w[" + S(a) + "];\n";
+      b += "    }\n  }\n  wave_sync();\n";
+      b += "  for (int k = lane; k < " + nsS + "; k += 64) {\n    double s[" + S(ww) + "];\n";
+      for (int a = 0; a <= dw; a++) b += "    s[" + S(a) + "] = 0.0;\n";
+      b += "    for (int e = 0; e < " + nsq + "; e++) {\n      const double t = " + tt(csex, "e", "k", slot != 255) + ";\n";
+      for (int a = 0; a <= dw; a++) b += "      s[" + S(a) + "] = fma(t, W[" + S(TB) + " + e * " + S(ww) + " + " + S(a) + "], s[" + S(a) + "]);\n";
+      b += "    }\n    double t[" + S(g.e + 1) + "];\n";
+      for (int c = 0; c <= g.e; c++) b += "    t[" + S(c) + "] = W[" + S(po[off_]) + " + k * " + S(capP[off_]) + " + " + S(c) + "];\n";
+      for (int a = 0; a <= g.e + dw; a++) {
+        std::string acc;
+        for (int c = std::max(0, a - dw); c <= std::min(a, g.e); c++)
+          acc = acc.empty() ? "t[" + S(c) + "] * s[" + S(a - c) + "]" : "fma(t[" + S(c) + "], s[" + S(a - c) + "], " + acc + ")";
+        b += "    W[" + S(po[off_]) + " + k * " + S(capP[off_]) + " + " + S(a) + "] = " + acc + ";\n";
+      }
+      b += "  }\n  wave_sync();\n";
+      code += b;
+    }
+  }
+  const int D = dP[fin];
+  code += "  for (int a = lane; a <= " + S(D) + "; a += 64) {\n    double s = 0.0;\n#pragma unroll\n    for (int i = 0; i < " + nsS +
+          "; i++) s += W[" + S(po[fin]) + " + i * " + S(capP[fin]) + " + a];\n    out[(size_t)a * os] = s;\n  }\n"
+          "  if (lane == 0) out[(size_t)(dcap - 1) * os] = " + S(D) + ".0;\n  wave_sync();\n";
+  return "__device__ __forceinline__ void " + name +
+         "(const uint8_t* __restrict__ pl, size_t np, const uint8_t* __restrict__ P11, const uint8_t* __restrict__ P12, "
+         "const uint8_t* __restrict__ P22, int p0, int g11, int g12, int g22, const double* lk, const double* __restrict__ t10, "
+         "const double* __restrict__ t10dn, const double* tb, const double* tr0, const double* tr1, double* W, int lane, "
+         "double* __restrict__ out, int os, int dcap) {\n" + code + "}\n";
+}
+
+std::string gen_wave_kernel(const std::vector<std::string>& fns, int ws, int wpb) {
+  std::string s = R"(
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+)";
+  std::string k = R"(
+extern "C" __global__ void __launch_bounds__(64 * WPB) es_hoist_wave(Args A) {   // blockDim = 64 WPB
+  __shared__ double lk[256], tb[6 * 27];
+  __shared__ double ws[WPB][WSIZE];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) lk[i] = A.lktab[i];
+  for (int i = threadIdx.x; i < 6 * 27; i += blockDim.x) tb[i] = i < 5 * 27 ? A.tba[i] : 1.0;
+  __syncthreads();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  double* W = ws[wave];
+  // the de novo transmission rows of this lane's marriage-partial pairs (lane, lane + 64), for every 10-state step
+  double tr0[10], tr1[10];
+#pragma unroll
+  for (int k = 0; k < 10; k++) {
+    tr0[k] = A.T10dn[lane * 10 + k];
+    tr1[k] = lane + 64 < 100 ? A.T10dn[(lane + 64) * 10 + k] : 0.0;
+  }
+  const double* t10 = A.T10;
+  const double* t10dn = A.T10dn;
+  const int nItems = min(A.counts[A.list], A.it1);
+  if (nItems <= A.it0) return;
+  const long long units = (long long)(nItems - A.it0) * A.nslots;
+  for (long long u = (long long)blockIdx.x * WPB + wave; u < units; u += (long long)gridDim.x * WPB) {
+    const int uq = (int)(u / A.nslots), k = (int)(u - (long long)uq * A.nslots);
+    const int it = A.it0 + uq;
+    const int item = __builtin_amdgcn_readfirstlane(A.items[it]);
+    const int site = item >> 3, cfg = item & 7, r = A.ref[site];
+    int a1, a2;
+    if (A.vcf) { a1 = r & 15; a2 = r >> 4; }
+    else if (cfg == 7) { a1 = A.res[(size_t)site * A.res_words + A.res_a1]; a2 = A.res[(size_t)site * A.res_words + A.res_a2]; }
+    else cfg_alleles(cfg, r, &a1, &a2);
+    const int g11 = gi(a1, a1), g12 = gi(a1, a2), g22 = gi(a2, a2);
+    const uint8_t* pl = A.pl + (size_t)site * A.np * 10;
+    const uint8_t* P11 = pl + (size_t)g11 * A.np;
+    const uint8_t* P12 = pl + (size_t)g12 * A.np;
+    const uint8_t* P22 = pl + (size_t)g22 * A.np;
+    const int e = __builtin_amdgcn_readfirstlane(A.slot_e[k]), q = e / A.T;
+    const int sig = __builtin_amdgcn_readfirstlane(A.slot_sig[k]), p0 = __builtin_amdgcn_readfirstlane(A.slot_p0[k]);
+    double* out = A.coef + ((size_t)uq * A.max_ext + q) * A.dcap * A.T + (e - q * A.T);
+    const int dn = A.denovo && cfg != 7, top = dn && cfg == 0 && !A.vcf;   // variant: 0 bi-allelic, 1 10-state, 2 top
+    switch (sig * 3 + (top ? 2 : dn ? 1 : 0)) {
+)";
+  k.replace(k.find("WSIZE"), 5, std::to_string(ws));
+  for (size_t at; (at = k.find("WPB")) != std::string::npos;) k.replace(at, 3, std::to_string(wpb));
+  s += k;
+  for (size_t i = 0; i < fns.size(); i++)
+    s += "      case " + std::to_string(i) + ": " + fns[i] +
+         "(pl, A.np, P11, P12, P22, p0, g11, g12, g22, lk, t10, t10dn, tb, tr0, tr1, W, lane, out, A.T, A.dcap); break;\n";
+  s += "    }\n  }\n}\n";
+  return s;
+}
+
+std::mutex g_mu;
+std::map<std::pair<int, std::string>, hipModule_t> g_modules;   // (device, source) -> module, for the process
+
+}  // namespace
+
+// Packs one extended family's ES_Peeling schedule for d_es_lk: marriage-partial slots are resolved the
+// way the reference's partial map behaves (created by the first type-1 step of a couple, looked up by
+// later type-2/3 steps, absent before that).  Returns the workspace doubles the family needs, -1 if it
+// cannot be packed (family larger than 255 members).
+int pack_steps(const pm_pedigree* ped, int f, int ns, std::vector<int2>& out) {
+  const int p0 = ped->fam_start[f], n = ped->fam_start[f + 1] - p0;
+  if (n > 255 || !ped->peel_start || !ped->steps) return -1;
+  std::vector<std::pair<int, int>> keys;
+  auto find = [&](int a, int b) {
+    for (size_t i = 0; i < keys.size(); i++) if (keys[i].first == a && keys[i].second == b) return (int)i;
+    return -1;
+  };
+  for (int k = ped->peel_start[f]; k < ped->peel_start[f + 1]; k++) {
+    const pm_peel_step& S = ped->steps[k];
+    int slot = 255, create = 0, fa2mo = 0;
+    if (S.type == 1) {
+      int i = find(S.to0, S.to1);
+      if (i < 0) { i = (int)keys.size(); keys.push_back({S.to0, S.to1}); create = 1; }
+      slot = i;
+    } else if (S.type == 2) {
+      int a, b;
+      if (ped->sex[p0 + S.from0] == FEMALE) { a = S.to0; b = S.from0; fa2mo = 0; } else { a = S.from0; b = S.to0; fa2mo = 1; }
+      const int i = find(a, b);
+      slot = i < 0 ? 255 : i;
+    } else if (S.type == 3) {
+      const int i = find(S.from0, S.from1);
+      slot = i < 0 ? 255 : i;
+    } else return -1;
+    if (keys.size() > 254) return -1;
+    int2 e;
+    e.x = (S.type & 255) | ((S.from0 & 255) << 8) | ((S.from1 & 255) << 16) | ((S.to0 & 255) << 24);
+    e.y = (S.to1 & 255) | (slot << 8) | (create << 16) | (fa2mo << 17);
+    out.push_back(e);
+  }
+  if (ped->peel_start[f + 1] == ped->peel_start[f]) return -1;
+  return n * ns + (int)keys.size() * ns * ns;
+}
+
+std::string generate(int chrom, const std::vector<Family>& fams, const double (*tba)[27], Kernel* out, bool denovo) {
+  std::map<std::string, int> shape_of;
+  std::vector<std::string> names, bodies, post_names, post_bodies, wave_names, wave_bodies;
+  int ws = 1;
+  std::vector<std::pair<int, int>> order;   // (shape, index into fams)
+  for (size_t i = 0; i < fams.size(); i++) {
+    const std::string key = shape_key(fams[i]);
+    auto it = shape_of.find(key);
+    int id;
+    if (it == shape_of.end()) {
+      id = (int)names.size();
+      shape_of[key] = id;
+      names.push_back("fam" + std::to_string(id));
+      if (!denovo) {
+        bodies.push_back(gen_family(fams[i], chrom, tba, names.back()));
+        post_names.push_back("post" + std::to_string(id));
+        post_bodies.push_back(gen_post_family(fams[i], chrom, tba, post_names.back()));
+      } else {   // variants 3 id + {0 bi-allelic, 1 10-state, 2 top}
+        for (int v = 0; v < 3; v++) {
+          int w = 0;
+          wave_names.push_back("wfam" + std::to_string(id) + "_" + std::to_string(v));
+          wave_bodies.push_back(gen_wave_family(fams[i], chrom, v == 0 ? 3 : 10, v == 2, wave_names.back(), &w));
+          ws = std::max(ws, w);
+        }
+      }
+    } else id = it->second;
+    order.push_back({id, (int)i});
+  }
+  std::stable_sort(order.begin(), order.end(), [](const std::pair<int, int>& a, const std::pair<int, int>& b) { return a.first < b.first; });
+  out->slot_e.clear(); out->slot_sig.clear(); out->slot_p0.clear();
+  for (auto& o : order) {
+    out->slot_e.push_back(fams[o.second].e);
+    out->slot_sig.push_back(o.first);
+    out->slot_p0.push_back(fams[o.second].p0);
+  }
+  out->n_shapes = (int)names.size();
+  std::string src = kPrologue;
+  if (!denovo) {
+    for (auto& b : bodies) src += b;
+    src += gen_kernel(names);
+    src += kPostPrologue;
+    for (auto& b : post_bodies) src += b;
+    src += gen_post_kernel(post_names);
+    out->wave = false;
+  } else {
+    // waves per block: as many workspace slices as fit the 64 KB of static LDS next to the tables
+    const int tables = (256 + 6 * 27) * 8;
+    out->wpb = std::max(1, std::min(8, (64 * 1024 - tables) / (ws * 8)));
+    if ((64 * 1024 - tables) / (ws * 8) < 1) out->wpb = 0;   // a family too large for one slice: the engine's generic kernel
+    std::string wk = gen_wave_kernel(wave_names, ws, std::max(1, out->wpb));
+    const size_t at = wk.find("extern \"C\"");   // device helpers first, then the family functions, then the kernel
+    src += wk.substr(0, at);
+    for (auto& b : wave_bodies) src += b;
+    src += wk.substr(at);
+    out->wave = true;
+    out->ws = ws;
+  }
+  return src;
+}
+
+bool compile(const std::string& src, std::vector<char>* code, std::string* err) {
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, src.c_str(), "es_hoist_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+    *err = "hiprtcCreateProgram failed";
+    return false;
+  }
+  // -ffp-contract=off: only the explicit fma() of the generated code fuses
+  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17"};
+  const hiprtcResult rc = hiprtcCompileProgram(prog, 4, opts);
+  if (rc != HIPRTC_SUCCESS) {
+    size_t ls = 0;
+    hiprtcGetProgramLogSize(prog, &ls);
+    std::string log(ls + 1, '\0');
+    hiprtcGetProgramLog(prog, &log[0]);
+    *err = "hipRTC compile of the peeling kernel failed: " + log.substr(0, 2000);
+    hiprtcDestroyProgram(&prog);
+    return false;
+  }
+  size_t cs = 0;
+  hiprtcGetCodeSize(prog, &cs);
+  code->resize(cs);
+  hiprtcGetCode(prog, code->data());
+  hiprtcDestroyProgram(&prog);
+  return true;
+}
+
+bool build(int device, int chrom, const std::vector<Family>& fams, const double (*tba)[27], bool denovo, Kernel* out,
+           std::string* err) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const std::string src = generate(chrom, fams, tba, out, denovo);
+  if (denovo && out->wpb == 0) { *err = "family workspace exceeds a block's LDS"; return false; }
+  std::lock_guard<std::mutex> lock(g_mu);
+  auto key = std::make_pair(device, src);
+  auto it = g_modules.find(key);
+  if (it == g_modules.end()) {
+    std::vector<char> code;
+    if (!compile(src, &code, err)) return false;
+    hipModule_t mod;
+    if (hipSetDevice(device) != hipSuccess || hipModuleLoadData(&mod, code.data()) != hipSuccess) {
+      *err = "hipModuleLoadData of the peeling kernel failed";
+      return false;
+    }
+    it = g_modules.emplace(key, mod).first;
+  }
+  const bool ok = denovo ? hipModuleGetFunction(&out->fn, it->second, "es_hoist_wave") == hipSuccess
+                         : hipModuleGetFunction(&out->fn, it->second, "es_hoist_jit") == hipSuccess &&
+                               hipModuleGetFunction(&out->fn_post, it->second, "es_post_jit") == hipSuccess;
+  if (!ok) {
+    *err = "hipModuleGetFunction of the generated kernels failed";
+    return false;
+  }
+  out->compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return true;
+}
+
+}  // namespace pmjit

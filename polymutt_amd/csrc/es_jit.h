@@ -1,0 +1,87 @@
+// es_jit.h -- the Elston-Stewart schedule compiler (host side of the EP hoisting).
+//
+// An extended family's peeling schedule (ES_Peeling, FamilyLikelihoodES.cpp:46-277) is fixed per pedigree, so
+// the polynomial-form peel of a (Brent item, family) -- the bi-allelic steps of :1105-1286 run on coefficient
+// vectors, see engine.hip "Elston-Stewart peeling in polynomial form" -- is compiled at engine creation into
+// straight-line HIP for gfx950 (hipRTC): one device function per distinct family shape of the section's
+// chromosome class, every partial and marriage-partial coefficient an SSA value (registers), the transmission
+// constants folded, structurally zero terms dropped.  One thread then hoists one (item, family) -- no
+// workspace, no schedule interpretation.  Families of one shape share a function; the kernel switches on it.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+#include <hip/hip_runtime.h>
+#include "../../include/polymutt_engine.h"
+
+namespace pmjit {
+
+struct Family {              // one extended family of the lane plan, in slot order e = q * T + lane
+  int e;                     // slot of the plan (coefficients go to es_coef[...][e / T][...][e % T])
+  int p0, n, nf;             // first person (flattened), persons, founders (Family::path: founders first)
+  std::vector<int8_t> sex, founder;
+  std::vector<int2> steps;   // packed schedule (engine.hip pack_steps: type | from0 | from1 | to0, to1 | slot | create | fa2mo)
+};
+
+// Arguments of the generated kernel es_hoist_jit (identical layout in the generated source).
+struct Args {
+  const int* items;          // the list's items (site << 3 | cfg)
+  const int* counts;         // counts[list] = list size
+  const uint8_t* ref;        // [site] refBase (vcf_mode: a1 | a2 << 4)
+  const int* res;            // pm_site_result as int32 words (cfg-7 items read allele1/allele2)
+  const uint8_t* pl;         // genotype-planar site blocks
+  const double* lktab;       // [256] phred -> likelihood
+  double* coef;              // es_coef
+  const int* slot_e;         // [nslots] plan slot, sorted by shape
+  const int* slot_sig;       // [nslots] shape index
+  const int* slot_p0;        // [nslots] first person
+  const double* T10;         // FamilyLikelihoodES::transmission [10][10][10] (es_hoist_wave)
+  const double* T10dn;       // transmission_denovo
+  const double* tba;         // transmission_BA tables [5][27]
+  int list, it0, it1, nslots, np, T, max_ext, dcap, vcf, res_words, res_a1, res_a2, denovo;
+};
+
+// Arguments of the generated posterior kernel es_post_jit (CalcPostProb_SingleExtendedPed_BA for every emitted row
+// and peeled family; the families are the Kernel's slots, sorted by shape).
+struct PostArgs {
+  const int* counts;         // counts[3] = emitted rows
+  const int* row_site;       // [row] site
+  const char* res;           // pm_site_result[site] (allele1/2, maxidx, af read at the byte offsets below)
+  const uint8_t* pl;
+  const double* lktab;
+  const double* gq_thr;      // [101] GQ thresholds (engine.hip d_gq)
+  void* calls;               // pm_geno_call[row][person], or pm_vcf_call in vcf_mode
+  const int* fam_p0;         // [nfams] first person (slot order, sorted by shape)
+  const int* fam_sig;        // [nfams] shape
+  int nfams, np, vcf, res_bytes, off_a1, off_a2, off_maxidx, off_af;
+  double theta;
+};
+
+struct Kernel {
+  hipFunction_t fn = nullptr;        // es_hoist_jit(Args)
+  hipFunction_t fn_post = nullptr;   // es_post_jit(PostArgs)
+  std::vector<int> slot_e, slot_sig, slot_p0;   // host copies (the engine uploads them)
+  int n_shapes = 0;
+  double compile_ms = 0;
+  bool wave = false;         // --denovo: es_hoist_wave, one (item, family) per wave, blockDim = 64 wpb
+  int wpb = 0, ws = 0;       // waves per block, workspace doubles per wave
+};
+
+// Packs family f's ES_Peeling schedule (pm_pedigree.steps) with its marriage-partial slots resolved the way the
+// reference's partial map behaves; appends to out; returns the workspace doubles of a reference-order peel with ns
+// states, -1 if it cannot be packed.
+int pack_steps(const pm_pedigree* ped, int f, int ns, std::vector<int2>& out);
+
+// The generated source of the hoisting kernel of `fams` (fills out's slot tables; no device needed).
+// denovo: the wave-cooperative kernel es_hoist_wave (10-state, bi-allelic and top variants per shape) instead of the
+// per-thread es_hoist_jit and es_post_jit.
+std::string generate(int chrom, const std::vector<Family>& fams, const double (*tba)[27], Kernel* out, bool denovo = false);
+// hipRTC compile of a generated source for gfx950 (no device needed).
+bool compile(const std::string& src, std::vector<char>* code, std::string* err);
+
+// Generates and compiles the hoisting and posterior kernels of `fams` for chromosome class `chrom` (PM_CHR_*); bi-allelic
+// (3-state) peels.  tba = transmission_BA tables [5][27] (:812-924).  Returns false with a message in err.
+bool build(int device, int chrom, const std::vector<Family>& fams, const double (*tba)[27], bool denovo, Kernel* out,
+           std::string* err);
+
+}  // namespace pmjit

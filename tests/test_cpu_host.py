@@ -321,3 +321,22 @@ def test_sharded_vcf_input_matches_one_process_gloo(cpu_driver, tmp_path, case, 
         import gzip
         gold = gzip.open(os.path.join(EXAMPLE, "testvcf.out.vcf.body.gz"), "rt").read().splitlines()
         assert vcf_body(sh)[1:] == gold[1:]
+
+
+@pytest.mark.parametrize("shape", ["ext10", "roof", "roof2"])
+def test_schedule_compiler_builds_every_class(tmp_path, shape):
+    """The Elston-Stewart schedule compiler (polymutt_amd/csrc/es_jit.h) generates the hoisting kernel of a
+    pedigree's extended families for every chromosome class and hipRTC compiles it for gfx950 (no device needed);
+    families of one shape share one device function; --denovo engines get the wave-cooperative variant."""
+    exe = os.path.join(ROOT, "tests", "native", "build", "jit_check")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "polymutt_amd"), "../tests/native/build/jit_check"], check=True)
+    pm.synth_write_dataset(str(tmp_path), shape, 5, 1, 3)
+    r = subprocess.run([exe, str(tmp_path / "test.dat"), str(tmp_path / "test.ped"), "--emit", str(tmp_path / "k.hip")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = [l.split() for l in r.stdout.splitlines() if l.startswith("class")]
+    assert [int(l[1]) for l in lines] == [0, 1, 2, 3] * 2   # bi-allelic engines, then --denovo engines
+    assert all(int(l[3]) == 1 and int(l[5]) == 5 and int(l[9]) > 0 for l in lines), r.stdout   # one shape, 5 families
+    src = (tmp_path / "k.hip").read_text()
+    assert "es_hoist_jit" in src and "fam0(" in src and "asm" not in src
