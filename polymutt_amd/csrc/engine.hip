@@ -22,6 +22,7 @@
 // the only deviations from the reference's arithmetic are OCML log10/exp10 (<=1 ulp) and the order of
 // the cross-family reduction inside the Brent objective (a fixed tree, deterministic for any batch).
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -110,6 +111,7 @@ struct DevArgs {
   // posteriors of peeled families: one work item per (row, person) of es_pers[n_es_pers] = family << 8 | member
   const int* es_pers;
   int n_es_pers;
+  const int* fam_perm;     // k_posterior: families ordered by (kind, size), so a wave's threads take one code path
   int unrelated;           // --quick_call MakeUnrelated(): every family is all-founder
   double theta_one;        // 1.0 (opaque to the compiler; timing experiments only)
   int vcf;                 // vcf_mode: one (ref, alt) Brent per site, FamilyLikelihoodSeq_VCF family rules
@@ -142,7 +144,7 @@ struct DevArgs {
   int* items[N_LISTS];
   int* counts;             // [0..2] list sizes, [3] rows, [4] first emitted site, [5] Brent stuck, [8]/[9] quick items/site visits
   unsigned long long* eval_total;
-  unsigned long long* phase;   // PM_PHASE_TIMING: [0] hoisting, [1] evaluations, [2] items -- k_brent wave time (100 MHz ticks)
+  unsigned long long* phase;   // PM_PHASE_TIMING: [0] hoisting, [1] evaluations, [2] items -- k_brent wave time (wall_clock64 ticks)
   int* row_site;           // [n] emitted row -> site
   unsigned long long* counters;   // pm_counters as 16 x u64
   int carry_postprob;      // famlk[0].CalcPostProb ran in an earlier batch
@@ -685,19 +687,22 @@ __device__ __forceinline__ void fam_poly4(const uint32_t* by, int nn, const doub
   for (int k = 0; k < 9; k++) kids[k] = 1.0;
 #pragma unroll
   for (int q = 2; q < 4; q++) {
-    const double l11 = lk[by[3 * q]], l12 = lk[by[3 * q + 1]], l22 = lk[by[3 * q + 2]];
+    // a missing kid reads l = 1: every autosomal d_one_kid term is then exactly 1.0 (0.5 * (1 + 1),
+    // 0.25 + 0.5 + 0.25), the factor the reference never multiplies in -- three selects instead of nine
     const bool kid = q < nn;
+    const double l11 = kid ? lk[by[3 * q]] : 1.0, l12 = kid ? lk[by[3 * q + 1]] : 1.0, l22 = kid ? lk[by[3 * q + 2]] : 1.0;
 #pragma unroll
-    for (int k = 0; k < 9; k++) kids[k] *= kid ? d_one_kid(k, PM_CHR_AUTO, 0, l11, l12, l22) : 1.0;
+    for (int k = 0; k < 9; k++) kids[k] *= d_one_kid(k, PM_CHR_AUTO, 0, l11, l12, l22);
   }
-  const double lF[3] = {lk[by[0]], lk[by[1]], lk[by[2]]};
-  const double lM[3] = {lk[by[3]], lk[by[4]], lk[by[5]]};
+  // no parents (empty slot): lF = 0 makes every term +0 (all values finite and >= 0)
   const bool fam = nn >= 2;
+  const double lF[3] = {fam ? lk[by[0]] : 0.0, fam ? lk[by[1]] : 0.0, fam ? lk[by[2]] : 0.0};
+  const double lM[3] = {lk[by[3]], lk[by[4]], lk[by[5]]};
   double c9[9];
 #pragma unroll
   for (int x = 0; x < 3; x++)
 #pragma unroll
-    for (int y = 0; y < 3; y++) c9[3 * x + y] = fam ? kids[3 * x + y] * (lF[x] * lM[y]) : 0.0;
+    for (int y = 0; y < 3; y++) c9[3 * x + y] = kids[3 * x + y] * (lF[x] * lM[y]);
   fold_poly(c9, a);
   if (nn == 0) {   // empty slot: the phantom family (f + g)^4 (selects, not a branch)
     a[0] = 1.0; a[1] = 4.0; a[2] = 6.0; a[3] = 4.0; a[4] = 1.0;
@@ -870,18 +875,19 @@ __device__ __forceinline__ void hoist_poly4_dn(const DevArgs& A, const int* su, 
           }
           D11 = lk[b11]; D12 = lk[b12]; D22 = lk[b22];
         }
-        const bool isKid = q + 2 < nn[j];
+        const bool isKid = q + 2 < nn[j];   // a missing kid: D = 1, every term exactly 1.0 (fam_poly4)
+        D11 = isKid ? D11 : 1.0; D12 = isKid ? D12 : 1.0; D22 = isKid ? D22 : 1.0;
 #pragma unroll
-        for (int k = 0; k < 9; k++) kids[k] *= isKid ? d_one_kid_dn(k, D11, D12, D22) : 1.0;
+        for (int k = 0; k < 9; k++) kids[k] *= d_one_kid_dn(k, D11, D12, D22);
       }
-      const double lF[3] = {lk[par[j][0]], lk[par[j][1]], lk[par[j][2]]};
-      const double lM[3] = {lk[par[j][3]], lk[par[j][4]], lk[par[j][5]]};
       const bool fam = nn[j] >= 2;
+      const double lF[3] = {fam ? lk[par[j][0]] : 0.0, fam ? lk[par[j][1]] : 0.0, fam ? lk[par[j][2]] : 0.0};
+      const double lM[3] = {lk[par[j][3]], lk[par[j][4]], lk[par[j][5]]};
       double c9[9];
 #pragma unroll
       for (int x = 0; x < 3; x++)
 #pragma unroll
-        for (int y = 0; y < 3; y++) c9[3 * x + y] = fam ? kids[3 * x + y] * (lF[x] * lM[y]) : 0.0;
+        for (int y = 0; y < 3; y++) c9[3 * x + y] = kids[3 * x + y] * (lF[x] * lM[y]);
       fold_poly(c9, a[c0 + j]);
       if (nn[j] == 0) {   // empty slot: the phantom family (selects)
         a[c0 + j][0] = 1.0; a[c0 + j][1] = 4.0; a[c0 + j][2] = 6.0; a[c0 + j][3] = 4.0; a[c0 + j][4] = 1.0;
@@ -901,6 +907,7 @@ __device__ __forceinline__ void hoist_poly4_dn(const DevArgs& A, const int* su, 
 #define DN_PF_C 1
 #endif
 #define DN_PF_WIN 272
+typedef const __attribute__((address_space(3))) double* lds_cdp;   // an LDS pointer (32-bit, ds_* addressing)
 #define DN_PF_BUF ((10 * DN_PF_C * DN_PF_WIN + 1023) / 1024 * 1024)   // per wave per chunk (C = 1: 2720 B as 3 x 1 KB)
 __device__ __forceinline__ void dn_pf_issue(const DevArgs& A, const uint8_t* pl, const int* start_al, uint8_t* dst) {
   const int lane = threadIdx.x & 63, np = A.n_person;
@@ -943,8 +950,10 @@ __device__ __forceinline__ void hoist_poly4_dn_pf(const DevArgs& A, const int* s
       __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
     }
     __builtin_amdgcn_sched_barrier(0);
-    int r11 = I.g11 * 10, r12 = I.g12 * 10, r22 = I.g22 * 10;
-    asm volatile("" : "+v"(r11), "+v"(r12), "+v"(r22));
+    // the item's three mutation-matrix rows, as LDS addresses made opaque once per chunk: the 30 entries are
+    // re-read per slot (holding them would take 60 VGPRs) with the entry offsets folded into ds_read2_b64
+    lds_cdp M11 = (lds_cdp)(M + I.g11 * 10), M12 = (lds_cdp)(M + I.g12 * 10), M22 = (lds_cdp)(M + I.g22 * 10);
+    asm volatile("" : "+v"(M11), "+v"(M12), "+v"(M22));
 #pragma unroll
     for (int j = 0; j < C; j++) {
       const int u = uu[c0 + j];
@@ -991,7 +1000,7 @@ __device__ __forceinline__ void hoist_poly4_dn_pf(const DevArgs& A, const int* s
         for (int q = 0; q < 2; q++) DK[q][0] = DK[q][1] = DK[q][2] = 0.0;
 #pragma unroll
         for (int g = 0; g < 10; g++) {   // each mutation-matrix entry read once for both kids (same per-kid order)
-          const double m11 = M[r11 + g], m12 = M[r12 + g], m22 = M[r22 + g];
+          const double m11 = M11[g], m12 = M12[g], m22 = M22[g];
 #pragma unroll
           for (int q = 0; q < 2; q++) {
             DK[q][0] = fma(m11, pg[q][g], DK[q][0]);
@@ -1005,19 +1014,22 @@ __device__ __forceinline__ void hoist_poly4_dn_pf(const DevArgs& A, const int* s
       }
 #pragma unroll
       for (int q = 0; q < 2; q++) {
-        const double D11 = DK[q][0], D12 = DK[q][1], D22 = DK[q][2];
+        // a missing kid gets D = 1: every d_one_kid_dn term is then exactly 1.0 (0.5 * (1 + 1), 0.25 + 0.5 + 0.25),
+        // the factor the reference's loop never multiplies in -- three selects instead of nine
         const bool isKid = q + 2 < nn;
+        const double D11 = isKid ? DK[q][0] : 1.0, D12 = isKid ? DK[q][1] : 1.0, D22 = isKid ? DK[q][2] : 1.0;
 #pragma unroll
-        for (int k = 0; k < 9; k++) kids[k] *= isKid ? d_one_kid_dn(k, D11, D12, D22) : 1.0;
+        for (int k = 0; k < 9; k++) kids[k] *= d_one_kid_dn(k, D11, D12, D22);
       }
-      const double lF[3] = {lk[par[0]], lk[par[1]], lk[par[2]]};
-      const double lM[3] = {lk[par[3]], lk[par[4]], lk[par[5]]};
+      // no parents (empty or founder-only slot): lF = 0 makes every term +0 (all values finite, >= 0)
       const bool fam = nn >= 2;
+      const double lF[3] = {fam ? lk[par[0]] : 0.0, fam ? lk[par[1]] : 0.0, fam ? lk[par[2]] : 0.0};
+      const double lM[3] = {lk[par[3]], lk[par[4]], lk[par[5]]};
       double c9[9];
 #pragma unroll
       for (int x = 0; x < 3; x++)
 #pragma unroll
-        for (int y = 0; y < 3; y++) c9[3 * x + y] = fam ? kids[3 * x + y] * (lF[x] * lM[y]) : 0.0;
+        for (int y = 0; y < 3; y++) c9[3 * x + y] = kids[3 * x + y] * (lF[x] * lM[y]);
       fold_poly(c9, a[c0 + j]);
       if (nn == 0) {
         a[c0 + j][0] = 1.0; a[c0 + j][1] = 4.0; a[c0 + j][2] = 6.0; a[c0 + j][3] = 4.0; a[c0 + j][4] = 1.0;
@@ -2164,7 +2176,7 @@ __device__ void d_kid_geno(int chrom, const uint8_t* pl, int np, const double* l
 // memory round trip instead of one per stage), then the arithmetic of hoist_nuc, CalcParentMarginal and
 // KidJointGenoLikelihood below in the same operation order -- the same values bit for bit
 __device__ __forceinline__ void lean_nuc_post(const DevArgs& A, const double* s_lk, const double* s_gq, const uint8_t* pl,
-                                              size_t out, int p0, int n, int g11, int g12, int g22, double freq, int is_mono) {
+                                              size_t out, int p0, int n, int g11, int g12, int g22, const double* pp) {
   const int np = A.n_person;
   double lF[3], lM[3], kl[2][3];
   lF[0] = s_lk[PLB(pl, np, p0, g11)]; lF[1] = s_lk[PLB(pl, np, p0, g12)]; lF[2] = s_lk[PLB(pl, np, p0, g22)];
@@ -2183,8 +2195,6 @@ __device__ __forceinline__ void lean_nuc_post(const DevArgs& A, const double* s_
 #pragma unroll
     for (int k = 0; k < 9; k++) kids[k] *= d_one_kid(k, PM_CHR_AUTO, 0, kl[i][0], kl[i][1], kl[i][2]);
   }
-  double pp[9];
-  d_parent_prior((!A.n_fam_gt1 && !is_mono) ? PR_TRIO : PR_AUTO, freq, pp);
   double m[9], wk[9];
 #pragma unroll
   for (int a = 0; a < 3; a++)
@@ -2213,29 +2223,31 @@ __device__ __forceinline__ void lean_nuc_post(const DevArgs& A, const double* s_
 #pragma unroll
   for (int j = 2; j < 4; j++) {   // KidJointGenoLikelihood :798-835, autosomal
     if (j >= n) break;
+    // J[k][t] = prod over kids (in order, from 1.0) of q_j(k)[t] for kid j and l_i(k) for the other kid, then
+    // g[t] = sum_k J[k][t] w[k].  The structurally zero q terms (e.g. q12 = q22 = 0 when both parents are 11) are
+    // skipped: their products are +0 and adding +0 leaves every partial sum's bits unchanged (all terms finite, >= 0)
+    const int me = j - 2, other = 1 - me;
+    const bool two = n == 4;
+    const double m11 = kl[me][0], m12 = kl[me][1], m22 = kl[me][2];
+    const double o11 = kl[other][0], o12 = kl[other][1], o22 = kl[other][2];
     double g[3] = {0.0, 0.0, 0.0};
 #pragma unroll
     for (int k = 0; k < 9; k++) {
-      double G[3] = {1.0, 1.0, 1.0};
-#pragma unroll
-      for (int i = 0; i < 2; i++) {
-        if (2 + i >= n) break;
-        const double l11 = kl[i][0], l12 = kl[i][1], l22 = kl[i][2];
-        double l, q11, q12, q22;
-        switch (k) {
-          case 0: l = l11; q11 = l11; q12 = q22 = 0; break;
-          case 1: case 3: l = 0.5 * (l11 + l12); q11 = l11 * 0.5; q12 = l12 * 0.5; q22 = 0; break;
-          case 2: case 6: l = l12; q11 = 0; q12 = l12; q22 = 0; break;
-          case 4: l = 0.25 * l11 + 0.5 * l12 + 0.25 * l22; q11 = l11 * 0.25; q12 = l12 * 0.5; q22 = l22 * 0.25; break;
-          case 5: case 7: l = 0.5 * (l12 + l22); q11 = 0; q12 = l12 * 0.5; q22 = l22 * 0.5; break;
-          default: l = l22; q11 = 0; q12 = 0; q22 = l22; break;
-        }
-        if (2 + i != j) { G[0] *= l; G[1] *= l; G[2] *= l; }
-        else { G[0] *= q11; G[1] *= q12; G[2] *= q22; }
+      double lo, q11 = 0, q12 = 0, q22 = 0;   // the other kid's likelihood, this kid's genotype terms (d_kid_geno's switch)
+      bool z11 = true, z12 = true, z22 = true;
+      switch (k) {
+        case 0: lo = o11; q11 = m11; z11 = false; break;
+        case 1: case 3: lo = 0.5 * (o11 + o12); q11 = m11 * 0.5; q12 = m12 * 0.5; z11 = z12 = false; break;
+        case 2: case 6: lo = o12; q12 = m12; z12 = false; break;
+        case 4: lo = 0.25 * o11 + 0.5 * o12 + 0.25 * o22; q11 = m11 * 0.25; q12 = m12 * 0.5; q22 = m22 * 0.25; z11 = z12 = z22 = false; break;
+        case 5: case 7: lo = 0.5 * (o12 + o22); q12 = m12 * 0.5; q22 = m22 * 0.5; z12 = z22 = false; break;
+        default: lo = o22; q22 = m22; z22 = false; break;
       }
       const double w = wk[k];
-#pragma unroll
-      for (int t = 0; t < 3; t++) g[t] = (k == 0) ? G[t] * w : g[t] + G[t] * w;
+      // kid order: (1.0 * f_kid2) * f_kid3 -- one product, whichever kid carries q
+      if (!z11) g[0] = g[0] + (two ? q11 * lo : q11) * w;
+      if (!z12) g[1] = g[1] + (two ? q12 * lo : q12) * w;
+      if (!z22) g[2] = g[2] + (two ? q22 * lo : q22) * w;
     }
     const double sum = g[0] + g[1] + g[2];
     if (A.vcf) {
@@ -2279,6 +2291,7 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
     int row, f;
     if (work < 0xFFFFFFFFll) { const unsigned u = (unsigned)gid, nf = (unsigned)A.n_fam; row = (int)(u / nf); f = (int)(u - (unsigned)row * nf); }
     else { row = (int)(gid / A.n_fam); f = (int)(gid % A.n_fam); }
+    f = A.fam_perm[f];
     const int site = A.row_site[row];
     const pm_site_result* R = A.res + site;
     const int np = A.n_person;
@@ -2320,7 +2333,12 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
       }
       if (ES && (kind == PM_FAM_EXTENDED || (A.nuc_es && kind == PM_FAM_NUCLEAR))) continue;   // k_posterior_es
       if (kind != PM_FAM_NUCLEAR) continue;
-      if constexpr (LEAN && !DN) { lean_nuc_post(A, s_lk, s_gq, pl, out, p0, n, g11, g12, g22, freq, is_mono); continue; }
+      if constexpr (LEAN && !DN) {
+        double pp[9];
+        d_parent_prior((!A.n_fam_gt1 && !is_mono) ? PR_TRIO : PR_AUTO, freq, pp);
+        lean_nuc_post(A, s_lk, s_gq, pl, out, p0, n, g11, g12, g22, pp);
+        continue;
+      }
       // CalcParentMarginal(_denovo) at freq
       ItemCtx I;
       I.a1 = a1; I.a2 = a2; I.g11 = g11; I.g12 = g12; I.g22 = g22; I.denovo = dn; I.sex = msex; I.chrom = chrom;
@@ -2451,6 +2469,51 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
           int best = 0; double mx = 0.0;
           for (int t = 0; t < 10; t++) if (mx < post[t]) { mx = post[t]; best = t; }
           d_emit_call(A, s_gq, out + p, post, best, PM_LBL_GENO10, 0.0);
+        }
+      }
+    }
+  }
+}
+
+// LEAN posteriors (autosome, no de novo model, nuclear families of <= 4 persons and single founders), row-blocked:
+// a block takes one emitted row at a time and its threads stride over the row's families (fam_perm order: one
+// family size per stretch of lanes), so the row's set-up -- its result fields, genotype indices, frequency and the
+// HWE parent prior SetParentPrior (:318-368) -- runs once per thread and row instead of once per (row, family), and
+// no work index is divided.  Same arithmetic, in the same order, as k_posterior<false, false, true>.
+__global__ void __launch_bounds__(256) k_posterior_lean(DevArgs A) {
+  __shared__ double s_lk[256];
+  __shared__ double s_gq[101];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) s_lk[i] = A.lktab[i];
+  load_gq_thr(s_gq);
+  __syncthreads();
+  const int rows = A.counts[3], np = A.n_person;
+  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+    const int site = A.row_site[row];
+    const pm_site_result* R = A.res + site;
+    const uint8_t* pl = A.pl + (size_t)site * np * 10;
+    const size_t out = (size_t)row * np;
+    const int a1 = R->allele1, a2 = R->allele2;
+    const int g11 = d_gi(a1, a1), g12 = d_gi(a1, a2), g22 = d_gi(a2, a2);
+    const double freq = (R->maxidx == 0) ? 1 - A.theta : R->af;   // main.cpp:576-587
+    const int is_mono = R->maxidx == 0 ? 1 : 0;
+    double pp[9];
+    d_parent_prior((!A.n_fam_gt1 && !is_mono) ? PR_TRIO : PR_AUTO, freq, pp);
+    const double fq = freq, gq = 1 - freq;
+    const double pr0 = fq * fq, pr1 = fq * gq * 2, pr2 = gq * gq;   // CalcPostProb_SinglePerson's HWE prior (:754-795)
+    for (int fi = threadIdx.x; fi < A.n_fam; fi += blockDim.x) {
+      const int f = A.fam_perm[fi];
+      const int p0 = A.fam_start[f], n = A.fam_start[f + 1] - p0, kind = A.fam_kind[f];
+      if (kind == PM_FAM_NUCLEAR) {
+        lean_nuc_post(A, s_lk, s_gq, pl, out, p0, n, g11, g12, g22, pp);
+      } else if (kind == PM_FAM_FOUNDERS) {
+        for (int j = 0; j < n; j++) {
+          const int p = p0 + j;
+          const double l11 = s_lk[PLB(pl, np, p, g11)], l12 = s_lk[PLB(pl, np, p, g12)], l22 = s_lk[PLB(pl, np, p, g22)];
+          const double m11 = l11 * pr0, m12 = l12 * pr1, m22 = l22 * pr2;
+          const double sum = m11 + m12 + m22;
+          double post[3] = {0, 0, 0};
+          if (sum != 0) { post[0] = m11 / sum; post[1] = m12 / sum; post[2] = m22 / sum; }
+          d_emit_call(A, s_gq, out + p, post, d_best3(m11, m12, m22), PM_LBL_VCF_DIPLOID, post[1] + post[2] * 2);
         }
       }
     }
@@ -2685,6 +2748,7 @@ struct pm_engine {
   int* d_jit_slots[2][4] = {{nullptr, nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr, nullptr}};   // e | sig | p0
   int *d_poly_start = nullptr, *d_poly_lay = nullptr, *d_poly_deg = nullptr;
   int *d_es_pers = nullptr, *d_es_pers1 = nullptr;   // (family << 8 | member) of peeled families: plan 0 / plan 1
+  int* d_fam_perm = nullptr;   // families by (kind, size) for k_posterior
   int n_es_pers = 0, n_es_pers1 = 0;
   // vcf_mode on chrX/Y/MT or with a single family: nuclear families go through ES peeling as well
   // (FamilyLikelihoodSeq_VCF.cpp:97-103), so a second lane plan with them in the per-lane ES lists
@@ -2699,6 +2763,7 @@ struct pm_engine {
   int* d_counts = nullptr;
   unsigned long long* d_eval_total = nullptr;
   unsigned long long* d_phase = nullptr;   // PM_PHASE_TIMING set at engine creation: k_brent hoisting / evaluation wave time
+  int wall_khz = 100000;                   // wall_clock64() rate (hipDeviceAttributeWallClockRate)
   int* d_row_site = nullptr;
   int* d_row_blk = nullptr;   // k_rows_count: written records per 1024-site block
   unsigned long long* d_counters = nullptr;
@@ -2877,7 +2942,7 @@ void pm_engine_destroy(pm_engine* E) {
   if (!E) return;
   hipSetDevice(E->device);
   void* bufs[] = {E->d_units1, E->d_ext_count1, E->d_ext_fam1, E->d_fam_founders, E->d_peel_start, E->d_ext_count, E->d_ext_fam, E->d_is_founder, E->d_steps, E->d_T10,
-                  E->d_T10dn, E->d_ws, E->d_tba, E->d_units_q, E->d_poly_start, E->d_poly_lay, E->d_poly_deg, E->d_es_coef, E->d_es_pers, E->d_es_pers1,
+                  E->d_T10dn, E->d_ws, E->d_tba, E->d_units_q, E->d_poly_start, E->d_poly_lay, E->d_poly_deg, E->d_es_coef, E->d_es_pers, E->d_es_pers1, E->d_fam_perm,
                   E->d_fam_start, E->d_fam_kind, E->d_fa, E->d_mo, E->d_sex, E->d_units, E->d_lktab, E->d_M, E->d_syn,
                   E->d_pl, E->d_stage, E->d_ref, E->d_dm, E->d_res, E->d_calls, E->d_raw, E->d_minv, E->d_mono, E->d_evals,
                   E->d_items[0], E->d_items[1], E->d_items[2], E->d_counts, E->d_eval_total, E->d_row_site,
@@ -3007,6 +3072,16 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
   HIP_TRY(hipMemcpy(E->d_mo, mo.data(), sizeof(int) * ped->n_person, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(E->d_sex, ped->sex, ped->n_person, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(E->d_units, units.data(), sizeof(int4) * units.size(), hipMemcpyHostToDevice));
+  {   // k_posterior's family order: by kind, then size (mixed trio / quad pedigrees: no divergent family-size paths)
+    std::vector<int> perm(ped->n_fam);
+    for (int f = 0; f < ped->n_fam; f++) perm[f] = f;
+    std::stable_sort(perm.begin(), perm.end(), [&](int a, int b) {
+      const int na = ped->fam_start[a + 1] - ped->fam_start[a], nb = ped->fam_start[b + 1] - ped->fam_start[b];
+      return ped->fam_kind[a] != ped->fam_kind[b] ? ped->fam_kind[a] < ped->fam_kind[b] : na < nb;
+    });
+    DALLOC(E->d_fam_perm, ped->n_fam);
+    HIP_TRY(hipMemcpy(E->d_fam_perm, perm.data(), sizeof(int) * ped->n_fam, hipMemcpyHostToDevice));
+  }
   HIP_TRY(hipMemcpy(E->d_lktab, lk, sizeof(lk), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(E->d_M, E->M_h, sizeof(E->M_h), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(E->d_syn, &syn, sizeof(syn), hipMemcpyHostToDevice));
@@ -3232,6 +3307,8 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
   HIP_TRY(hipMemset(E->d_counters, 0, 16 * sizeof(unsigned long long)));
   HIP_TRY(hipMemset(E->d_eval_total, 0, sizeof(unsigned long long)));
   if (getenv("PM_PHASE_TIMING")) {
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0) E->wall_khz = khz;
     DALLOC(E->d_phase, 3);
     HIP_TRY(hipMemset(E->d_phase, 0, 3 * sizeof(unsigned long long)));
   }
@@ -3303,6 +3380,7 @@ static DevArgs make_args(pm_engine* E, int n, const uint8_t* pl, const uint32_t*
   A.es_coef = E->d_es_coef; A.es_it0 = 0; A.es_it1 = INT_MAX; A.max_ext = E->use_plan1 ? E->max_ext1 : E->max_ext;
   A.hoist_ws = E->poly_coef; A.hoist_tmp = E->hoist_tmp;
   A.es_pers = E->use_plan1 ? E->d_es_pers1 : E->d_es_pers;
+  A.fam_perm = E->d_fam_perm;
   A.n_es_pers = E->use_plan1 ? E->n_es_pers1 : E->n_es_pers;
   A.theta_one = 1.0;
   A.unrelated = E->par.quick_call ? 1 : 0;   // k_prep: route sites through the quick pre-filter first
@@ -3571,7 +3649,7 @@ static int run_pipeline(pm_engine* E, int n, const uint8_t* pl, const uint32_t* 
     const bool es = (E->use_plan1 ? E->n_ext1 : E->n_ext) > 0;
     const bool lean = !E->par.denovo && !es && E->chrom == PM_CHR_AUTO && E->max_nuc <= 4 && !E->use_plan1;
     void (*post)(DevArgs) = E->par.denovo ? (es ? k_posterior<true, true> : k_posterior<true, false>)
-                          : es ? k_posterior<false, true> : lean ? k_posterior<false, false, true> : k_posterior<false, false>;
+                          : es ? k_posterior<false, true> : lean ? k_posterior_lean : k_posterior<false, false>;
     hipLaunchKernelGGL(post, dim3(E->grid_post), dim3(256), 0, E->stream, A);
     const pmjit::Kernel* K = es && A.n_es_pers > 0 ? jit_kernel(E) : nullptr;
     if (K && K->fn_post) {   // compiled schedule: one thread per (row, peeled family), all its persons' 3 peels in registers
@@ -3779,8 +3857,8 @@ int pm_engine_kernel_stats(pm_engine* E, pm_kernel_stats* out, int32_t reset) {
   if (E->d_phase) {
     unsigned long long ph[3];
     HIP_TRY(hipMemcpy(ph, E->d_phase, sizeof(ph), hipMemcpyDeviceToHost));
-    out->hoist_wave_ns = (int64_t)ph[0] * 10;   // wall_clock64 runs at 100 MHz
-    out->eval_wave_ns = (int64_t)ph[1] * 10;
+    out->hoist_wave_ns = (int64_t)((double)ph[0] * 1e6 / E->wall_khz);   // wall_clock64 ticks at wall_khz
+    out->eval_wave_ns = (int64_t)((double)ph[1] * 1e6 / E->wall_khz);
     out->timed_items = (int64_t)ph[2];
   }
   if (reset) {
