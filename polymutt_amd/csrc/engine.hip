@@ -2069,18 +2069,20 @@ __device__ __forceinline__ int8_t d_vcf_label(int chrom, int membersex) {
 }
 // GQ = (pb > 0.9999999999) ? 100 : int(-10 log10(1 - pb) + 0.5) (OutputVCF :1818-1820) without a log10: the
 // host derives, with glibc's log10 in that very expression, the smallest q = 1 - pb giving GQ <= k for every
-// k (c_gq_thr[k], decreasing in k); a float log10 guesses k and at most a step or two against the thresholds
-// makes it exact.  Identical to the reference's glibc result for every double pb.
+// k (c_gq_thr[k], decreasing in k), so GQ = #{k < 100 : q < thr[k]} (q >= 1e-10 keeps it <= 100).  A float
+// log10 guess g is within 1 of that count (its error is < 1e-4 on -10 log10 q <= 100), so counting over the four
+// thresholds [g-2, g+2) -- one round of independent LDS reads, no loop, no branch -- gives it exactly.
+// Identical to the reference's glibc result for every double pb.
 __constant__ double c_gq_thr[101];
 // (thr: the block's LDS copy of c_gq_thr -- the lookups' index diverges, so they are not scalar loads)
 __device__ __forceinline__ int d_gq(double pb, const double* thr) {
-  if (pb > 0.9999999999) return 100;
   const double q = 1. - pb;
-  int k = (int)(-10.0f * __log10f((float)q) + 0.5f);
-  k = k < 0 ? 0 : k > 100 ? 100 : k;
-  while (k < 100 && q < thr[k]) k++;
-  while (k > 0 && q >= thr[k - 1]) k--;
-  return k;
+  const int g = (int)(-10.0f * __log10f((float)q) + 0.5f);   // (q = 0: +inf saturates; the select below wins)
+  const int base = min(max(g - 2, 0), 96);
+  int k = base;
+#pragma unroll
+  for (int i = 0; i < 4; i++) k += q < thr[base + i] ? 1 : 0;
+  return pb > 0.9999999999 ? 100 : k;
 }
 __device__ __forceinline__ void load_gq_thr(double* s_gq) {
   for (int i = threadIdx.x; i < 101; i += blockDim.x) s_gq[i] = c_gq_thr[i];
@@ -2088,11 +2090,13 @@ __device__ __forceinline__ void load_gq_thr(double* s_gq) {
 
 // one person's genotype row entry: pm_geno_call (16 B), or in vcf_mode the 4-B pm_vcf_call (best, GQ, label:
 // FamilyLikelihoodSeq_VCF::OutputVCF prints no dosage), a quarter of the bytes of the row stream
+// V: vcf_mode known at compile time (0 / 1), or -1 = read A.vcf
+template <int V = -1>
 __device__ __forceinline__ void d_emit_call(const DevArgs& A, const double* s_gq, size_t idx, const double* post, int best,
                                             int8_t label, double dosage) {
   const double pb = post[best];
   const int gq = d_gq(pb, s_gq);
-  if (A.vcf) {
+  if (V < 0 ? A.vcf != 0 : V == 1) {
     pm_vcf_call c;
     c.best = (int8_t)best; c.gq = (int8_t)gq; c.label = label; c.pad = 0;
     ((pm_vcf_call*)A.calls)[idx] = c;
@@ -2172,19 +2176,27 @@ __device__ void d_kid_geno(int chrom, const uint8_t* pl, int np, const double* l
   out[0] = G11; out[1] = G12; out[2] = G22;
 }
 
-// LEAN nuclear family (autosome, <= 4 persons, not de novo): every PL lookup of the family is issued first (one
-// memory round trip instead of one per stage), then the arithmetic of hoist_nuc, CalcParentMarginal and
-// KidJointGenoLikelihood below in the same operation order -- the same values bit for bit
-__device__ __forceinline__ void lean_nuc_post(const DevArgs& A, const double* s_lk, const double* s_gq, const uint8_t* pl,
-                                              size_t out, int p0, int n, int g11, int g12, int g22, const double* pp) {
-  const int np = A.n_person;
-  double lF[3], lM[3], kl[2][3];
-  lF[0] = s_lk[PLB(pl, np, p0, g11)]; lF[1] = s_lk[PLB(pl, np, p0, g12)]; lF[2] = s_lk[PLB(pl, np, p0, g22)];
-  lM[0] = s_lk[PLB(pl, np, p0 + 1, g11)]; lM[1] = s_lk[PLB(pl, np, p0 + 1, g12)]; lM[2] = s_lk[PLB(pl, np, p0 + 1, g22)];
+// The 12 PL bytes of a nuclear family of <= 4 persons: (g11, g12, g22) of father, mother and the two kid slots
+// (a trio's second kid slot repeats its kid; every read stays inside the family)
+__device__ __forceinline__ void lean_fam_bytes(const uint8_t* pl, int np, int p0, int n, int g11, int g12, int g22, uint32_t* by) {
+  const uint8_t *P11 = pl + (size_t)g11 * np, *P12 = pl + (size_t)g12 * np, *P22 = pl + (size_t)g22 * np;
 #pragma unroll
-  for (int i = 0; i < 2; i++) {
-    const int pi = p0 + 2 + (2 + i < n ? i : 0);
-    kl[i][0] = s_lk[PLB(pl, np, pi, g11)]; kl[i][1] = s_lk[PLB(pl, np, pi, g12)]; kl[i][2] = s_lk[PLB(pl, np, pi, g22)];
+  for (int q = 0; q < 4; q++) {
+    const int pq = p0 + (q < 2 ? q : 2 + (q < n ? q - 2 : 0));
+    by[3 * q] = P11[pq]; by[3 * q + 1] = P12[pq]; by[3 * q + 2] = P22[pq];
+  }
+}
+
+// LEAN nuclear family (autosome, <= 4 persons, not de novo) from its 12 PL bytes (lean_fam_bytes, loaded ahead by
+// the caller): the arithmetic of hoist_nuc, CalcParentMarginal and KidJointGenoLikelihood below in the same
+// operation order -- the same values bit for bit
+template <bool VCF>
+__device__ __forceinline__ void lean_nuc_post(const DevArgs& A, const double* s_lk, const double* s_gq, const uint32_t* by,
+                                              size_t out, int p0, int n, const double* pp) {
+  double lF[3], lM[3], kl[2][3];
+#pragma unroll
+  for (int t = 0; t < 3; t++) {
+    lF[t] = s_lk[by[t]]; lM[t] = s_lk[by[3 + t]]; kl[0][t] = s_lk[by[6 + t]]; kl[1][t] = s_lk[by[9 + t]];
   }
   double kids[9];
 #pragma unroll
@@ -2210,7 +2222,7 @@ __device__ __forceinline__ void lean_nuc_post(const DevArgs& A, const double* s_
     if (j == 0) { q11 = m[0] + m[1] + m[2]; q12 = m[3] + m[4] + m[5]; q22 = m[6] + m[7] + m[8]; }
     else { q11 = m[0] + m[3] + m[6]; q12 = m[1] + m[4] + m[7]; q22 = m[2] + m[5] + m[8]; }
     const double sum = q11 + q12 + q22;
-    if (A.vcf) {   // one quotient: post[best]
+    if constexpr (VCF) {   // one quotient: post[best]
       const int best = d_best3(q11, q12, q22);
       const double qb = best == 0 ? q11 : best == 1 ? q12 : q22;
       d_emit_vcf(A, s_gq, out + p0 + j, sum != 0 ? qb / sum : 0.0, best, PM_LBL_VCF_DIPLOID);
@@ -2218,7 +2230,7 @@ __device__ __forceinline__ void lean_nuc_post(const DevArgs& A, const double* s_
     }
     double post[3] = {0, 0, 0};
     if (sum != 0) { post[0] = q11 / sum; post[1] = q12 / sum; post[2] = q22 / sum; }
-    d_emit_call(A, s_gq, out + p0 + j, post, d_best3(q11, q12, q22), PM_LBL_VCF_DIPLOID, post[1] + post[2] * 2);
+    d_emit_call<0>(A, s_gq, out + p0 + j, post, d_best3(q11, q12, q22), PM_LBL_VCF_DIPLOID, post[1] + post[2] * 2);
   }
 #pragma unroll
   for (int j = 2; j < 4; j++) {   // KidJointGenoLikelihood :798-835, autosomal
@@ -2250,7 +2262,7 @@ __device__ __forceinline__ void lean_nuc_post(const DevArgs& A, const double* s_
       if (!z22) g[2] = g[2] + (two ? q22 * lo : q22) * w;
     }
     const double sum = g[0] + g[1] + g[2];
-    if (A.vcf) {
+    if constexpr (VCF) {
       // d_best3 over the quotients g[t] / sum (sum > 0, g >= 0: division is monotone) is the first t whose
       // quotient equals the largest one, post[b] with b = d_best3(g); an earlier quotient can only equal it
       // when its g is within a rounding of g[b], so the other divisions are done only then
@@ -2269,13 +2281,12 @@ __device__ __forceinline__ void lean_nuc_post(const DevArgs& A, const double* s_
     }
     double post[3] = {0, 0, 0};
     if (sum != 0.0) { post[0] = g[0] / sum; post[1] = g[1] / sum; post[2] = g[2] / sum; }
-    d_emit_call(A, s_gq, out + p0 + j, post, d_best3(post[0], post[1], post[2]), PM_LBL_VCF_DIPLOID, post[1] + post[2] * 2);
+    d_emit_call<0>(A, s_gq, out + p0 + j, post, d_best3(post[0], post[1], post[2]), PM_LBL_VCF_DIPLOID, post[1] + post[2] * 2);
   }
 }
 
-// LEAN: autosome, no extended family, nuclear families of <= 4 persons (the common case): the chrX/Y/MT
-// branches fold away and the generic kid path is not compiled, so the kernel runs at a higher occupancy.
-template <bool DN, bool ES, bool LEAN = false>
+// (autosomal nuclear families of <= 4 persons without the de novo model and extended families: k_posterior_lean)
+template <bool DN, bool ES>
 __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
   __shared__ double s_lk[256];
   __shared__ double s_M[100];
@@ -2299,7 +2310,7 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
     const size_t out = (size_t)row * np;   // genotype row index base
     const int a1 = R->allele1, a2 = R->allele2;
     const int g11 = d_gi(a1, a1), g12 = d_gi(a1, a2), g22 = d_gi(a2, a2);
-    const int chrom = LEAN ? (int)PM_CHR_AUTO : A.chrom;
+    const int chrom = A.chrom;
     constexpr int dn = DN ? 1 : 0;
     // CalcPostProb freq (main.cpp:576-587)
     const double freq = (R->maxidx == 0) ? (dn ? 1.0 : 1 - A.theta) : R->af;
@@ -2333,12 +2344,6 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
       }
       if (ES && (kind == PM_FAM_EXTENDED || (A.nuc_es && kind == PM_FAM_NUCLEAR))) continue;   // k_posterior_es
       if (kind != PM_FAM_NUCLEAR) continue;
-      if constexpr (LEAN && !DN) {
-        double pp[9];
-        d_parent_prior((!A.n_fam_gt1 && !is_mono) ? PR_TRIO : PR_AUTO, freq, pp);
-        lean_nuc_post(A, s_lk, s_gq, pl, out, p0, n, g11, g12, g22, pp);
-        continue;
-      }
       // CalcParentMarginal(_denovo) at freq
       ItemCtx I;
       I.a1 = a1; I.a2 = a2; I.g11 = g11; I.g12 = g12; I.g22 = g22; I.denovo = dn; I.sex = msex; I.chrom = chrom;
@@ -2412,7 +2417,6 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
           double post[3] = {0, 0, 0};
           if (sum != 0.0) { post[0] = g[0] / sum; post[1] = g[1] / sum; post[2] = g[2] / sum; }
           d_emit_call(A, s_gq, out + p, post, d_best3(post[0], post[1], post[2]), d_vcf_label(chrom, sx), post[1] + post[2] * 2);
-        } else if (LEAN) {   // (every nuclear family has <= 4 persons: the branch above took them)
         } else if (!dn) {   // KidJointGenoLikelihood :798-835
           double J[9][3];
           for (int k = 0; k < 9; k++) {
@@ -2475,48 +2479,74 @@ __global__ void __launch_bounds__(256) k_posterior(DevArgs A) {
   }
 }
 
-// LEAN posteriors (autosome, no de novo model, nuclear families of <= 4 persons and single founders), row-blocked:
-// a block takes one emitted row at a time and its threads stride over the row's families (fam_perm order: one
-// family size per stretch of lanes), so the row's set-up -- its result fields, genotype indices, frequency and the
-// HWE parent prior SetParentPrior (:318-368) -- runs once per thread and row instead of once per (row, family), and
-// no work index is divided.  Same arithmetic, in the same order, as k_posterior<false, false, true>.
+// LEAN posteriors (autosome, no de novo model, nuclear families of <= 4 persons and founder families),
+// row-blocked: a block takes one emitted row at a time and its threads stride over the row's families in
+// fam_perm order (one family size per stretch of lanes).  The family table (fam_perm order, packed first person |
+// persons << 24 | nuclear << 31) sits in LDS, so a family's PL addresses need no global round trip; the row's
+// set-up (genotype indices, frequency, SetParentPrior :318-368) runs once per thread and row, and its successor's
+// result fields are loaded while the row is computed.  VCF: vcf_mode rows (A.vcf).  Same arithmetic, in the same
+// order, as k_posterior.
+struct LeanRow {
+  const uint8_t* pl;
+  size_t out;
+  int g11, g12, g22;
+  double freq;
+  int mono;
+};
+__device__ __forceinline__ void lean_row(const DevArgs& A, int row, LeanRow& r) {
+  const int site = A.row_site[row];
+  const pm_site_result* R = A.res + site;
+  r.pl = A.pl + (size_t)site * A.n_person * 10;
+  r.out = (size_t)row * A.n_person;
+  const int a1 = R->allele1, a2 = R->allele2;
+  r.g11 = d_gi(a1, a1); r.g12 = d_gi(a1, a2); r.g22 = d_gi(a2, a2);
+  r.mono = R->maxidx == 0 ? 1 : 0;
+  r.freq = r.mono ? 1 - A.theta : R->af;   // main.cpp:576-587
+}
+template <bool VCF>
 __global__ void __launch_bounds__(256) k_posterior_lean(DevArgs A) {
   __shared__ double s_lk[256];
   __shared__ double s_gq[101];
+  extern __shared__ uint32_t s_fam[];   // [n_fam]
   for (int i = threadIdx.x; i < 256; i += blockDim.x) s_lk[i] = A.lktab[i];
   load_gq_thr(s_gq);
+  for (int fi = threadIdx.x; fi < A.n_fam; fi += blockDim.x) {
+    const int f = A.fam_perm[fi];
+    const int p0 = A.fam_start[f], n = A.fam_start[f + 1] - p0;
+    s_fam[fi] = (uint32_t)p0 | (uint32_t)n << 24 | (A.fam_kind[f] == PM_FAM_NUCLEAR ? 1u << 31 : 0u);
+  }
   __syncthreads();
-  const int rows = A.counts[3], np = A.n_person;
-  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
-    const int site = A.row_site[row];
-    const pm_site_result* R = A.res + site;
-    const uint8_t* pl = A.pl + (size_t)site * np * 10;
-    const size_t out = (size_t)row * np;
-    const int a1 = R->allele1, a2 = R->allele2;
-    const int g11 = d_gi(a1, a1), g12 = d_gi(a1, a2), g22 = d_gi(a2, a2);
-    const double freq = (R->maxidx == 0) ? 1 - A.theta : R->af;   // main.cpp:576-587
-    const int is_mono = R->maxidx == 0 ? 1 : 0;
+  const int rows = A.counts[3], np = A.n_person, nf = A.n_fam;
+  int row = blockIdx.x;
+  if (row >= rows || (int)threadIdx.x >= nf) return;
+  LeanRow cur, nxt;
+  lean_row(A, row, cur);
+  for (; row < rows; row += gridDim.x) {
+    if (row + (int)gridDim.x < rows) lean_row(A, row + gridDim.x, nxt);
     double pp[9];
-    d_parent_prior((!A.n_fam_gt1 && !is_mono) ? PR_TRIO : PR_AUTO, freq, pp);
-    const double fq = freq, gq = 1 - freq;
+    d_parent_prior((!A.n_fam_gt1 && !cur.mono) ? PR_TRIO : PR_AUTO, cur.freq, pp);
+    const double fq = cur.freq, gq = 1 - cur.freq;
     const double pr0 = fq * fq, pr1 = fq * gq * 2, pr2 = gq * gq;   // CalcPostProb_SinglePerson's HWE prior (:754-795)
-    for (int fi = threadIdx.x; fi < A.n_fam; fi += blockDim.x) {
-      const int f = A.fam_perm[fi];
-      const int p0 = A.fam_start[f], n = A.fam_start[f + 1] - p0, kind = A.fam_kind[f];
-      if (kind == PM_FAM_NUCLEAR) {
-        lean_nuc_post(A, s_lk, s_gq, pl, out, p0, n, g11, g12, g22, pp);
-      } else if (kind == PM_FAM_FOUNDERS) {
+    for (int fi = threadIdx.x; fi < nf; fi += blockDim.x) {
+      const uint32_t d = s_fam[fi];
+      const int p0 = d & 0xFFFFFF, n = (d >> 24) & 127;
+      if (d >> 31) {
+        uint32_t by[12];
+        lean_fam_bytes(cur.pl, np, p0, n, cur.g11, cur.g12, cur.g22, by);
+        lean_nuc_post<VCF>(A, s_lk, s_gq, by, cur.out, p0, n, pp);
+      } else {
         for (int j = 0; j < n; j++) {
           const int p = p0 + j;
-          const double l11 = s_lk[PLB(pl, np, p, g11)], l12 = s_lk[PLB(pl, np, p, g12)], l22 = s_lk[PLB(pl, np, p, g22)];
+          const double l11 = s_lk[PLB(cur.pl, np, p, cur.g11)], l12 = s_lk[PLB(cur.pl, np, p, cur.g12)], l22 = s_lk[PLB(cur.pl, np, p, cur.g22)];
           const double m11 = l11 * pr0, m12 = l12 * pr1, m22 = l22 * pr2;
           const double sum = m11 + m12 + m22;
           double post[3] = {0, 0, 0};
           if (sum != 0) { post[0] = m11 / sum; post[1] = m12 / sum; post[2] = m22 / sum; }
-          d_emit_call(A, s_gq, out + p, post, d_best3(m11, m12, m22), PM_LBL_VCF_DIPLOID, post[1] + post[2] * 2);
+          d_emit_call<VCF ? 1 : 0>(A, s_gq, cur.out + p, post, d_best3(m11, m12, m22), PM_LBL_VCF_DIPLOID, post[1] + post[2] * 2);
         }
       }
     }
+    cur = nxt;
   }
 }
 
@@ -2712,6 +2742,7 @@ struct pm_engine {
   std::vector<int> fam_start_h;
   std::vector<int8_t> sex_h;
   int single_nuclear = 0, max_nuc = 0;
+  int max_fam = 0;            // largest family (persons)
   double prior = 0;
   int n_founders = 0, male_founders = 0, female_founders = 0;
   // device buffers
@@ -2985,8 +3016,10 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
   E->n_founders = ped->n_founders; E->male_founders = ped->male_founders; E->female_founders = ped->female_founders;
   // a lone nuclear family is evaluated once at 0.5 (FamilyLikelihoodSeq.cpp:91-104); the VCF path always runs Brent
   E->single_nuclear = (!E->vcf && ped->n_fam == 1 && ped->fam_kind[0] == PM_FAM_NUCLEAR) ? 1 : 0;
-  for (int f = 0; f < ped->n_fam; f++)
+  for (int f = 0; f < ped->n_fam; f++) {
     if (ped->fam_kind[f] == PM_FAM_NUCLEAR) E->max_nuc = std::max(E->max_nuc, ped->fam_start[f + 1] - ped->fam_start[f]);
+    E->max_fam = std::max(E->max_fam, ped->fam_start[f + 1] - ped->fam_start[f]);
+  }
   for (int f = 0; f < ped->n_fam; f++) {
     if (ped->fam_kind[f] != PM_FAM_NUCLEAR) E->has_fp = true;
     if (ped->fam_kind[f] == PM_FAM_EXTENDED) E->n_ext++;
@@ -3647,10 +3680,13 @@ static int run_pipeline(pm_engine* E, int n, const uint8_t* pl, const uint32_t* 
   HIP_TRY(hipGetLastError());
   {
     const bool es = (E->use_plan1 ? E->n_ext1 : E->n_ext) > 0;
-    const bool lean = !E->par.denovo && !es && E->chrom == PM_CHR_AUTO && E->max_nuc <= 4 && !E->use_plan1;
+    // k_posterior_lean: its LDS family table packs first person (24 bits) and persons (7 bits), <= 48 KB
+    const bool lean = !E->par.denovo && !es && E->chrom == PM_CHR_AUTO && E->max_nuc <= 4 && !E->use_plan1 &&
+                      E->n_fam <= 12288 && E->max_fam <= 127 && E->n_person < (1 << 24);
     void (*post)(DevArgs) = E->par.denovo ? (es ? k_posterior<true, true> : k_posterior<true, false>)
-                          : es ? k_posterior<false, true> : lean ? k_posterior_lean : k_posterior<false, false>;
-    hipLaunchKernelGGL(post, dim3(E->grid_post), dim3(256), 0, E->stream, A);
+                          : es ? k_posterior<false, true> : lean ? (E->vcf ? k_posterior_lean<true> : k_posterior_lean<false>)
+                                                                 : k_posterior<false, false>;
+    hipLaunchKernelGGL(post, dim3(E->grid_post), dim3(256), lean ? (size_t)E->n_fam * 4 : 0, E->stream, A);
     const pmjit::Kernel* K = es && A.n_es_pers > 0 ? jit_kernel(E) : nullptr;
     if (K && K->fn_post) {   // compiled schedule: one thread per (row, peeled family), all its persons' 3 peels in registers
       HIP_TRY(hipGetLastError());

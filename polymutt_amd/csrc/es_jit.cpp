@@ -371,13 +371,12 @@ struct GenoCall { double dosage; short best; short gq; signed char label; signed
 struct VcfCall { signed char best; signed char gq; signed char label; signed char pad; };
 // d_gq (engine.hip): GQ of OutputVCF :1818-1820 from the host's glibc thresholds, exact for every double
 __device__ __forceinline__ int gq_of(double pb, const double* thr) {
-  if (pb > 0.9999999999) return 100;
   const double q = 1. - pb;
-  int k = (int)(-10.0f * log10f((float)q) + 0.5f);
-  k = k < 0 ? 0 : k > 100 ? 100 : k;
-  while (k < 100 && q < thr[k]) k++;
-  while (k > 0 && q >= thr[k - 1]) k--;
-  return k;
+  const int g = (int)(-10.0f * log10f((float)q) + 0.5f);
+  const int base = min(max(g - 2, 0), 96);
+  int k = base;
+  for (int i = 0; i < 4; i++) k += q < thr[base + i] ? 1 : 0;
+  return pb > 0.9999999999 ? 100 : k;
 }
 // k_posterior_es's tail: post = l / sum, best = d_best3(l), GQ of post[best], DS = post12 + 2 post22
 __device__ __forceinline__ void emit(void* calls, size_t idx, double l11, double l12, double l22, int label, const double* thr,
