@@ -20,17 +20,22 @@ step() {   # step NAME SECONDS CMD...
   if [ $rc -ne 0 ]; then echo "step $name failed rc=$rc" >&2; tail -20 "$OUT/$name.err" >&2; exit $rc; fi
 }
 step fp64_peak 120 "$R/tools/fp64_peak"
+# the default bench line itself (with its cpu_baseline leg), as the driver runs it
+step bench 600 python3 $R/bench.py
 # default bench (3 overlapping engines): whole-step kernel mix; per-kernel durations there include GPU sharing
 step trace 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- $BENCH
 # one engine: each kernel alone on the GPU -- the per-kernel times the roofline uses
 step trace1 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace1" -o run -- $BENCH --engines 1
 # BASELINE config 4 shape (200 ext10 pedigrees, Elston-Stewart peeling), one engine
 step trace_ext10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_ext10" -o run -- $BENCH --engines 1 --shape ext10 --families 200 --batch 16384 --no-denovo --steps 8
+step trace_ext10dn 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_ext10dn" -o run -- $BENCH --engines 1 --shape ext10 --families 200 --batch 4096 --steps 6
 # BASELINE config 5 shape (2000 mixed families, --in_vcf engine mode), one engine
 step trace_cfg5 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_cfg5" -o run -- $BENCH --engines 1 --shape mixed --families 2000 --vcf --no-denovo --batch 65536 --steps 12
 step pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- $BENCH --engines 1 --steps 4 --warmup 1 --calib-steps 0
 step pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- $BENCH --engines 1 --steps 4 --warmup 1 --calib-steps 0
-step pmc_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES --output-format csv -d "$OUT/pmc_sq" -o run -- $BENCH --engines 1 --steps 4 --warmup 1 --calib-steps 0
+step pmc_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_INSTS_VMEM_RD --output-format csv -d "$OUT/pmc_sq" -o run -- $BENCH --engines 1 --steps 4 --warmup 1 --calib-steps 0
+step pmc_sq2 400 rocprofv3 --pmc SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA SQ_INSTS_VMEM_WR SQ_INSTS_SMEM --output-format csv -d "$OUT/pmc_sq2" -o run -- $BENCH --engines 1 --steps 4 --warmup 1 --calib-steps 0
+step pmc_sq3 400 rocprofv3 --pmc SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_sq3" -o run -- $BENCH --engines 1 --steps 4 --warmup 1 --calib-steps 0
 # the other BASELINE configs' bench lines (default three engines)
 B="python3 $R/bench.py --no-cpu-baseline"
 step cfg2 300 $B --shape trio --families 1000 --no-denovo --steps 100

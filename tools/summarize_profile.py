@@ -30,7 +30,8 @@ def main():
     src = os.path.join(ROOT, "gpurun_out", f"prof_{rnd}")
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
-    for sub, suffix in (("trace", ""), ("trace1", "_1engine"), ("trace_ext10", "_ext10")):
+    for sub, suffix in (("trace", "_3engines"), ("trace1", "_1engine"), ("trace_ext10", "_ext10"), ("trace_ext10dn", "_ext10dn"),
+                        ("trace_cfg5", "_cfg5")):
         if not os.path.exists(os.path.join(src, sub, "run_kernel_stats.csv")):
             continue
         shutil.copy(os.path.join(src, sub, "run_kernel_stats.csv"), os.path.join(dst, f"{rnd}_kernel_stats{suffix}.csv"))
@@ -38,13 +39,31 @@ def main():
         if bench:
             with open(os.path.join(dst, f"{rnd}_bench{suffix}.json"), "w") as fh:
                 fh.write(bench[-1] + "\n")
+    if os.path.exists(os.path.join(src, "bench.out")):   # the default bench line (3 engines, cpu_baseline)
+        bench = [l for l in open(os.path.join(src, "bench.out")).read().splitlines() if l.startswith("{")]
+        if bench:
+            with open(os.path.join(dst, f"{rnd}_bench.json"), "w") as fh:
+                fh.write(bench[-1] + "\n")
+    others = []
+    for name in ("cfg2", "cfg3plain", "cfg4", "cfg4dn", "cfg5"):
+        path = os.path.join(src, name + ".out")
+        if os.path.exists(path):
+            lines = [l for l in open(path).read().splitlines() if l.startswith("{")]
+            if lines:
+                d = json.loads(lines[-1])
+                d["profile_step"] = name
+                others.append(json.dumps(d))
+    if others:
+        with open(os.path.join(dst, f"{rnd}_bench_other_configs.jsonl"), "w") as fh:
+            fh.write("\n".join(others) + "\n")
     peak = [l for l in open(os.path.join(src, "fp64_peak.out")).read().splitlines() if l.startswith("{")]
     if peak:
         with open(os.path.join(dst, f"{rnd}_fp64_peak.json"), "w") as fh:
             fh.write(peak[-1] + "\n")
     acc = defaultdict(lambda: defaultdict(float))
     disp = defaultdict(set)
-    for sub in ("pmc_fetch", "pmc_write", "pmc_sq"):
+    src_of = {}   # counter -> the pass it was collected in
+    for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sq2", "pmc_sq3"):
         path = os.path.join(src, sub, "run_counter_collection.csv")
         if not os.path.exists(path):
             continue
@@ -52,14 +71,19 @@ def main():
             k = short(row["Kernel_Name"])
             acc[k][row["Counter_Name"]] += float(row["Counter_Value"])
             disp[(k, sub)].add(row["Dispatch_Id"])
+            src_of[row["Counter_Name"]] = sub
     out = {}
     for k, counters in acc.items():
         d = {}
         for c, v in counters.items():
-            sub = "pmc_fetch" if c == "FETCH_SIZE" else "pmc_write" if c == "WRITE_SIZE" else "pmc_sq"
+            sub = src_of[c]
             n = max(1, len(disp[(k, sub)]))
             d[c + "_per_dispatch"] = v / n
             d["dispatches_" + sub] = n
+        if "SQ_WAVE_CYCLES_per_dispatch" in d:
+            for c in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS"):
+                if c + "_per_dispatch" in d:
+                    d[c + "_frac_of_wave_cycles"] = d[c + "_per_dispatch"] / d["SQ_WAVE_CYCLES_per_dispatch"]
         if "FETCH_SIZE_per_dispatch" in d:
             # FETCH_SIZE / WRITE_SIZE are reported in KiB
             d["hbm_read_bytes_per_dispatch"] = 2 * d["FETCH_SIZE_per_dispatch"] * 1024
