@@ -120,6 +120,7 @@ struct DevArgs {
   int* row_blk;            // k_rows_count / k_rows: written records per 1024-site block
   int pf_npad;             // lean kernel: > 0 = the item's 3 genotype planes are prefetched into LDS (stride)
   int dn_pf;               // lean --denovo kernel: PL windows staged through LDS by LDS-DMA (hoist_poly4_dn_pf)
+  int quad_full;           // QUAD plan (hoist_quad): slot rows below this have no empty lane
   // tables
   const double* lktab;     // [256]
   const double* M;         // [100] genotype mutation matrix
@@ -714,7 +715,7 @@ __device__ __forceinline__ void fam_poly4(const uint32_t* by, int nn, const doub
 // chunk overlap instead of running slot after slot.  Arithmetic is hoist_nuc's, in the same order.
 template <int S, int T>
 __device__ __forceinline__ void hoist_poly4(const DevArgs& A, const int* su, const ItemCtx& I, const uint8_t* pl, const double* lk,
-                                            double (*a)[5], unsigned& live) {
+                                            double (*a)[5]) {
   constexpr int C = S < PM_HOIST_CHUNK ? S : PM_HOIST_CHUNK;
   const size_t np = (size_t)A.n_person;
   const uint8_t* P11 = pl + I.g11 * np;   // the three genotype planes of the item
@@ -729,7 +730,6 @@ __device__ __forceinline__ void hoist_poly4(const DevArgs& A, const int* su, con
 #pragma unroll
     for (int j = 0; j < C; j++) {
       const int u = uu[c0 + j];
-      const bool nuc = u != 0;
       nn[j] = unit_nn(u);
 #pragma unroll
       for (int q = 0; q < 4; q++) {
@@ -738,7 +738,6 @@ __device__ __forceinline__ void hoist_poly4(const DevArgs& A, const int* su, con
         by[j][3 * q + 1] = P12[pp];
         by[j][3 * q + 2] = P22[pp];
       }
-      if (nuc) live |= 1u << (c0 + j);
     }
 #pragma unroll
     for (int j = 0; j < C; j++) fam_poly4(by[j], nn[j], lk, a[c0 + j]);
@@ -783,7 +782,7 @@ __device__ __forceinline__ void prefetch_planes(const DevArgs& A, const int* ite
 #endif
 template <int S, int T>
 __device__ __forceinline__ void hoist_poly4_lds(const DevArgs& A, const int* su, const uint8_t* buf, const double* lk,
-                                                double (*a)[5], unsigned& live) {
+                                                double (*a)[5]) {
   const int npad = A.pf_npad;
   constexpr int C = S < PM_HOIST_CHUNK_LDS ? S : PM_HOIST_CHUNK_LDS;
   int uu[S];
@@ -801,7 +800,6 @@ __device__ __forceinline__ void hoist_poly4_lds(const DevArgs& A, const int* su,
       by[3 * q + 1] = buf[npad + pp];
       by[3 * q + 2] = buf[2 * npad + pp];
     }
-    if (nn) live |= 1u << s;
     fam_poly4(by, nn, lk, a[s]);
   }
 }
@@ -815,7 +813,7 @@ __device__ __forceinline__ void hoist_poly4_lds(const DevArgs& A, const int* su,
 #endif
 template <int S, int T>
 __device__ __forceinline__ void hoist_poly4_dn(const DevArgs& A, const int* su, const ItemCtx& I, const uint8_t* pl, const double* lk,
-                                               const double* M, double (*a)[5], unsigned& live) {
+                                               const double* M, double (*a)[5]) {
   constexpr int C = S < PM_HOIST_CHUNK_DN ? S : PM_HOIST_CHUNK_DN;
   const size_t np = (size_t)A.n_person;
   int uu[S];
@@ -831,7 +829,6 @@ __device__ __forceinline__ void hoist_poly4_dn(const DevArgs& A, const int* su, 
 #pragma unroll
     for (int j = 0; j < C; j++) {
       const int u = uu[c0 + j];
-      const bool nuc = u != 0;
       nn[j] = unit_nn(u);
 #pragma unroll
       for (int q = 0; q < 2; q++) {
@@ -846,7 +843,6 @@ __device__ __forceinline__ void hoist_poly4_dn(const DevArgs& A, const int* su, 
 #pragma unroll
         for (int g = 0; g < 10; g++) kid[j][q][g] = R[g * np];
       }
-      if (nuc) live |= 1u << (c0 + j);
     }
 #pragma unroll
     for (int j = 0; j < C; j++) {   // branch-free over the lanes' family sizes (see fam_poly4)
@@ -923,7 +919,7 @@ __device__ __forceinline__ void dn_pf_issue(const DevArgs& A, const uint8_t* pl,
 
 template <int S, int T>
 __device__ __forceinline__ void hoist_poly4_dn_pf(const DevArgs& A, const int* su, const ItemCtx& I, const uint8_t* pl,
-                                                  const double* lk, const double* M, double (*a)[5], unsigned& live,
+                                                  const double* lk, const double* M, double (*a)[5],
                                                   uint8_t* wbuf) {
   static_assert(S % DN_PF_C == 0, "chunking");
   constexpr int C = DN_PF_C;
@@ -958,7 +954,6 @@ __device__ __forceinline__ void hoist_poly4_dn_pf(const DevArgs& A, const int* s
     for (int j = 0; j < C; j++) {
       const int u = uu[c0 + j];
       const int nn = unit_nn(u);
-      if (u != 0) live |= 1u << (c0 + j);
       const uint8_t* W = cur + j * 10 * DN_PF_WIN;   // plane g of this slot at W[g * DN_PF_WIN + person - start]
       const int rel = u ? unit_first(u) - start_al[c0 + j] : 0;
       // every PL byte of the slot first (one LDS round trip), then every table lookup (a second), then the
@@ -1039,12 +1034,168 @@ __device__ __forceinline__ void hoist_poly4_dn_pf(const DevArgs& A, const int* s
   }
 }
 
-// Four interleaved (mantissa, exponent) accumulators: short dependency chains, few live registers.
-// Slots below `full` are occupied on every lane (families are dealt round-robin); only the slot rows at
-// or above it can be empty and are masked (h = 1).  LO selects the Horner direction (t = f / (1 - f) or
-// its inverse); the hot path is lane_poly_r, this form only serves f = 1.
-template <int S, bool LO>
-__device__ __forceinline__ void lane_poly_dir(double t, int full, unsigned live, const double (*a)[5], double& m, int& e) {
+// ---- QUAD plan (lean --denovo kernel; pm_engine::quad): families are 4-person nuclear families stored in order
+// (family f = persons 4f..4f+3) and dealt round-robin, so slot row s of the wave holds families 64 s + lane and
+// its persons are the 256-byte window [256 s, 256 s + 256) of every genotype plane, one aligned dword per lane
+// (father, mother, kid 1, kid 2).  Each slot's ten windows arrive in LDS by three LDS-DMA instructions (lane l
+// of instruction i copies 16 bytes of plane 4 i + l / 16: per-lane source offsets fixed for the kernel, the slot
+// in the scalar base) into a ring of QB slot buffers, QD_AHEAD slots ahead of the hoisting; the next item's
+// first QD_AHEAD slots are fetched while this item's Brent runs.  A slot is then 13 conflict-free ds_read_b32
+// and 26 table lookups -- no per-byte address arithmetic, no per-family selects (only the partial last slot row
+// needs the phantom family).
+#define QB 3
+#define QD_AHEAD 2
+#define QSLOT 3072   // 10 planes x 256 B + the third DMA instruction's tail
+#define QWAVE (QB * QSLOT)
+
+// Per-lane source offset of DMA instruction i within a slot window (plane 4 i + lane / 16, 16 B per lane); lanes
+// past plane 9 re-read plane 9 (their bytes land in the buffer's tail and are never read).
+__device__ __forceinline__ uint32_t quad_voff(int i, int np) {
+  const int lane = threadIdx.x & 63, g = min(4 * i + (lane >> 4), 9);
+  return (uint32_t)(g * np + (lane & 15) * 16);
+}
+
+// DMA of slot row s of one site block into an LDS slot buffer.  Rows that reach past the plane end (the partial
+// last row) clamp each lane's window start so that no read leaves the site block.  (Unsigned 32-bit lane offsets
+// on a uniform base: the scalar-base + vector-offset form of the DMA instruction, no 64-bit address per lane.)
+__device__ __forceinline__ void quad_dma(const uint8_t* site, int s, int np, const uint32_t* voff, uint8_t* dst) {
+  if (256 * (s + 1) <= np) {
+    const uint8_t* src = site + 256 * s;
+    asm volatile("" : "+s"(src));   // an opaque scalar base: each lane adds only its 32-bit offset (saddr form)
+#pragma unroll
+    for (int i = 0; i < 3; i++) __builtin_amdgcn_global_load_lds((const void*)(src + voff[i]), (void*)(dst + i * 1024), 16, 0, 0);
+  } else {
+    int lane = threadIdx.x & 63;
+    asm volatile("" : "+v"(lane));   // (no per-slot offsets hoisted out of the item loop)
+    const int o = min(256 * s + (lane & 15) * 16, np - 16);
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      const int g = min(4 * i + (lane >> 4), 9);
+      __builtin_amdgcn_global_load_lds((const void*)(site + (uint32_t)(g * np + o)), (void*)(dst + i * 1024), 16, 0, 0);
+    }
+  }
+}
+
+// One dword into LDS by LDS-DMA, every lane copying the same source (dst[0..63] all hold it).
+__device__ __forceinline__ void quad_aux(const void* src, int* dst) {
+  __builtin_amdgcn_global_load_lds(src, (void*)dst, 4, 0, 0);
+}
+
+// The first QD_AHEAD slots of an item (issued ahead: before the previous item's Brent loop).
+__device__ __forceinline__ void quad_prefetch(const DevArgs& A, int item, const uint32_t* voff, uint8_t* ring) {
+  const int site = item >> 3;
+  int np = A.n_person;
+  asm volatile("" : "+s"(np));   // (keeps the clamped-row offsets from being hoisted out of the item loop)
+  const uint8_t* pl = A.pl + (size_t)site * np * 10;
+#pragma unroll
+  for (int s = 0; s < QD_AHEAD; s++) quad_dma(pl, s, np, voff, ring + s * QSLOT);
+}
+
+// One family's quartic from its kid terms (D[q] = (D11, D12, D22) of kid q: CalcDenovoMutLk's dot products for de
+// novo items, (l11, l12, l22) otherwise) and parent likelihoods: the sums of hoist_nuc's c9 that share a kid factor
+// (likelihoodONEKid(_denovo) gives k = 1, 3 / 2, 6 / 5, 7 equal terms, :1202-1296) are factored, and the powers of
+// two of those terms (0.5, 0.25) are applied once at the end (exact scalings).  Equal to fold_poly(c9) in real
+// arithmetic; non-negative throughout (POLY numerics).
+__device__ __forceinline__ void quad_poly4(const double (*D)[3], const double* lF, const double* lM, double* a) {
+  double At[2], Bt[2], Ct[2];
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    At[q] = D[q][0] + D[q][1];                     // 2 x likelihoodONEKid k = 1, 3
+    Bt[q] = D[q][1] + D[q][2];                     // 2 x k = 5, 7
+    Ct[q] = fma(2.0, D[q][1], D[q][0]) + D[q][2];  // 4 x k = 4
+  }
+  const double P0 = D[0][0] * D[1][0], P2 = D[0][1] * D[1][1], P8 = D[0][2] * D[1][2];
+  const double PA = At[0] * At[1], PB = Bt[0] * Bt[1], PC = Ct[0] * Ct[1];
+  const double s01 = fma(lF[0], lM[1], lF[1] * lM[0]);
+  const double s02 = fma(lF[0], lM[2], lF[2] * lM[0]);
+  const double s12 = fma(lF[1], lM[2], lF[2] * lM[1]);
+  a[0] = P0 * (lF[0] * lM[0]);
+  a[1] = (0.5 * PA) * s01;
+  a[2] = fma(P2, s02, (0.25 * PC) * (lF[1] * lM[1]));
+  a[3] = (0.5 * PB) * s12;
+  a[4] = P8 * (lF[2] * lM[2]);
+}
+
+// QUAD hoisting of one item: slots 0 .. QD_AHEAD - 1 are already in the ring (quad_prefetch).  vmcnt counts in
+// issue order (loads, stores and LDS-DMA together), so waiting until only the next slot's three DMA instructions
+// may be outstanding means this slot's have landed.
+template <int S, bool DNV>
+__device__ __forceinline__ void hoist_quad_t(const DevArgs& A, const ItemCtx& I, const uint8_t* pl, const double* lk,
+                                             const double* M, double (*a)[5], uint8_t* ring, const uint32_t* voff) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t* rw = (const uint32_t*)ring + lane;   // the lane's dword of plane g, slot buffer b: rw[(b * QSLOT + g * 256) / 4]
+  const int o11 = I.g11 * 64, o12 = I.g12 * 64, o22 = I.g22 * 64;
+  // re-read per item (opaque), so the compiler does not keep S slot predicates live across the Brent loop
+  int qfull = A.quad_full, nfam = A.n_fam, npo = A.n_person;
+  asm volatile("" : "+s"(qfull), "+s"(nfam), "+s"(npo));
+#pragma unroll
+  for (int s = 0; s < S; s++) {
+    if (s + 1 < S) __builtin_amdgcn_s_waitcnt(0x0F70 | 3);   // vmcnt(3): slot s has landed
+    else __builtin_amdgcn_s_waitcnt(0x0F70);                   // vmcnt(0)
+    __builtin_amdgcn_sched_barrier(0);
+    const uint32_t* b = rw + (s % QB) * (QSLOT / 4);
+    // byte j of a plane dword: person j of the family (0 father, 1 mother, 2 / 3 kids)
+    uint32_t w[3];   // planes g11, g12, g22
+    w[0] = b[o11]; w[1] = b[o12]; w[2] = b[o22];
+    double lF[3], lM[3], D[2][3];
+    if constexpr (DNV) {
+      uint32_t wg[10];   // planes 0-9
+#pragma unroll
+      for (int g = 0; g < 10; g++) wg[g] = b[g * 64];
+#pragma unroll
+      for (int k = 0; k < 3; k++) { lF[k] = lk[w[k] & 0xFF]; lM[k] = lk[(w[k] >> 8) & 0xFF]; }
+      double pg[2][10];   // both kids' 20 table lookups in flight together
+#pragma unroll
+      for (int g = 0; g < 10; g++) { pg[0][g] = lk[(wg[g] >> 16) & 0xFF]; pg[1][g] = lk[wg[g] >> 24]; }
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + QD_AHEAD < S) quad_dma(pl, s + QD_AHEAD, npo, voff, ring + ((s + QD_AHEAD) % QB) * QSLOT);
+      lds_cdp M11 = (lds_cdp)(M + I.g11 * 10), M12 = (lds_cdp)(M + I.g12 * 10), M22 = (lds_cdp)(M + I.g22 * 10);
+      asm volatile("" : "+v"(M11), "+v"(M12), "+v"(M22));
+#pragma unroll
+      for (int q = 0; q < 2; q++) D[q][0] = D[q][1] = D[q][2] = 0.0;
+#pragma unroll
+      for (int g = 0; g < 10; g++) {   // CalcDenovoMutLk (:1553-1562), each matrix entry read once for both kids
+        const double m11 = M11[g], m12 = M12[g], m22 = M22[g];
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+          D[q][0] = fma(m11, pg[q][g], D[q][0]);
+          D[q][1] = fma(m12, pg[q][g], D[q][1]);
+          D[q][2] = fma(m22, pg[q][g], D[q][2]);
+        }
+      }
+    } else {   // cfg-7 items: likelihoodONEKid's autosomal terms on the item's three planes
+#pragma unroll
+      for (int k = 0; k < 3; k++) { lF[k] = lk[w[k] & 0xFF]; lM[k] = lk[(w[k] >> 8) & 0xFF]; }
+#pragma unroll
+      for (int q = 0; q < 2; q++)
+#pragma unroll
+        for (int k = 0; k < 3; k++) D[q][k] = lk[(w[k] >> (16 + 8 * q)) & 0xFF];
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + QD_AHEAD < S) quad_dma(pl, s + QD_AHEAD, npo, voff, ring + ((s + QD_AHEAD) % QB) * QSLOT);
+    }
+    quad_poly4(D, lF, lM, a[s]);
+    if (s >= qfull) {   // the partial last slot row: empty lanes hold the phantom family (f + g)^4
+      const bool empty = 64 * s + lane >= nfam;
+      a[s][0] = empty ? 1.0 : a[s][0]; a[s][1] = empty ? 4.0 : a[s][1]; a[s][2] = empty ? 6.0 : a[s][2];
+      a[s][3] = empty ? 4.0 : a[s][3]; a[s][4] = empty ? 1.0 : a[s][4];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// de novo items and cfg-7 items (uniform per item) take separate straight-line slot loops
+template <int S>
+__device__ __forceinline__ void hoist_quad(const DevArgs& A, const ItemCtx& I, const uint8_t* pl, const double* lk,
+                                           const double* M, double (*a)[5], uint8_t* ring, const uint32_t* voff) {
+  if (I.denovo) hoist_quad_t<S, true>(A, I, pl, lk, M, a, ring, voff);
+  else hoist_quad_t<S, false>(A, I, pl, lk, M, a, ring, voff);
+}
+
+// f = 1 (the generic-path de novo monomorphism item): L_fam(1) = a0, the f^4 coefficient; an empty slot's
+// phantom family (f + g)^4 has a0 = 1, so no slot needs masking.  Four interleaved (mantissa, exponent)
+// accumulators, renormalised after every factor.
+template <int S>
+__device__ __forceinline__ void lane_poly_top(const double (*a)[5], double& m, int& e) {
   constexpr int NA = S < 4 ? S : 4;
   double am[NA];
   int ae[NA];
@@ -1052,12 +1203,8 @@ __device__ __forceinline__ void lane_poly_dir(double t, int full, unsigned live,
   for (int j = 0; j < NA; j++) { am[j] = 1.0; ae[j] = 0; }
 #pragma unroll
   for (int s = 0; s < S; s++) {
-    double h;
-    if (LO) h = fma(t, fma(t, fma(t, fma(t, a[s][0], a[s][1]), a[s][2]), a[s][3]), a[s][4]);
-    else h = fma(t, fma(t, fma(t, fma(t, a[s][4], a[s][3]), a[s][2]), a[s][1]), a[s][0]);
-    if (s >= full) h = ((live >> s) & 1) ? h : 1.0;
     int x;
-    am[s % NA] = frexp(am[s % NA] * h, &x);   // |am| in [0.5, 1), h >= ~1e-128 for nuclear families: no underflow
+    am[s % NA] = frexp(am[s % NA] * a[s][0], &x);
     ae[s % NA] += x;
   }
 #pragma unroll
@@ -1442,7 +1589,8 @@ constexpr int brent_waves() { return (NUM == PM_NUM_POLY && !GEN && (T == 64 || 
 // PF: lean kernel whose items' genotype planes are prefetched into LDS (prefetch_planes); no other hoisting path.
 // EP: extended families in polynomial form (coefficients from k_es_hoist, es_poly_eval per evaluation); the
 // reference-order peel (d_es_lk) is compiled out, and the block asks for 2 waves per SIMD.
-template <int T, int S, int NUM, bool GEN, bool ES, bool DN = false, bool PF = false, bool EP = false>
+// QD: lean --denovo kernel on a QUAD plan (hoist_quad: coalesced dword loads, prefetched across items).
+template <int T, int S, int NUM, bool GEN, bool ES, bool DN = false, bool PF = false, bool EP = false, bool QD = false>
 __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k_brent(DevArgs A, int list) {
   constexpr bool PROD = NUM != PM_NUM_EXACT;
   constexpr bool POLYK = NUM == PM_NUM_POLY && !GEN;
@@ -1463,7 +1611,6 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
 #pragma unroll
     for (int s = 0; s < S; s++) unit[s] = A.units[s * T + threadIdx.x];
   }
-  const int full = A.n_fam / T;   // POLY: slot rows below this are occupied on every lane
   const int nItems = A.counts[list];
   const int* items = A.items[list];
   int par = 0;
@@ -1474,18 +1621,47 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
   constexpr bool PFK = PF && NUM == PM_NUM_POLY && !GEN && !ES && !DN && T == 64;
   // PF on the lean de novo kernel: the 64 x 16 instantiation with only the LDS-staged hoisting compiled (the
   // direct-load hoisting of 16 de novo slots spills; this one keeps 1024 families on one wave per item)
-  constexpr bool DNPF_ONLY = PF && POLYK && DN && T == 64 && S == 16;
+  constexpr bool DNPF_ONLY = PF && POLYK && DN && T == 64 && S == 16 && !QD;
+  static_assert(!QD || (POLYK && DN && T == 64 && !ES), "QUAD plans run on the lean one-wave --denovo kernel");
   extern __shared__ uint8_t s_pf[];
   const bool pf = PFK && A.pf_npad > 0;
   if (pf) prefetch_planes(A, items, vb, nItems, s_pf);
   unsigned long long ev_acc = 0;   // evaluation count of this block's items: one atomic per block, at exit
   unsigned long long ph_h = 0, ph_e = 0, ph_n = 0, ph_t = 0;   // PM_PHASE_TIMING (A.phase): hoisting / evaluation split
   const int itEnd = min(nItems, A.es_it1);   // EP: this launch's chunk of the list [es_it0, es_it1)
+  // QD: this wave's LDS slot ring and the per-lane DMA source offsets; the first item's first slots
+  uint8_t* qring = s_pf + (QD ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * QWAVE : 0);
+  uint32_t qvoff[3];
+  // QD: the next item's index and the dword holding its reference base arrive by LDS-DMA as well (every lane
+  // copies the same dword: s_qaux[0..63] = the ref dword, s_qaux[64..127] = the item after it), so no load is
+  // waited for at the top of an item.  Issue order per item: ref dword, slot 0, slot 1, next item index.
+  __shared__ __attribute__((aligned(16))) int s_qaux[QD ? 128 : 1];
+  int q_item = 0;
+  if constexpr (QD) {
+#pragma unroll
+    for (int i = 0; i < 3; i++) qvoff[i] = quad_voff(i, A.n_person);
+    if (A.es_it0 + vb < itEnd) {
+      q_item = items[A.es_it0 + vb];
+      quad_aux(A.ref + ((q_item >> 3) & ~3), s_qaux);
+      quad_prefetch(A, q_item, qvoff, qring);
+      if (A.es_it0 + vb + (int)gridDim.x < itEnd) quad_aux(items + A.es_it0 + vb + gridDim.x, s_qaux + 64);
+    }
+  }
+  // QD: an item's results wait in LDS and are stored after the next item's hoisting, so that they are older
+  // than that item's prefetch in vmcnt order
+  __shared__ double s_pend[QD ? 2 : 1];
+  __shared__ int s_pendi[QD ? 3 : 1];
+  const int it_first = A.es_it0 + vb;
   for (int it = A.es_it0 + vb; it < itEnd; it += gridDim.x) {
     if (A.phase) ph_t = wall_clock64();
-    const int item = items[it];
+    const int item = QD ? q_item : items[it];
     const int site = item >> 3, cfg = item & 7;
-    const int r = A.ref[site];
+    int r;
+    if constexpr (QD) {
+      __builtin_amdgcn_s_waitcnt(0x0F70 | 6);   // vmcnt(6): the ref dword has landed (slots 0, 1 and the next index may not)
+      __builtin_amdgcn_sched_barrier(0);
+      r = __builtin_amdgcn_readfirstlane(((const volatile __attribute__((address_space(3))) uint8_t*)s_qaux)[site & 3]);
+    } else r = A.ref[site];
     ItemCtx I;
     item_alleles(A, site, cfg, r, &I.a1, &I.a2);
     I.g11 = d_gi(I.a1, I.a1); I.g12 = d_gi(I.a1, I.a2); I.g22 = d_gi(I.a2, I.a2);
@@ -1505,39 +1681,59 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
     constexpr int NC = POLY ? 5 : 9;
     double cond[S][NC];
     int fl[S];
-    unsigned live = 0;
     bool hoisted = false;
     if constexpr (POLY) {
       if constexpr (PFK) {
         if (pf) {
           __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this item's planes have landed in LDS
-          hoist_poly4_lds<S, T>(A, s_u, s_pf, s_lk, cond, live);
+          hoist_poly4_lds<S, T>(A, s_u, s_pf, s_lk, cond);
           __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): every read of the buffer is done ...
           __builtin_amdgcn_sched_barrier(0);
           prefetch_planes(A, items, it + gridDim.x, nItems, s_pf);   // ... before the next item's planes overwrite it
           hoisted = true;
         }
       }
-      if (!PFK && !hoisted && A.max_nuc <= 4) {
-        if constexpr (DN) {   // de novo and cfg-7 items
-          if constexpr (DNPF_ONLY) hoist_poly4_dn_pf<S, T>(A, s_u, I, pl, s_lk, s_M, cond, live, s_pf + (threadIdx.x >> 6) * 2 * DN_PF_BUF);
-          else if constexpr (S % DN_PF_C == 0) {
-            if (A.dn_pf) hoist_poly4_dn_pf<S, T>(A, s_u, I, pl, s_lk, s_M, cond, live, s_pf + (threadIdx.x >> 6) * 2 * DN_PF_BUF);
-            else hoist_poly4_dn<S, T>(A, s_u, I, pl, s_lk, s_M, cond, live);
-          } else hoist_poly4_dn<S, T>(A, s_u, I, pl, s_lk, s_M, cond, live);
+      if constexpr (QD) {
+        hoist_quad<S>(A, I, pl, s_lk, s_M, cond, qring, qvoff);
+        hoisted = true;
+        const int itn = it + gridDim.x;   // the next item's first slots land during this item's Brent
+        // (landed: the hoisting ended with vmcnt(0)); uniform, so the next site's addresses are scalar
+        const int nitem = __builtin_amdgcn_readfirstlane(((const volatile __attribute__((address_space(3))) int*)s_qaux)[64]);
+        if (threadIdx.x == 0 && it != it_first) {
+          const int ps = s_pendi[0], pc = s_pendi[1];
+          A.raw[(size_t)ps * 8 + pc] = s_pend[0];
+          A.minv[ps * 8 + pc] = s_pend[1];
+          A.evals[ps * 8 + pc] = s_pendi[2];
         }
-        else hoist_poly4<S, T>(A, s_u, I, pl, s_lk, cond, live);
+        if (itn < itEnd) {
+          __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): s_qaux has been read before the DMA refills it
+          __builtin_amdgcn_sched_barrier(0);
+          quad_aux(A.ref + ((nitem >> 3) & ~3), s_qaux);
+          quad_prefetch(A, nitem, qvoff, qring);
+          if (itn + (int)gridDim.x < itEnd) quad_aux(items + itn + gridDim.x, s_qaux + 64);
+          q_item = nitem;
+        }
+      }
+      if (!PFK && !QD && !hoisted && A.max_nuc <= 4) {
+        if constexpr (DN) {   // de novo and cfg-7 items
+          if constexpr (DNPF_ONLY) hoist_poly4_dn_pf<S, T>(A, s_u, I, pl, s_lk, s_M, cond, s_pf + (threadIdx.x >> 6) * 2 * DN_PF_BUF);
+          else if constexpr (S % DN_PF_C == 0) {
+            if (A.dn_pf) hoist_poly4_dn_pf<S, T>(A, s_u, I, pl, s_lk, s_M, cond, s_pf + (threadIdx.x >> 6) * 2 * DN_PF_BUF);
+            else hoist_poly4_dn<S, T>(A, s_u, I, pl, s_lk, s_M, cond);
+          } else hoist_poly4_dn<S, T>(A, s_u, I, pl, s_lk, s_M, cond);
+        }
+        else hoist_poly4<S, T>(A, s_u, I, pl, s_lk, cond);
         hoisted = true;
       }
     }
 #pragma unroll
     for (int s = 0; s < S; s++) {
       fl[s] = 0;
-      if (PFK || DNPF_ONLY || hoisted) continue;
+      if (PFK || DNPF_ONLY || QD || hoisted) continue;
       if constexpr (POLY) {
         const int4 u = A.units[s * T + threadIdx.x];   // L1/L2-resident; not kept in registers
         double c9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-        if (u.x == U_NUC) { hoist_nuc<false, DN>(A, I, pl, s_lk, s_M, u.z, u.w, c9); live |= 1u << s; }
+        if (u.x == U_NUC) hoist_nuc<false, DN>(A, I, pl, s_lk, s_M, u.z, u.w, c9);
         fold_poly(c9, cond[s]);
         if (u.x != U_NUC) phantom_poly(cond[s]);   // empty slot (lane_poly_r)
       } else if (unit[s].x == U_NUC) hoist_nuc<GEN>(A, I, pl, s_lk, s_M, unit[s].z, unit[s].w, cond[s]);
@@ -1593,8 +1789,8 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
           lane_poly_r<S>(x / g, (g * g) * (g * g), (const double(*)[5])cond, m, e);
           tot = block_logprod<T>(m, e, s_red, s_rede, par);
         } else {
-          lane_poly_dir<S, false>(g / x, full, live, (const double(*)[5])cond, m, e);
-          tot = block_logprod<T>(m, e, s_red, s_rede, par) + (4.0 * A.n_fam) * log10(x);
+          lane_poly_top<S>((const double(*)[5])cond, m, e);   // x = 1: L = a0 per family, log10(x^4) = 0
+          tot = block_logprod<T>(m, e, s_red, s_rede, par);
         }
       } else if (PROD) {
         double m; int e;
@@ -1687,13 +1883,22 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
       x = fabs(d) >= tol1 ? mn + d : mn + d_sign(tol1, d);
     }
     if (threadIdx.x == 0) {
-      raw[cfg] = -fmin;
-      A.minv[site * 8 + cfg] = mn;
-      A.evals[site * 8 + cfg] = nev;
+      if constexpr (QD) { s_pend[0] = -fmin; s_pend[1] = mn; s_pendi[0] = site; s_pendi[1] = cfg; s_pendi[2] = nev; }
+      else {
+        raw[cfg] = -fmin;
+        A.minv[site * 8 + cfg] = mn;
+        A.evals[site * 8 + cfg] = nev;
+      }
       if (!single) ev_acc += nev - skipped;   // objective evaluations computed
       if (!ok) atomicExch(&A.counts[5], 1);
     }
     if (A.phase) { ph_e += wall_clock64() - ph_t; ph_n++; }
+  }
+  if (QD && threadIdx.x == 0 && it_first < itEnd) {
+    const int ps = s_pendi[0], pc = s_pendi[1];
+    A.raw[(size_t)ps * 8 + pc] = s_pend[0];
+    A.minv[ps * 8 + pc] = s_pend[1];
+    A.evals[ps * 8 + pc] = s_pendi[2];
   }
   if (threadIdx.x == 0 && ev_acc) atomicAdd(A.eval_total, ev_acc);
   if (A.phase && threadIdx.x == 0) { atomicAdd(&A.phase[0], ph_h); atomicAdd(&A.phase[1], ph_e); atomicAdd(&A.phase[2], ph_n); }
@@ -2736,6 +2941,8 @@ struct pm_engine {
   int T = 64, S = 1;
   int grid_brent = 1024;
   bool has_fp = false;
+  bool quad = false;       // QUAD lane plan (hoist_quad): every unit a 4-person nuclear family at a multiple-of-4 person
+  int quad_full = 0;       // slot rows below this have no empty lane
   int last_n = 0;
   int n_cu = 256;
   bool carry_postprob = false;
@@ -3070,6 +3277,18 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
       if (pref[i].x >= tmin && plan_units(ped, pref[i].x, pref[i].y, units)) { E->T = pref[i].x; E->S = pref[i].y; planned = true; }
   }
   if (!planned) { pm_engine_destroy(E); pm_set_last_error("pm_engine_create: pedigree too large for the lane plan"); return PM_EPED; }
+  {   // QUAD plan: each nuclear family's four PL bytes of a genotype plane form one aligned dword
+    bool q = E->n_person % 16 == 0 && !E->has_fp && E->T == 64;
+    int full = E->S;
+    for (int sl = 0; sl < E->S && q; sl++)
+      for (int l = 0; l < E->T; l++) {
+        const int4 u = units[(size_t)sl * E->T + l];
+        if (u.x == U_NONE) { full = std::min(full, sl); continue; }
+        if (u.x != U_NUC || u.w != 4 || u.z != 4 * (sl * E->T + l)) { q = false; break; }
+      }
+    E->quad = q && !getenv("PM_NO_QUAD");
+    E->quad_full = full;
+  }
   hipDeviceProp_t prop;
   HIP_TRY(hipGetDeviceProperties(&prop, device));
   const int blocksPerCU = std::max(1, 1024 / E->T);   // ~16 waves per CU
@@ -3547,15 +3766,22 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
     A.pf_npad = (E->n_person + 1023) / 1024 * 1024;
     shmem = (size_t)3 * A.pf_npad;
   }
-  // lean --denovo kernel: LDS-DMA staging of the PL windows (double buffer per wave)
+  // lean --denovo kernel: QUAD plans load each family's PL dwords directly (hoist_quad); other plans stage the PL
+  // windows through LDS by LDS-DMA (double buffer per wave)
   A.dn_pf = 0;
-  if (!gen && !unrelated && n_ext == 0 && A.denovo && E->par.numerics == PM_NUM_POLY && E->max_nuc <= 4 && S % DN_PF_C == 0 &&
+  A.quad_full = E->quad_full;
+  const bool quad = !gen && !unrelated && n_ext == 0 && A.denovo && E->par.numerics == PM_NUM_POLY && E->quad && T == 64 &&
+                    (S == 8 || S == 16);
+  if (quad) shmem = QWAVE;
+  if (!quad && !gen && !unrelated && n_ext == 0 && A.denovo && E->par.numerics == PM_NUM_POLY && E->max_nuc <= 4 && S % DN_PF_C == 0 &&
       E->n_person % 16 == 0 && E->n_person >= 16 && !getenv("PM_NO_PREFETCH")) {
     A.dn_pf = 1;
     shmem = (size_t)(T / 64) * 2 * DN_PF_BUF;
   }
   const bool ep = !unrelated && n_ext > 0 && E->es_poly && E->par.numerics == PM_NUM_POLY;
-  BrentFn fn = brent_kernel(T, S, E->par.numerics, gen, !unrelated && n_ext > 0, A.denovo != 0, A.pf_npad > 0 || A.dn_pf, ep);
+  BrentFn fn = quad ? (S == 16 ? k_brent<64, 16, PM_NUM_POLY, false, false, true, false, false, true>
+                              : k_brent<64, 8, PM_NUM_POLY, false, false, true, false, false, true>)
+                   : brent_kernel(T, S, E->par.numerics, gen, !unrelated && n_ext > 0, A.denovo != 0, A.pf_npad > 0 || A.dn_pf, ep);
   if (!fn) { pm_set_last_error("launch_brent: no kernel variant for the lane plan"); return PM_EINVAL; }
   // multi-wave de novo plans (T = 512 / 1024: more than 1024 families) stage 2 buffers per wave: above the
   // default 64 KB dynamic-LDS limit the kernel must opt in, and the block (plus its static LDS: lane plan,

@@ -157,6 +157,30 @@ def test_plane_prefetch_bit_identical(built, tmp_path, monkeypatch, shape, nfam,
     assert compare_results(b, o, bc, oc, label="direct ")["called"] > 0
 
 
+@pytest.mark.parametrize("nfam,nsites", [(300, 200), (512, 128), (600, 128), (1024, 64)])
+def test_quad_plan_matches_oracle(built, tmp_path, monkeypatch, nfam, nsites):
+    """QUAD lane plans (every family a 4-person nuclear family in person order, n_person % 16 == 0: the lean de
+    novo kernel reads each family's PL bytes as one dword per genotype plane, LDS-DMA ring, prefetch across items,
+    factored quartic) against the oracle, and the same sites through the general de novo hoisting (PM_NO_QUAD=1)
+    against the oracle too.  300 / 600 families end in a partial slot row (phantom families), 512 / 1024 fill the
+    64 x 8 / 64 x 16 plans exactly; planted de novo kids give cfg-7 items as well."""
+    d = str(tmp_path / "qd")
+    pm.synth_write_dataset(d, "quad+dn", nfam, nsites, 17)
+    ped = pm.Pedigree(os.path.join(d, "test.dat"), os.path.join(d, "test.ped"))
+    label, pos, ref, pl, dm = _read_all(ped, d)[0]
+    params = pm.Params.defaults(numerics=pm.NUM_POLY, denovo=1, denovo_mut_rate=1e-5)
+    o, oc = Oracle(ped.view, params).run(pl, dm, ref)
+    for noquad in ("", "1"):
+        if noquad:
+            monkeypatch.setenv("PM_NO_QUAD", noquad)
+        eng = pm.Engine(ped.view, params, max_batch=len(ref))
+        assert eng.plan() == (64, 8 if nfam <= 512 else 16)
+        e, ec = eng.run(pl, dm, ref)
+        eng.close()
+        st = compare_results(e, o, ec, oc, label=("general " if noquad else "quad "))
+        assert st["called"] > 0
+
+
 @pytest.mark.parametrize("numerics", [pm.NUM_PRODUCT, pm.NUM_POLY])
 @pytest.mark.parametrize("shape", ["quad+dn", "trio+dn"])
 def test_denovo_planted_parity(built, tmp_path, numerics, shape):
