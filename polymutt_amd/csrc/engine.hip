@@ -124,6 +124,7 @@ struct DevArgs {
   // tables
   const double* lktab;     // [256]
   const double* M;         // [100] genotype mutation matrix
+  double Mk[100];          // the same, by value in the kernel arguments: uniform reads become scalar loads (QUAD hoisting)
   const pm_synth_tables* syn;
   // parameters
   double precision, posterior, theta;
@@ -1147,15 +1148,18 @@ __device__ __forceinline__ void hoist_quad_t(const DevArgs& A, const ItemCtx& I,
       double pg[2][10];   // both kids' 20 table lookups in flight together
 #pragma unroll
       for (int g = 0; g < 10; g++) { pg[0][g] = lk[(wg[g] >> 16) & 0xFF]; pg[1][g] = lk[wg[g] >> 24]; }
+      // the item's three mutation-matrix rows from the kernel arguments (scalar loads issued beside the lookups):
+      // scalar FMA operands, no LDS read per slot
+      double mr[3][10];
+#pragma unroll
+      for (int g = 0; g < 10; g++) { mr[0][g] = A.Mk[I.g11 * 10 + g]; mr[1][g] = A.Mk[I.g12 * 10 + g]; mr[2][g] = A.Mk[I.g22 * 10 + g]; }
       __builtin_amdgcn_sched_barrier(0);
       if (s + QD_AHEAD < S) quad_dma(pl, s + QD_AHEAD, npo, voff, ring + ((s + QD_AHEAD) % QB) * QSLOT);
-      lds_cdp M11 = (lds_cdp)(M + I.g11 * 10), M12 = (lds_cdp)(M + I.g12 * 10), M22 = (lds_cdp)(M + I.g22 * 10);
-      asm volatile("" : "+v"(M11), "+v"(M12), "+v"(M22));
 #pragma unroll
       for (int q = 0; q < 2; q++) D[q][0] = D[q][1] = D[q][2] = 0.0;
 #pragma unroll
       for (int g = 0; g < 10; g++) {   // CalcDenovoMutLk (:1553-1562), each matrix entry read once for both kids
-        const double m11 = M11[g], m12 = M12[g], m22 = M22[g];
+        const double m11 = mr[0][g], m12 = mr[1][g], m22 = mr[2][g];
 #pragma unroll
         for (int q = 0; q < 2; q++) {
           D[q][0] = fma(m11, pg[q][g], D[q][0]);
@@ -3642,6 +3646,7 @@ static DevArgs make_args(pm_engine* E, int n, const uint8_t* pl, const uint32_t*
     A.ext_count = E->n_ext1 ? E->d_ext_count1 : nullptr; A.ext_fam = E->d_ext_fam1; A.nuc_es = 1;
   }
   A.lktab = E->d_lktab; A.M = E->d_M; A.syn = E->d_syn;
+  memcpy(A.Mk, E->M_h, sizeof(A.Mk));
   A.precision = E->par.precision; A.posterior = E->par.posterior; A.theta = E->par.theta;
   A.min_total_depth = E->par.min_total_depth; A.max_total_depth = E->par.max_total_depth; A.min_map_quality = E->par.min_map_quality;
   A.min_ps = E->par.min_ps; A.denovo_min_llr = E->par.denovo_min_llr; A.log10_denovo_min_llr = log10(E->par.denovo_min_llr);
