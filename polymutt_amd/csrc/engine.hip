@@ -119,6 +119,7 @@ struct DevArgs {
   int mono_dn;             // k_prep computes the de novo monomorphism item (cfg 0) itself (lean --denovo)
   int* row_blk;            // k_rows_count / k_rows: written records per 1024-site block
   int pf_npad;             // lean kernel: > 0 = the item's 3 genotype planes are prefetched into LDS (stride)
+  int pf_dw;               // ... in 4-byte pieces (n_person % 16 != 0, n_person % 4 == 0)
   int dn_pf;               // lean --denovo kernel: PL windows staged through LDS by LDS-DMA (hoist_poly4_dn_pf)
   int quad_full;           // QUAD plan (hoist_quad): slot rows below this have no empty lane
   // tables
@@ -755,8 +756,9 @@ __device__ __forceinline__ void item_alleles(const DevArgs& A, int site, int cfg
 // Lean-kernel plane prefetch: the three genotype planes (g11, g12, g22) of an item's site block are
 // copied into this wave's LDS buffer with LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave-instruction,
 // no VGPRs), issued right after the previous item's hoisting so the copy runs under that item's Brent
-// evaluations.  Needs n_person % 16 == 0 (16-B aligned planes); lanes past a plane's end re-read its
-// last 16 bytes (never used), so no access leaves the site block.
+// evaluations.  16-B pieces need n_person % 16 == 0 (16-B aligned planes); with n_person % 4 == 0 (pf_dw) the
+// copy goes in 4-B pieces (256 B per wave-instruction).  Lanes past a plane's end re-read its last piece (never
+// used), so no access leaves the site block.  The waves of a multi-wave block split the pieces.
 __device__ __forceinline__ void prefetch_planes(const DevArgs& A, const int* items, int it, int nItems, uint8_t* buf) {
   if (it >= nItems) return;
   const int item = items[it];
@@ -767,10 +769,22 @@ __device__ __forceinline__ void prefetch_planes(const DevArgs& A, const int* ite
   const int gs[3] = {d_gi(a1, a1), d_gi(a1, a2), d_gi(a2, a2)};
   const uint8_t* base = A.pl + (size_t)site * np * 10;
   const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), W = blockDim.x >> 6;
+  if (A.pf_dw) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const uint8_t* plane = base + (size_t)gs[k] * np;
+      for (int c = wv * 256; c < np; c += W * 256) {
+        const int off = min(c + lane * 4, np - 4);
+        __builtin_amdgcn_global_load_lds((const void*)(plane + off), (void*)(buf + k * npad + c), 4, 0, 0);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     const uint8_t* plane = base + (size_t)gs[k] * np;
-    for (int c = 0; c < npad; c += 1024) {
+    for (int c = wv * 1024; c < npad; c += W * 1024) {
       const int off = min(c + lane * 16, np - 16);
       __builtin_amdgcn_global_load_lds((const void*)(plane + off), (void*)(buf + k * npad + c), 16, 0, 0);
     }
@@ -1303,17 +1317,36 @@ __device__ __forceinline__ double sgpr_const(double c) {
   asm volatile("" : "+s"(c));
   return c;
 }
+// n / d for a finite n and a positive d in the normal range, from the hardware reciprocal: two Newton steps and one
+// residual correction (within an ulp of the IEEE quotient; 8 dependent operations instead of the 11 of the IEEE
+// division sequence, which matters on the serial per-evaluation path of Brent)
+__device__ __forceinline__ double pos_div(double n, double d) {
+  double y = __builtin_amdgcn_rcp(d);
+  double e = fma(-d, y, 1.0);
+  y = fma(y, e, y);
+  e = fma(-d, y, 1.0);
+  y = fma(y, e, y);
+  const double q = n * y;
+  return fma(fma(-d, q, n), y, q);
+}
+
 __device__ __forceinline__ double log10_mant(double m, int e) {
   if (m == 0.0) return -INFINITY;   // an underflowed family product: log10(0), as the reference
   if (m < 0.70710678118654752440) { m *= 2.0; e -= 1; }
-  const double t = (m - 1.0) / (m + 1.0);
+  const double u = m - 1.0;                  // exact (Sterbenz)
+  const double t = pos_div(u, m + 1.0);       // |t| <= 0.172
   const double t2 = t * t;
-  // series coefficients as SGPR operands materialised at their use (otherwise the compiler keeps ten of
+  // P(t2) = sum_k 2 / (2k + 3) t2^k, k = 0..9, by Estrin (all terms >= 0: no cancellation), depth 4 instead of 9;
+  // the series coefficients as SGPR operands materialised at their use (otherwise the compiler keeps ten of
   // them in VGPRs across the Brent loop, next to the 5 x S hoisted coefficients)
-  double p = sgpr_const(2.0 / 21);
-  p = fma(p, t2, sgpr_const(2.0 / 19)); p = fma(p, t2, sgpr_const(2.0 / 17)); p = fma(p, t2, sgpr_const(2.0 / 15));
-  p = fma(p, t2, sgpr_const(2.0 / 13)); p = fma(p, t2, sgpr_const(2.0 / 11)); p = fma(p, t2, sgpr_const(2.0 / 9));
-  p = fma(p, t2, sgpr_const(2.0 / 7)); p = fma(p, t2, sgpr_const(2.0 / 5)); p = fma(p, t2, sgpr_const(2.0 / 3));
+  const double t4 = t2 * t2, t8 = t4 * t4, t16 = t8 * t8;
+  const double q0 = fma(sgpr_const(2.0 / 5), t2, sgpr_const(2.0 / 3));
+  const double q1 = fma(sgpr_const(2.0 / 9), t2, sgpr_const(2.0 / 7));
+  const double q2 = fma(sgpr_const(2.0 / 13), t2, sgpr_const(2.0 / 11));
+  const double q3 = fma(sgpr_const(2.0 / 17), t2, sgpr_const(2.0 / 15));
+  const double q4 = fma(sgpr_const(2.0 / 21), t2, sgpr_const(2.0 / 19));
+  const double r0 = fma(q1, t4, q0), r1 = fma(q3, t4, q2);
+  const double p = fma(q4, t16, fma(r1, t8, r0));
   const double ln = fma(t * t2, p, 2.0 * t);
   const double de = (double)e;
   return ln * PM_INV_LN10 + (de * PM_LOG10_2_HI + de * PM_LOG10_2_LO);
@@ -1621,8 +1654,8 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
   // XCD-aware item order: blocks are dealt round-robin to the 8 XCDs (separate L2s), so consecutive
   // items -- the 2-4 configurations of one site, which read the same PL block -- go to blocks of one XCD.
   const int vb = (gridDim.x % 8 == 0) ? (blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8 : blockIdx.x;
-  // lean kernel, one wave per item: the item's genotype planes arrive in LDS by prefetch (pf_npad > 0)
-  constexpr bool PFK = PF && NUM == PM_NUM_POLY && !GEN && !ES && !DN && T == 64;
+  // lean kernel, one or two waves per item: the item's genotype planes arrive in LDS by prefetch (pf_npad > 0)
+  constexpr bool PFK = PF && NUM == PM_NUM_POLY && !GEN && !ES && !DN && (T == 64 || T == 128);
   // PF on the lean de novo kernel: the 64 x 16 instantiation with only the LDS-staged hoisting compiled (the
   // direct-load hoisting of 16 de novo slots spills; this one keeps 1024 families on one wave per item)
   constexpr bool DNPF_ONLY = PF && POLYK && DN && T == 64 && S == 16 && !QD;
@@ -1689,9 +1722,11 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
     if constexpr (POLY) {
       if constexpr (PFK) {
         if (pf) {
-          __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this item's planes have landed in LDS
+          __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's pieces of the item's planes have landed
+          if constexpr (T > 64) __syncthreads();   // ... and the other waves' pieces
           hoist_poly4_lds<S, T>(A, s_u, s_pf, s_lk, cond);
           __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): every read of the buffer is done ...
+          if constexpr (T > 64) __syncthreads();   // ... by every wave of the block ...
           __builtin_amdgcn_sched_barrier(0);
           prefetch_planes(A, items, it + gridDim.x, nItems, s_pf);   // ... before the next item's planes overwrite it
           hoisted = true;
@@ -1790,7 +1825,7 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
         double m; int e;
         if (__builtin_amdgcn_readfirstlane((int)(g > 0.0))) {
           // (r from the hardware reciprocal + a Newton step instead of the division: measured no faster)
-          lane_poly_r<S>(x / g, (g * g) * (g * g), (const double(*)[5])cond, m, e);
+          lane_poly_r<S>(pos_div(x, g), (g * g) * (g * g), (const double(*)[5])cond, m, e);
           tot = block_logprod<T>(m, e, s_red, s_rede, par);
         } else {
           lane_poly_top<S>((const double(*)[5])cond, m, e);   // x = 1: L = a0 per family, log10(x^4) = 0
@@ -1971,7 +2006,11 @@ __global__ void __launch_bounds__(256) k_prep(DevArgs A) {
       uint32_t x[VEC];
       uint8_t hr[VEC];
       if (p0 < np) {   // np % VEC == 0: a lane's VEC persons are all present or all absent
-        load_dwords<VEC>(dm + p0, x);
+        if (!A.vcf) load_dwords<VEC>(dm + p0, x);
+        else {   // the VCF path has no read depth or mapping quality (PedVCF / FamilyLikelihoodSeq_VCF): dm is not read
+#pragma unroll
+          for (int k = 0; k < VEC; k++) x[k] = 0;
+        }
         load_bytes<VEC>(plane_h + p0, hr);
       } else {
 #pragma unroll
@@ -2399,9 +2438,12 @@ __device__ __forceinline__ void lean_fam_bytes(const uint8_t* pl, int np, int p0
 // LEAN nuclear family (autosome, <= 4 persons, not de novo) from its 12 PL bytes (lean_fam_bytes, loaded ahead by
 // the caller): the arithmetic of hoist_nuc, CalcParentMarginal and KidJointGenoLikelihood below in the same
 // operation order -- the same values bit for bit
-template <bool VCF>
+// NF = the family's persons when the caller knows them for the whole wave (3: trio, 4: quad; 0 = runtime n): the
+// kid loops and the one-kid / two-kid selects then resolve at compile time (same operations, same bits)
+template <bool VCF, int NF = 0>
 __device__ __forceinline__ void lean_nuc_post(const DevArgs& A, const double* s_lk, const double* s_gq, const uint32_t* by,
-                                              size_t out, int p0, int n, const double* pp) {
+                                              size_t out, int p0, int n_rt, const double* pp) {
+  const int n = NF ? NF : n_rt;
   double lF[3], lM[3], kl[2][3];
 #pragma unroll
   for (int t = 0; t < 3; t++) {
@@ -2742,7 +2784,12 @@ __global__ void __launch_bounds__(256) k_posterior_lean(DevArgs A) {
       if (d >> 31) {
         uint32_t by[12];
         lean_fam_bytes(cur.pl, np, p0, n, cur.g11, cur.g12, cur.g22, by);
-        lean_nuc_post<VCF>(A, s_lk, s_gq, by, cur.out, p0, n, pp);
+        // fam_perm groups families by size, so a wave's families almost always share one: specialised bodies
+        const int n0 = __builtin_amdgcn_readfirstlane(n);
+        const bool uni = __builtin_amdgcn_ballot_w64(n != n0) == 0;
+        if (uni && n0 == 4) lean_nuc_post<VCF, 4>(A, s_lk, s_gq, by, cur.out, p0, n, pp);
+        else if (uni && n0 == 3) lean_nuc_post<VCF, 3>(A, s_lk, s_gq, by, cur.out, p0, n, pp);
+        else lean_nuc_post<VCF>(A, s_lk, s_gq, by, cur.out, p0, n, pp);
       } else {
         for (int j = 0; j < n; j++) {
           const int p = p0 + j;
@@ -3685,6 +3732,7 @@ static BrentFn brent_kernel(int T, int S, int num, bool gen, bool es, bool dn = 
 #define PMKP(s) if (T == 64 && S == s) return k_brent<64, s, PM_NUM_POLY, false, false, false, true>;
     PMKP(1) PMKP(2) PMKP(4) PMKP(8) PMKP(16)
 #undef PMKP
+    if (T == 128 && S == 16) return k_brent<128, 16, PM_NUM_POLY, false, false, false, true>;   // 1025-2048 families
     return nullptr;
   }
   if (dn && !gen && !es && n == PM_NUM_POLY) {   // lean autosomal --denovo
@@ -3765,10 +3813,15 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
   // lean non-de-novo kernel at one wave per item: LDS-DMA plane prefetch when the planes are 16-B aligned
   size_t shmem = 0;
   A.pf_npad = 0;
-  if (!gen && !unrelated && n_ext == 0 && !A.denovo && T == 64 && E->par.numerics == PM_NUM_POLY && E->max_nuc <= 4 &&
-      E->n_person % 16 == 0 && E->n_person >= 16 && (E->n_person + 1023) / 1024 * 1024 * 3 <= 60 * 1024 &&
+  A.pf_dw = 0;
+  // (16-B pieces need 16-B aligned planes: n_person % 16 == 0 and a 16-B aligned block; 4-B pieces otherwise; the
+  // 128 x 16 plan of 1025-2048 families shares one buffer between its two waves)
+  const bool al16 = E->n_person % 16 == 0 && ((uintptr_t)A.pl & 15) == 0, al4 = E->n_person % 4 == 0 && ((uintptr_t)A.pl & 3) == 0;
+  if (!gen && !unrelated && n_ext == 0 && !A.denovo && (T == 64 || (T == 128 && S == 16)) && E->par.numerics == PM_NUM_POLY &&
+      E->max_nuc <= 4 && (al16 || al4) && E->n_person >= 16 && (E->n_person + 1023) / 1024 * 1024 * 3 <= 60 * 1024 &&
       !getenv("PM_NO_PREFETCH")) {
     A.pf_npad = (E->n_person + 1023) / 1024 * 1024;
+    A.pf_dw = al16 ? 0 : 1;
     shmem = (size_t)3 * A.pf_npad;
   }
   // lean --denovo kernel: QUAD plans load each family's PL dwords directly (hoist_quad); other plans stage the PL

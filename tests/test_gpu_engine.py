@@ -130,11 +130,15 @@ def test_synthetic_device_generator_and_parity(built, shape, nfam, nsites, tmp_p
 
 @pytest.mark.parametrize("shape,nfam,denovo,nsites", [("quad", 64, 0, 500), ("quad+dn", 64, 1, 500), ("trio+dn", 64, 1, 500),
                                                      ("quad+dn", 300, 1, 300), ("quad+dn", 600, 1, 150), ("trio+dn", 528, 1, 150),
-                                                     ("quad+dn", 1200, 1, 96), ("quad+dn", 2100, 1, 64)])
+                                                     ("quad+dn", 1200, 1, 96), ("quad+dn", 2100, 1, 64),
+                                                     ("trio", 300, 0, 300), ("mixed", 1104, 0, 96), ("quad", 1200, 0, 96),
+                                                     ("mixed", 2000, 0, 48)])
 def test_plane_prefetch_bit_identical(built, tmp_path, monkeypatch, shape, nfam, denovo, nsites):
-    """The lean kernels' LDS staging of the PL bytes (plain: the item's 3 planes; --denovo: per-wave windows of
-    all 10 planes, double-buffered by LDS-DMA), taken when n_person % 16 == 0, gives bit-identical results to
-    the direct-load hoisting (PM_NO_PREFETCH=1) on the same lane plan, and both match the oracle."""
+    """The lean kernels' LDS staging of the PL bytes (plain: the item's 3 planes, 16-B pieces when n_person % 16 == 0
+    and 4-B pieces when only n_person % 4 == 0 -- trio 300: 900 persons, mixed 1104: 3864 -- on one-wave plans and
+    on the two-wave 128 x 16 plan of 1025-2048 families; --denovo: per-wave windows of all 10 planes,
+    double-buffered by LDS-DMA) gives bit-identical results to the direct-load hoisting (PM_NO_PREFETCH=1) on the
+    same lane plan, and both match the oracle."""
     d = str(tmp_path / "pf")
     pm.synth_write_dataset(d, shape, nfam, nsites, 13)   # n_person % 16 == 0
     ped = pm.Pedigree(os.path.join(d, "test.dat"), os.path.join(d, "test.ped"))
