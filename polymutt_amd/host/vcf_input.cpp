@@ -118,6 +118,8 @@ struct Pending {          // one record awaiting output, in file order
   int slot = -1;
   int a1 = 0, a2 = 0;
   bool indel = false;
+  int dp_idx = -1;        // DP's FORMAT index as it stood when the record was read: the reference writes each record at
+                          // once (PedVCF.cpp:118-160), with DP looked up per record until found (:311-314)
 };
 
 struct State {            // what FamilyLikelihoodSeq_VCF holds between records (stale output, :412-521)
@@ -278,8 +280,8 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
       if (col_person[i] < 0) continue;
       AC += st.calls[col_person[i]].best;
       int dp = 0;
-      if (fs.DP_index > 0) {
-        missing = get_field(L, r.cols[9 + i], fs.DP_index, f);
+      if (r.dp_idx > 0) {
+        missing = get_field(L, r.cols[9 + i], r.dp_idx, f);
         dp = missing ? 0 : atoi(L.c_str() + f.b);
       }
       if (missing) continue;
@@ -296,8 +298,8 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
       const std::string lab = label_text(c);
       fprintf(fo, "\t%s:%d:", (c.gq > 0 || lab == ".") ? lab.c_str() : "./.", (int)c.gq);
       std::string dps = ".";
-      if (fs.DP_index > 0) {
-        missing = get_field(L, r.cols[9 + i], fs.DP_index, f);
+      if (r.dp_idx > 0) {
+        missing = get_field(L, r.cols[9 + i], r.dp_idx, f);
         if (!missing) dps = L.substr(f.b, f.e - f.b);
       }
       fprintf(fo, "%s:", missing ? "." : dps.c_str());
@@ -332,6 +334,7 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
       r.a1 = r.indel ? 1 : allele2int(refS);
       r.a2 = r.indel ? 2 : allele2int(altS);
       if (fs.DP_index < 0) fs.DP_index = format_index(L, r.cols[8], "DP");
+      r.dp_idx = fs.DP_index;
       if (fs.GL_idx < 0 && fs.PL_idx < 0) {
         fs.GL_idx = format_index(L, r.cols[8], "GL");
         fs.PL_idx = format_index(L, r.cols[8], "PL");
@@ -423,7 +426,7 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
     const int cls = chrom == opt.chrX ? PM_CHR_X : chrom == opt.chrY ? PM_CHR_Y : chrom == opt.MT ? PM_CHR_MT : PM_CHR_AUTO;
     if (withdata == 0) {   // written with the previous record's QUAL / AF / genotypes (:113)
       if (lead && !computed_any) {   // ... which an earlier rank computed: written after the exchange
-        fprintf(lead, "%s\n", r.line.c_str());
+        fprintf(lead, "%d\t%s\n", r.dp_idx, r.line.c_str());   // (with its DP index snapshot)
         n_lead++;
       } else pend.push_back(std::move(r));
       continue;
@@ -480,7 +483,9 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
     if (!lr.open(lead_in)) throw FatalError("VCF shard: " + lead_in + " is missing\n");
     for (int64_t k = 0; k < n_lead && lr.next(line); k++) {
       Pending r;
-      r.line.swap(line);
+      const size_t tab = line.find('\t');
+      r.dp_idx = atoi(line.c_str());
+      r.line.assign(line, tab + 1, std::string::npos);
       split(r.line, '\t', r.cols);
       write_record(lo_out, r, false, nullptr, nullptr);
     }
