@@ -202,7 +202,8 @@ int pm_engine_begin_section(pm_engine *eng, int32_t chrom);
 
 /* Evaluate n sites.  Inputs are the dense per-site block, persons in pm_pedigree order:
  *   pl  [n][n_person][10]  phred genotype likelihoods AA,AC,AG,AT,CC,CG,CT,GG,GT,TT (0 when absent)
- *   dm  [n][n_person]      depth (bits 0-23) | mapQ << 24   (0 when absent; not read in vcf_mode: the VCF path has no depth)
+ *   dm  [n][n_person]      depth (bits 0-23) | mapQ << 24   (0 when absent; not read in vcf_mode -- the VCF path has no
+ *                          depth -- where it may be NULL)
  *   ref [n]                refBase 1..4 (anything else -> PM_SITE_BAD_REF)
  * inputs_on_device != 0: pl/dm/ref are device pointers on this engine's GPU, else host pointers.
  * Outputs are host pointers: res[n]; calls[n_rows * n_person] receives one row per written record

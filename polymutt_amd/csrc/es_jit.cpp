@@ -791,14 +791,16 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
   return src;
 }
 
-bool compile(const std::string& src, std::vector<char>* code, std::string* err) {
+bool compile(const std::string& src, std::vector<char>* code, std::string* err, const std::string& arch) {
   hiprtcProgram prog;
   if (hiprtcCreateProgram(&prog, src.c_str(), "es_hoist_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
     *err = "hiprtcCreateProgram failed";
     return false;
   }
   // -ffp-contract=off: only the explicit fma() of the generated code fuses
-  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17"};
+  // (the device's own target -- gcnArchName without feature suffixes -- so the module always loads on it)
+  const std::string off = "--offload-arch=" + arch;
+  const char* opts[] = {off.c_str(), "-O3", "-ffp-contract=off", "-std=c++17"};
   const hiprtcResult rc = hiprtcCompileProgram(prog, 4, opts);
   if (rc != HIPRTC_SUCCESS) {
     size_t ls = 0;
@@ -827,7 +829,13 @@ bool build(int device, int chrom, const std::vector<Family>& fams, const double 
   auto it = g_modules.find(key);
   if (it == g_modules.end()) {
     std::vector<char> code;
-    if (!compile(src, &code, err)) return false;
+    std::string arch = "gfx950";
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.gcnArchName[0]) {
+      arch = prop.gcnArchName;
+      arch = arch.substr(0, arch.find(':'));
+    }
+    if (!compile(src, &code, err, arch)) return false;
     hipModule_t mod;
     if (hipSetDevice(device) != hipSuccess || hipModuleLoadData(&mod, code.data()) != hipSuccess) {
       *err = "hipModuleLoadData of the peeling kernel failed";

@@ -77,7 +77,7 @@ int pack_steps(const pm_pedigree* ped, int f, int ns, std::vector<int2>& out);
 // per-thread es_hoist_jit and es_post_jit.
 std::string generate(int chrom, const std::vector<Family>& fams, const double (*tba)[27], Kernel* out, bool denovo = false);
 // hipRTC compile of a generated source for gfx950 (no device needed).
-bool compile(const std::string& src, std::vector<char>* code, std::string* err);
+bool compile(const std::string& src, std::vector<char>* code, std::string* err, const std::string& arch = "gfx950");
 
 // Generates and compiles the hoisting and posterior kernels of `fams` for chromosome class `chrom` (PM_CHR_*); bi-allelic
 // (3-state) peels.  tba = transmission_BA tables [5][27] (:812-924).  Returns false with a message in err.

@@ -354,7 +354,16 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
 
   int64_t lo = body, hi = INT64_MAX;
   if (sharded) {
-    const int64_t total = in.size();
+    // gzip input: one rank inflates the whole stream to learn its size and shares it (every rank doing so cost
+    // O(file) inflation each); each rank then re-inflates only up to its own slice in seek()
+    int64_t total;
+    if (gzdirect(in.fh)) total = in.size();
+    else {
+      int64_t mine = R == 0 ? in.size() : 0;
+      std::vector<int64_t> all(N);
+      comm->allgather(&mine, 1, all.data());
+      total = all[0];
+    }
     lo = body + (total - body) * R / N;
     if (R < N - 1) hi = body + (total - body) * (R + 1) / N;
     if (R > 0) {

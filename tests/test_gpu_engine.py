@@ -167,22 +167,31 @@ def test_quad_plan_matches_oracle(built, tmp_path, monkeypatch, nfam, nsites):
     novo kernel reads each family's PL bytes as one dword per genotype plane, LDS-DMA ring, prefetch across items,
     factored quartic) against the oracle, and the same sites through the general de novo hoisting (PM_NO_QUAD=1)
     against the oracle too.  300 / 600 families end in a partial slot row (phantom families), 512 / 1024 fill the
-    64 x 8 / 64 x 16 plans exactly; planted de novo kids give cfg-7 items as well."""
+    64 x 8 / 64 x 16 plans exactly; planted de novo kids give cfg-7 items as well.  On the QUAD plan the de novo
+    monomorphism likelihood (cfg 0) comes from the cfg-1 items' hoisted f^4 coefficients; PM_MONO_DN_PREP=1 forms
+    it in k_prep from all ten planes instead: both against the oracle, and within 1e-13 of each other."""
     d = str(tmp_path / "qd")
     pm.synth_write_dataset(d, "quad+dn", nfam, nsites, 17)
     ped = pm.Pedigree(os.path.join(d, "test.dat"), os.path.join(d, "test.ped"))
     label, pos, ref, pl, dm = _read_all(ped, d)[0]
     params = pm.Params.defaults(numerics=pm.NUM_POLY, denovo=1, denovo_mut_rate=1e-5)
     o, oc = Oracle(ped.view, params).run(pl, dm, ref)
-    for noquad in ("", "1"):
-        if noquad:
-            monkeypatch.setenv("PM_NO_QUAD", noquad)
+    got = {}
+    for env in ("", "PM_MONO_DN_PREP", "PM_NO_QUAD"):
+        if env:
+            monkeypatch.setenv(env, "1")
         eng = pm.Engine(ped.view, params, max_batch=len(ref))
         assert eng.plan() == (64, 8 if nfam <= 512 else 16)
         e, ec = eng.run(pl, dm, ref)
         eng.close()
-        st = compare_results(e, o, ec, oc, label=("general " if noquad else "quad "))
+        st = compare_results(e, o, ec, oc, label=(env or "quad") + " ")
         assert st["called"] > 0
+        got[env] = e
+        if env:
+            monkeypatch.delenv(env)
+    a, b = got[""], got["PM_MONO_DN_PREP"]
+    called = a["status"] == 0   # PM_SITE_CALLED
+    np.testing.assert_allclose(a["varllk"][called, 0], b["varllk"][called, 0], rtol=1e-13, atol=0)
 
 
 @pytest.mark.parametrize("numerics", [pm.NUM_PRODUCT, pm.NUM_POLY])
