@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 4
+#define PM_ABI_VERSION 5
 #define PM_NCFG 7           /* varllk slots: 0 mono, 1 ref/ts, 2 ref/tv1, 3 ref/tv2, 4 ts/tv1, 5 ts/tv2, 6 tv1/tv2 */
 
 typedef enum { PM_OK = 0, PM_EINVAL = -1, PM_EHIP = -2, PM_ENOMEM = -3, PM_EBRENT = -4, PM_EPED = -5 } pm_status;
@@ -212,6 +212,20 @@ int pm_engine_begin_section(pm_engine *eng, int32_t chrom);
  * Counters accumulate into the section totals.  Synchronous. */
 int pm_engine_run(pm_engine *eng, int32_t n, const uint8_t *pl, const uint32_t *dm, const uint8_t *ref,
                   int32_t inputs_on_device, pm_site_result *res, pm_geno_call *calls, int32_t *n_rows);
+
+/* pm_engine_run split in two, so a driver keeps several batches in flight (one per engine; each engine has its
+ * own HIP stream): pm_engine_submit queues the batch's host-to-device copies (asynchronous when pl/dm/ref are
+ * page-locked, pm_host_alloc), the pipeline and the copy-back of the per-site results on the engine's stream and
+ * returns; pm_engine_collect waits for that batch and writes res[n], the genotype rows and *n_rows exactly as
+ * pm_engine_run does.  One batch per engine between the two calls.  The input buffers must stay untouched until
+ * the collect.  (The reference's site loop body, main.cpp:327-589, per batch; no reference counterpart for the
+ * asynchrony itself.) */
+int pm_engine_submit(pm_engine *eng, int32_t n, const uint8_t *pl, const uint32_t *dm, const uint8_t *ref);
+int pm_engine_collect(pm_engine *eng, pm_site_result *res, pm_geno_call *calls, int32_t *n_rows);
+
+/* Page-locked host memory for pm_engine_submit's inputs and the result rows (H2D/D2H at full PCIe rate). */
+int pm_host_alloc(uint64_t bytes, void **h_ptr);
+int pm_host_free(void *h_ptr);
 
 /* Device-resident variant for benchmarking / multi-GPU sharding: all pointers are device pointers,
  * results stay on the device (d_res[n], d_calls[n * n_person] indexed by site), launched on the

@@ -11,6 +11,9 @@
 #include <stdlib.h>
 #include <string.h>
 #include <stdio.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #define MALE 1
 #define FEMALE 2
@@ -27,6 +30,14 @@ typedef struct {
   double min, fmin;            /* ScalarMinimizer::min/fmin, persists between sites */
   long evals;
 } lkobj;
+
+#define PMO_MAXT 64
+struct pmo_scratch {
+  double parentGLF[9], parentPrior[9], parentMarginal[9];
+  double *partials;            /* [max fam size][10] */
+  double mp[64][10][10];       /* marriage partials, keyed below */
+  int mpkey[64][2], nmp;
+};
 
 struct pmo_ctx {
   pm_pedigree ped;
@@ -50,11 +61,9 @@ struct pmo_ctx {
   const uint32_t *dm;
   int refBase;
   pm_counters cnt;
-  /* scratch */
-  double parentGLF[9], parentPrior[9], parentMarginal[9];
-  double *partials;            /* [max fam size][10] */
-  double mp[64][10][10];       /* marriage partials, keyed below */
-  int mpkey[64][2], nmp;
+  /* scratch of the objective, one per OpenMP thread (pmo_site runs the reference's `omp parallel sections` over the
+   * allele configurations when built with -fopenmp, main.cpp:361-393, 401-426, 439-495, 501-535) */
+  struct pmo_scratch *scr;
   double *postv;               /* [n_person][10] */
   int *best;
   int8_t *label;
@@ -75,6 +84,15 @@ static inline int fam_founders(const pmo_ctx *c, int f) { return c->unrelated ? 
 static inline int fam_nuclear(const pmo_ctx *c, int f) { return !c->unrelated && c->fam_kind[f] == PM_FAM_NUCLEAR; }
 static inline int fam_allfounders(const pmo_ctx *c, int f) { return fam_count(c, f) == fam_founders(c, f); }
 static inline double pen(const pmo_ctx *c, int person, int g) { return c->lktab[c->pl[person * 10 + g]]; }
+static inline struct pmo_scratch *SC(const pmo_ctx *c) {   /* this thread's scratch (unique across nested teams) */
+#ifdef _OPENMP
+  int t = 0;
+  for (int l = 1, lv = omp_get_level(); l <= lv; l++) t = t * omp_get_team_size(l) + omp_get_ancestor_thread_num(l);
+  return &c->scr[t < PMO_MAXT ? t : 0];
+#else
+  return &c->scr[0];
+#endif
+}
 
 static void set_alleles(const pmo_ctx *c, lkobj *o, int a1, int a2) {
   (void)c; o->a1 = a1; o->a2 = a2; o->g11 = GI(a1, a1); o->g12 = GI(a1, a2); o->g22 = GI(a2, a2);
@@ -144,7 +162,7 @@ static double poly_prior(const pmo_ctx *c) {
 
 /* SetParentPrior, NucFamGenotypeLikelihood.cpp:318-368 (pow(freq,k) is __builtin_powi under gnu++98) */
 static void set_parent_prior(pmo_ctx *c, const lkobj *o, double f) {
-  double *p = c->parentPrior;
+  double *p = SC(c)->parentPrior;
   if (c->ped.n_fam > 1 || o->is_mono) {
     if (!c->isX && !c->isY && !c->isMT) {
       p[0] = (f * f) * (f * f);
@@ -177,7 +195,7 @@ static void set_parent_prior(pmo_ctx *c, const lkobj *o, double f) {
 
 /* SetParentPrior_denovo / SetParentPriorSingleTrio_denovo, :370-420 */
 static void set_parent_prior_denovo(pmo_ctx *c, double f) {
-  double *p = c->parentPrior;
+  double *p = SC(c)->parentPrior;
   if (c->ped.n_fam > 1 || f == 1.0) {
     p[0] = (f * f) * (f * f);
     p[1] = f * f * f * (1 - f) * 2;
@@ -262,7 +280,8 @@ static void parent_marginal(pmo_ctx *c, const lkobj *o, int f, double freq, int 
     if (c->isMT) F12 = M12 = 0.0;
   }
   double lF[3] = {F11, F12, F22}, lM[3] = {M11, M12, M22};
-  for (int a = 0; a < 3; a++) for (int b = 0; b < 3; b++) c->parentGLF[3 * a + b] = lF[a] * lM[b];
+  struct pmo_scratch *w = SC(c);
+  for (int a = 0; a < 3; a++) for (int b = 0; b < 3; b++) w->parentGLF[3 * a + b] = lF[a] * lM[b];
   if (!denovo) set_parent_prior(c, o, freq);
   else set_parent_prior_denovo(c, freq);
   for (int k = 0; k < 9; k++) {
@@ -273,8 +292,8 @@ static void parent_marginal(pmo_ctx *c, const lkobj *o, int f, double freq, int 
       else t = one_kid_denovo(c, o, p0 + j, k);
       kids *= t;
     }
-    double cond = kids * c->parentGLF[k];
-    c->parentMarginal[k] = cond * c->parentPrior[k];
+    double cond = kids * w->parentGLF[k];
+    w->parentMarginal[k] = cond * w->parentPrior[k];
   }
 }
 
@@ -301,7 +320,8 @@ static double lk_single_fam(pmo_ctx *c, const lkobj *o, int f, double freq, int 
   }
   parent_marginal(c, o, f, freq, denovo);
   double sum = 0.0;
-  for (int k = 0; k < 9; k++) sum += c->parentMarginal[k];
+  const double *pm = SC(c)->parentMarginal;
+  for (int k = 0; k < 9; k++) sum += pm[k];
   return sum;
 }
 
@@ -316,12 +336,13 @@ static double tba(const pmo_ctx *c, int i, int j, int k, int child_sex) {
 }
 
 static double *find_mp(pmo_ctx *c, int a, int b, int create) {
-  for (int i = 0; i < c->nmp; i++) if (c->mpkey[i][0] == a && c->mpkey[i][1] == b) return &c->mp[i][0][0];
+  struct pmo_scratch *w = SC(c);
+  for (int i = 0; i < w->nmp; i++) if (w->mpkey[i][0] == a && w->mpkey[i][1] == b) return &w->mp[i][0][0];
   if (!create) return NULL;
-  int i = c->nmp++;   /* SetMarriagePartials, :1400-1415: all ones */
-  c->mpkey[i][0] = a; c->mpkey[i][1] = b;
-  for (int x = 0; x < 10; x++) for (int y = 0; y < 10; y++) c->mp[i][x][y] = 1.0;
-  return &c->mp[i][0][0];
+  int i = w->nmp++;   /* SetMarriagePartials, :1400-1415: all ones */
+  w->mpkey[i][0] = a; w->mpkey[i][1] = b;
+  for (int x = 0; x < 10; x++) for (int y = 0; y < 10; y++) w->mp[i][x][y] = 1.0;
+  return &w->mp[i][0][0];
 }
 
 /* One ES likelihood of family f.  ns = 3 (bi-allelic, CalcSingleFamLikelihood_BA, FamilyLikelihoodSeq.cpp:256-266)
@@ -330,7 +351,7 @@ static double *find_mp(pmo_ctx *c, int a, int b, int create) {
 static double es_likelihood(pmo_ctx *c, const lkobj *o, int f, double freq, int ns, int zero_person, int zero_geno) {
   const int p0 = c->fam_start[f], n = fam_count(c, f), nf = c->fam_founders[f];
   const int gidx[3] = {o->g11, o->g12, o->g22};
-  double *P = c->partials;
+  double *P = SC(c)->partials;
   /* penetrance with FillZeroPenetrance applied */
 #define PEN(i, g) ((zero_person == (i) && (g) != zero_geno) ? 0.0 : pen(c, p0 + (i), (g)))
   for (int i = 0; i < n; i++) {
@@ -363,7 +384,7 @@ static double es_likelihood(pmo_ctx *c, const lkobj *o, int f, double freq, int 
     }
   }
 #undef PEN
-  c->nmp = 0;
+  SC(c)->nmp = 0;
   const pm_peel_step *st = c->steps + c->peel_start[f];
   const int nst = c->peel_start[f + 1] - c->peel_start[f];
   for (int s = 0; s < nst; s++) {
@@ -416,6 +437,10 @@ static double es_likelihood(pmo_ctx *c, const lkobj *o, int f, double freq, int 
 /* FamilyLikelihoodSeq::CalcAllFamLogLikelihood, FamilyLikelihoodSeq.cpp:222-240 (serial family order) */
 static double all_fam_loglik(pmo_ctx *c, lkobj *o, double freq) {
   double loglk = 0.0;
+  /* the reference's family loop is an `omp parallel for reduction(+:loglk)` (:225): inside the configuration sections
+   * it is an inactive nested region (serial, in family order); only the de novo LR re-optimisation outside them
+   * (main.cpp:569-572) runs it on several threads, with a thread-count-dependent summation order */
+#pragma omp parallel for reduction(+:loglk)
   for (int f = 0; f < c->ped.n_fam; f++) {
     if (fam_nuclear(c, f) || fam_allfounders(c, f))
       loglk += log10(lk_single_fam(c, o, f, freq, c->denovo));
@@ -486,7 +511,10 @@ static int g_brent_err;
 static double poly_loglik(pmo_ctx *c, lkobj *o, int a1, int a2) {
   set_alleles(c, o, a1, a2);
   if (c->ped.n_fam > 1 || (c->ped.n_fam == 1 && !fam_nuclear(c, 0))) {
-    if (optimize(c, o) != 0) g_brent_err = 1;
+    if (optimize(c, o) != 0) {
+#pragma omp atomic write
+      g_brent_err = 1;
+    }
     return -o->fmin;
   }
   o->evals++;
@@ -648,7 +676,7 @@ static void post_nuc(pmo_ctx *c, lkobj *o, int f, double freq, int denovo) {
     return;
   }
   parent_marginal(c, o, f, freq, denovo);
-  const double *m = c->parentMarginal;
+  const double *m = SC(c)->parentMarginal;
   for (int j = 0; j < n; j++) {
     int p = p0 + j;
     if (!denovo) o->sex = c->sex[p];
@@ -668,7 +696,7 @@ static void post_nuc(pmo_ctx *c, lkobj *o, int f, double freq, int denovo) {
       double J[9][3];
       for (int k = 0; k < 9; k++) {
         kid_geno(c, o, f, j, k, J[k]);
-        double w = c->parentGLF[k] * c->parentPrior[k];
+        double w = SC(c)->parentGLF[k] * SC(c)->parentPrior[k];
         J[k][0] *= w; J[k][1] *= w; J[k][2] *= w;
       }
       double g[3];
@@ -690,7 +718,7 @@ static void post_nuc(pmo_ctx *c, lkobj *o, int f, double freq, int denovo) {
           if (i != j) { double lk = one_kid_denovo(c, o, p0 + i, k); for (int t = 0; t < 10; t++) J[k][t] *= lk; }
           else { double jt[10]; joint_geno_denovo(c, o, p0 + i, k, jt); for (int t = 0; t < 10; t++) J[k][t] *= jt[t]; }
         }
-        double w = c->parentGLF[k] * c->parentPrior[k];
+        double w = SC(c)->parentGLF[k] * SC(c)->parentPrior[k];
         for (int t = 0; t < 10; t++) J[k][t] *= w;
       }
       double g[10], sum = 0.0;
@@ -803,7 +831,7 @@ static double vcf_all_fam_loglik(pmo_ctx *c, lkobj *o, double freq) {
     } else if (vcf_closed_form(c, f)) {
       parent_marginal(c, o, f, freq, 0);   /* lkSingleFam :527-535; SetParentPrior since nFam > 1 */
       double sum = 0.0;
-      for (int k = 0; k < 9; k++) sum += c->parentMarginal[k];
+      for (int k = 0; k < 9; k++) sum += SC(c)->parentMarginal[k];
       loglk += log10(sum);
     } else {
       loglk += log10(es_likelihood(c, o, f, freq, 3, -1, -1));   /* CalcSingleFamLogLikelihood_BA */
@@ -876,7 +904,8 @@ pmo_ctx *pmo_create(const pm_pedigree *ped, const pm_params *par) {
   c->is_founder = malloc(np); memcpy(c->is_founder, ped->is_founder, np);
   int maxfs = 1;
   for (int f = 0; f < nf; f++) if (c->fam_start[f + 1] - c->fam_start[f] > maxfs) maxfs = c->fam_start[f + 1] - c->fam_start[f];
-  c->partials = malloc(sizeof(double) * 10 * maxfs);
+  c->scr = calloc(PMO_MAXT, sizeof(struct pmo_scratch));
+  for (int t = 0; t < PMO_MAXT; t++) c->scr[t].partials = malloc(sizeof(double) * 10 * maxfs);
   c->postv = calloc((size_t)np * 10, sizeof(double));
   c->best = calloc(np, sizeof(int)); c->label = calloc(np, 1); c->dosage = calloc(np, sizeof(double));
   c->denovo = par->denovo;
@@ -889,7 +918,9 @@ pmo_ctx *pmo_create(const pm_pedigree *ped, const pm_params *par) {
 void pmo_destroy(pmo_ctx *c) {
   if (!c) return;
   free(c->fam_start); free(c->fam_founders); free(c->fam_kind); free(c->peel_start); free(c->steps);
-  free(c->sex); free(c->is_founder); free(c->partials); free(c->postv); free(c->best); free(c->label); free(c->dosage);
+  free(c->sex); free(c->is_founder);
+  for (int t = 0; t < PMO_MAXT; t++) free(c->scr[t].partials);
+  free(c->scr); free(c->postv); free(c->best); free(c->label); free(c->dosage);
   free(c);
 }
 
@@ -964,13 +995,28 @@ int pmo_site(pmo_ctx *c, const uint8_t *pl, const uint32_t *dm, int32_t refBase,
   if (P->quick_call) {   /* main.cpp:354-437 */
     c->unrelated = 1;
     double v[7];
-    v[0] = log10(1 - prior) + mono_loglik(c);
-    v[1] = log10(prior * pts) + poly_loglik(c, &c->lk[1], refBase, ts);
-    v[2] = log10(prior * ptv) + poly_loglik(c, &c->lk[2], refBase, tv1);
-    v[3] = log10(prior * ptv) + poly_loglik(c, &c->lk[3], refBase, tv2);
+#pragma omp parallel sections
+    {
+#pragma omp section
+      v[0] = log10(1 - prior) + mono_loglik(c);
+#pragma omp section
+      v[1] = log10(prior * pts) + poly_loglik(c, &c->lk[1], refBase, ts);
+#pragma omp section
+      v[2] = log10(prior * ptv) + poly_loglik(c, &c->lk[2], refBase, tv1);
+#pragma omp section
+      v[3] = log10(prior * ptv) + poly_loglik(c, &c->lk[3], refBase, tv2);
+    }
     maxidx = var_posterior(c, v, 4, &vpp, &qual);
     if (vpp < 0.99) {
-      for (int k = 4; k < 7; k++) v[k] = log10(prior * 0.001) + poly_loglik(c, &c->lk[k], pa[k], pb[k]);
+#pragma omp parallel sections
+      {
+#pragma omp section
+        v[4] = log10(prior * 0.001) + poly_loglik(c, &c->lk[4], pa[4], pb[4]);
+#pragma omp section
+        v[5] = log10(prior * 0.001) + poly_loglik(c, &c->lk[5], pa[5], pb[5]);
+#pragma omp section
+        v[6] = log10(prior * 0.001) + poly_loglik(c, &c->lk[6], pa[6], pb[6]);
+      }
       maxidx = var_posterior(c, v, 7, &vpp, &qual);
     }
     c->unrelated = 0;
@@ -980,24 +1026,42 @@ int pmo_site(pmo_ctx *c, const uint8_t *pl, const uint32_t *dm, int32_t refBase,
   }
 
   lkobj *o0 = &c->lk[0];
-  if (!c->denovo) {
-    varllk[0] = log10(1 - prior) + mono_loglik(c);
-  } else {
-    /* FamilyLikelihoodSeq::MonomorphismLogLikelihood_denovo, FamilyLikelihoodSeq.cpp:68-72 */
-    set_alleles(c, o0, refBase, refBase == 4 ? refBase - 1 : refBase + 1);
-    o0->evals++;
-    varllk[0] = log10(1 - prior) + all_fam_loglik(c, o0, 1.0);
+  /* the four configurations as the reference's `omp parallel sections` (main.cpp:439-495; a serial build runs them in
+   * order); each has its own lkobj and, under OpenMP, the thread's own objective scratch */
+#pragma omp parallel sections
+  {
+#pragma omp section
+    {
+      if (!c->denovo) {
+        varllk[0] = log10(1 - prior) + mono_loglik(c);
+      } else {
+        /* FamilyLikelihoodSeq::MonomorphismLogLikelihood_denovo, FamilyLikelihoodSeq.cpp:68-72 */
+        set_alleles(c, o0, refBase, refBase == 4 ? refBase - 1 : refBase + 1);
+        o0->evals++;
+        varllk[0] = log10(1 - prior) + all_fam_loglik(c, o0, 1.0);
+      }
+      noprior[0] = varllk[0] - log10(1 - prior); varfreq[0] = 1.0;
+    }
+#pragma omp section
+    {
+      varllk[1] = log10(prior * pts) + poly_loglik(c, &c->lk[1], refBase, ts);
+      noprior[1] = varllk[1] - log10(prior * 2. / 3.); varfreq[1] = c->lk[1].min;
+    }
+#pragma omp section
+    {
+      varllk[2] = log10(prior * ptv) + poly_loglik(c, &c->lk[2], refBase, tv1);
+      noprior[2] = varllk[2] - log10(prior * 1. / 6.); varfreq[2] = c->lk[2].min;
+    }
+#pragma omp section
+    {
+      varllk[3] = log10(prior * ptv) + poly_loglik(c, &c->lk[3], refBase, tv2);
+      noprior[3] = varllk[3] - log10(prior * 1. / 6.); varfreq[3] = c->lk[3].min;
+    }
   }
-  noprior[0] = varllk[0] - log10(1 - prior); varfreq[0] = 1.0;
-  varllk[1] = log10(prior * pts) + poly_loglik(c, &c->lk[1], refBase, ts);
-  noprior[1] = varllk[1] - log10(prior * 2. / 3.); varfreq[1] = c->lk[1].min;
-  varllk[2] = log10(prior * ptv) + poly_loglik(c, &c->lk[2], refBase, tv1);
-  noprior[2] = varllk[2] - log10(prior * 1. / 6.); varfreq[2] = c->lk[2].min;
-  varllk[3] = log10(prior * ptv) + poly_loglik(c, &c->lk[3], refBase, tv2);
-  noprior[3] = varllk[3] - log10(prior * 1. / 6.); varfreq[3] = c->lk[3].min;
   maxidx = var_posterior(c, varllk, 4, &vpp, &qual);
   int ncfg = 4;
-  if (vpp < 0.99) {
+  if (vpp < 0.99) {   /* main.cpp:499-537 */
+#pragma omp parallel for schedule(static, 1)
     for (int k = 4; k < 7; k++) {
       varllk[k] = log10(prior * 0.001) + poly_loglik(c, &c->lk[k], pa[k], pb[k]);
       noprior[k] = varllk[k] - log10(prior * 0.001);

@@ -275,15 +275,29 @@ int main(int argc, char* argv[]) {
 
       if (quick_call) {
         for (int r = 0; r < 7; r++) lk[r].MakeUnrelated();
-        m0.varllk[0] = log10(1 - polyPrior_unr) + lk[0].MonomorphismLogLikelihood(refBase);
-        m0.varllk[1] = log10(polyPrior_unr * p_ts) + lk[1].PolymorphismLogLikelihood(refBase, ts);
-        m0.varllk[2] = log10(polyPrior_unr * p_tv) + lk[2].PolymorphismLogLikelihood(refBase, tv1);
-        m0.varllk[3] = log10(polyPrior_unr * p_tv) + lk[3].PolymorphismLogLikelihood(refBase, tv2);
+        // main.cpp:361-393 / 401-426: `omp parallel sections` over the configurations, as the reference
+#pragma omp parallel sections
+        {
+#pragma omp section
+          m0.varllk[0] = log10(1 - polyPrior_unr) + lk[0].MonomorphismLogLikelihood(refBase);
+#pragma omp section
+          m0.varllk[1] = log10(polyPrior_unr * p_ts) + lk[1].PolymorphismLogLikelihood(refBase, ts);
+#pragma omp section
+          m0.varllk[2] = log10(polyPrior_unr * p_tv) + lk[2].PolymorphismLogLikelihood(refBase, tv1);
+#pragma omp section
+          m0.varllk[3] = log10(polyPrior_unr * p_tv) + lk[3].PolymorphismLogLikelihood(refBase, tv2);
+        }
         maxidx = m0.CalcVarPosterior(4);
         if (m0.varPostProb < 0.99) {
-          m0.varllk[4] = log10(polyPrior_unr * 0.001) + lk[4].PolymorphismLogLikelihood(ts, tv1);
-          m0.varllk[5] = log10(polyPrior_unr * 0.001) + lk[5].PolymorphismLogLikelihood(ts, tv2);
-          m0.varllk[6] = log10(polyPrior_unr * 0.001) + lk[6].PolymorphismLogLikelihood(tv1, tv2);
+#pragma omp parallel sections
+          {
+#pragma omp section
+            m0.varllk[4] = log10(polyPrior_unr * 0.001) + lk[4].PolymorphismLogLikelihood(ts, tv1);
+#pragma omp section
+            m0.varllk[5] = log10(polyPrior_unr * 0.001) + lk[5].PolymorphismLogLikelihood(ts, tv2);
+#pragma omp section
+            m0.varllk[6] = log10(polyPrior_unr * 0.001) + lk[6].PolymorphismLogLikelihood(tv1, tv2);
+          }
           maxidx = m0.CalcVarPosterior(7);
         }
         if (m0.varPostProb < posterior || maxidx == 0) { sd.status = 7; if (dsFH) fwrite(&sd, sizeof(sd), 1, dsFH); continue; }
@@ -291,30 +305,41 @@ int main(int argc, char* argv[]) {
         for (int r = 0; r < 7; r++) lk[r].evals = 0;
       }
 
-      // Most likely configurations: monomorphic + the three ref/alt pairs (reference: 4 omp sections).
-      if (!par.denovo) {
-        double l = log10(1 - polyPrior) + lk[0].MonomorphismLogLikelihood(refBase);
-        m0.varllk[0] = l; m0.varllk_noprior[0] = l - log10(1 - polyPrior); m0.varfreq[0] = 1.0;
-      } else {
-        double l = log10(1 - polyPrior) + lk[0].MonomorphismLogLikelihood_denovo(refBase, refBase == 4 ? refBase - 1 : refBase + 1);
-        m0.varllk[0] = l; m0.varllk_noprior[0] = l - log10(1 - polyPrior); m0.varfreq[0] = 1.0;
-      }
+      // Most likely configurations: monomorphic + the three ref/alt pairs, as the reference's 4 `omp parallel
+      // sections` (main.cpp:439-495; the family loops inside them are inactive nested regions)
+#pragma omp parallel sections
       {
-        double l = log10(polyPrior * p_ts) + lk[1].PolymorphismLogLikelihood(refBase, ts);
-        m0.varllk[1] = l; m0.varllk_noprior[1] = l - log10(polyPrior * 2. / 3.); m0.varfreq[1] = lk[1].GetMinimizer();
-      }
-      {
-        double l = log10(polyPrior * p_tv) + lk[2].PolymorphismLogLikelihood(refBase, tv1);
-        m0.varllk[2] = l; m0.varllk_noprior[2] = l - log10(polyPrior * 1. / 6.); m0.varfreq[2] = lk[2].GetMinimizer();
-      }
-      {
-        double l = log10(polyPrior * p_tv) + lk[3].PolymorphismLogLikelihood(refBase, tv2);
-        m0.varllk[3] = l; m0.varllk_noprior[3] = l - log10(polyPrior * 1. / 6.); m0.varfreq[3] = lk[3].GetMinimizer();
+#pragma omp section
+        {
+          if (!par.denovo) {
+            double l = log10(1 - polyPrior) + lk[0].MonomorphismLogLikelihood(refBase);
+            m0.varllk[0] = l; m0.varllk_noprior[0] = l - log10(1 - polyPrior); m0.varfreq[0] = 1.0;
+          } else {
+            double l = log10(1 - polyPrior) + lk[0].MonomorphismLogLikelihood_denovo(refBase, refBase == 4 ? refBase - 1 : refBase + 1);
+            m0.varllk[0] = l; m0.varllk_noprior[0] = l - log10(1 - polyPrior); m0.varfreq[0] = 1.0;
+          }
+        }
+#pragma omp section
+        {
+          double l = log10(polyPrior * p_ts) + lk[1].PolymorphismLogLikelihood(refBase, ts);
+          m0.varllk[1] = l; m0.varllk_noprior[1] = l - log10(polyPrior * 2. / 3.); m0.varfreq[1] = lk[1].GetMinimizer();
+        }
+#pragma omp section
+        {
+          double l = log10(polyPrior * p_tv) + lk[2].PolymorphismLogLikelihood(refBase, tv1);
+          m0.varllk[2] = l; m0.varllk_noprior[2] = l - log10(polyPrior * 1. / 6.); m0.varfreq[2] = lk[2].GetMinimizer();
+        }
+#pragma omp section
+        {
+          double l = log10(polyPrior * p_tv) + lk[3].PolymorphismLogLikelihood(refBase, tv2);
+          m0.varllk[3] = l; m0.varllk_noprior[3] = l - log10(polyPrior * 1. / 6.); m0.varfreq[3] = lk[3].GetMinimizer();
+        }
       }
       maxidx = m0.CalcVarPosterior(4);
       sd.n_cfg = 4;
       if (m0.varPostProb < 0.99) {
         const int pa[3] = {ts, ts, tv1}, pb[3] = {tv1, tv2, tv2};
+#pragma omp parallel for schedule(static, 1)   // main.cpp:501-535: three sections
         for (int k = 0; k < 3; k++) {
           double l = log10(polyPrior * 0.001) + lk[4 + k].PolymorphismLogLikelihood(pa[k], pb[k]);
           m0.varllk[4 + k] = l; m0.varllk_noprior[4 + k] = l - log10(polyPrior * 0.001);

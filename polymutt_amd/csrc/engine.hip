@@ -45,6 +45,10 @@ struct pm_engine {
   pm_synth_tables* d_syn = nullptr;
   uint8_t *d_pl = nullptr, *d_ref = nullptr;
   uint8_t* d_stage = nullptr;   // person-major staging block of pm_engine_run (transposed into d_pl)
+  // pm_engine_submit / pm_engine_collect: the batch in flight, its results and counts landing in page-locked memory
+  pm_site_result* h_res = nullptr;
+  int* h_counts = nullptr;
+  int pending_n = -1;
   uint32_t* d_dm = nullptr;
   pm_site_result* d_res = nullptr;
   pm_geno_call* d_calls = nullptr;
@@ -269,6 +273,8 @@ void pm_engine_destroy(pm_engine* E) {
   for (auto& pl : E->d_jit_slots)
     for (int* b : pl) if (b) hipFree(b);
   for (auto& pr : E->brent_events) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
+  if (E->h_res) hipHostFree(E->h_res);
+  if (E->h_counts) hipHostFree(E->h_counts);
   if (E->ev0) hipEventDestroy(E->ev0);
   if (E->ev1) hipEventDestroy(E->ev1);
   if (E->stream) hipStreamDestroy(E->stream);
@@ -955,7 +961,7 @@ static int run_pipeline(pm_engine* E, int n, const uint8_t* pl, const uint32_t* 
     void (*prep)(DevArgs) = E->par.numerics == PM_NUM_EXACT ? k_prep<1, true>
                           : (np % 16 == 0 && vmax >= 16) ? k_prep<16, false> : (np % 8 == 0 && vmax >= 8) ? k_prep<8, false>
                           : (np % 4 == 0 && vmax >= 4) ? k_prep<4, false> : k_prep<1, false>;
-    hipLaunchKernelGGL(prep, dim3((n + 3) / 4), dim3(256), 0, E->stream, A);
+    hipLaunchKernelGGL(prep, dim3((n + 4 * PREP_SPW - 1) / (4 * PREP_SPW)), dim3(256), 0, E->stream, A);
   }
   HIP_TRY(hipGetLastError());
   int rc;
@@ -1061,12 +1067,8 @@ int pm_engine_run_device(pm_engine* E, int32_t n, const uint8_t* d_pl, const uin
   return run_pipeline(E, n, d_pl, d_dm, d_ref, d_res ? d_res : E->d_res, d_calls ? d_calls : E->d_calls);
 }
 
-int pm_engine_sync(pm_engine* E) {
-  if (!E) return PM_EINVAL;
-  HIP_TRY(hipSetDevice(E->device));
-  HIP_TRY(hipStreamSynchronize(E->stream));
-  int counts[16];
-  HIP_TRY(hipMemcpy(counts, E->d_counts, sizeof(counts), hipMemcpyDeviceToHost));
+// Bookkeeping after a batch's stream work has completed (counts = the batch's d_counts, already on the host).
+static int finish_batch(pm_engine* E, const int* counts) {
   if (counts[4] != 0x7fffffff) E->carry_postprob = true;
   E->stats.items += (int64_t)counts[0] + counts[1] + counts[2] + counts[8];
   E->stats.site_visits += (int64_t)counts[0] / (E->vcf ? 1 : (E->par.denovo && !mono_dn_in_prep(E)) ? 4 : 3) + counts[1] / 3 +
@@ -1078,26 +1080,94 @@ int pm_engine_sync(pm_engine* E) {
   return PM_OK;
 }
 
+int pm_engine_sync(pm_engine* E) {
+  if (!E) return PM_EINVAL;
+  HIP_TRY(hipSetDevice(E->device));
+  HIP_TRY(hipStreamSynchronize(E->stream));
+  int counts[16];
+  HIP_TRY(hipMemcpy(counts, E->d_counts, sizeof(counts), hipMemcpyDeviceToHost));
+  return finish_batch(E, counts);
+}
+
+// Host batch -> the engine's stream, without waiting: H2D of the person-major block (asynchronous when the host
+// buffers are page-locked, pm_host_alloc), transpose, the pipeline, and D2H of the per-site results and the
+// batch counters into the engine's page-locked buffers.  pm_engine_collect waits and hands them out.
+int pm_engine_submit(pm_engine* E, int32_t n, const uint8_t* pl, const uint32_t* dm, const uint8_t* ref) {
+  if (!E || n < 0 || n > E->max_batch || (n > 0 && (!pl || !ref || (!dm && !E->vcf)))) {
+    pm_set_last_error("pm_engine_submit: invalid arguments");
+    return PM_EINVAL;
+  }
+  if (E->pending_n >= 0) { pm_set_last_error("pm_engine_submit: the previous batch has not been collected"); return PM_EINVAL; }
+  HIP_TRY(hipSetDevice(E->device));
+  if (!E->h_res) {
+    HIP_TRY(hipHostMalloc((void**)&E->h_res, sizeof(pm_site_result) * (size_t)E->max_batch, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&E->h_counts, 16 * sizeof(int), hipHostMallocDefault));
+  }
+  E->pending_n = n;
+  if (n == 0) return PM_OK;
+  const size_t np = E->n_person;
+  HIP_TRY(hipMemcpyAsync(E->d_stage, pl, (size_t)n * np * 10, hipMemcpyHostToDevice, E->stream));
+  if (!E->vcf)   // (vcf_mode reads no depth: dm is neither copied nor needed, and may be NULL)
+    HIP_TRY(hipMemcpyAsync(E->d_dm, dm, (size_t)n * np * 4, hipMemcpyHostToDevice, E->stream));
+  HIP_TRY(hipMemcpyAsync(E->d_ref, ref, (size_t)n, hipMemcpyHostToDevice, E->stream));
+  int rc = pm_engine_to_planar(E, n, E->d_stage, E->d_pl);   // the engine's genotype-planar layout
+  if (rc) return rc;
+  rc = run_pipeline(E, n, E->d_pl, E->d_dm, E->d_ref, E->d_res, E->d_calls);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(E->h_res, E->d_res, sizeof(pm_site_result) * n, hipMemcpyDeviceToHost, E->stream));
+  HIP_TRY(hipMemcpyAsync(E->h_counts, E->d_counts, 16 * sizeof(int), hipMemcpyDeviceToHost, E->stream));
+  return PM_OK;
+}
+
+int pm_engine_collect(pm_engine* E, pm_site_result* res, pm_geno_call* calls, int32_t* n_rows) {
+  if (!E || !n_rows || E->pending_n < 0 || (E->pending_n > 0 && !res)) {
+    pm_set_last_error("pm_engine_collect: invalid arguments (no batch submitted?)");
+    return PM_EINVAL;
+  }
+  const int n = E->pending_n;
+  E->pending_n = -1;
+  *n_rows = 0;
+  if (n == 0) return PM_OK;
+  HIP_TRY(hipSetDevice(E->device));
+  HIP_TRY(hipStreamSynchronize(E->stream));
+  int counts[16];
+  memcpy(counts, E->h_counts, sizeof(counts));
+  int rc = finish_batch(E, counts);
+  if (rc) return rc;
+  memcpy(res, E->h_res, sizeof(pm_site_result) * n);
+  *n_rows = counts[3];
+  const size_t np = E->n_person;
+  if (calls && counts[3] > 0) {
+    if (E->vcf) {   // 4-B rows on the device (pm_vcf_call), expanded into the caller's pm_geno_call rows
+      const size_t nr = np * (size_t)counts[3];
+      std::vector<pm_vcf_call> v(nr);
+      HIP_TRY(hipMemcpy(v.data(), E->d_calls, sizeof(pm_vcf_call) * nr, hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < nr; i++) {
+        pm_geno_call c;
+        c.dosage = 0.0; c.best = v[i].best; c.gq = v[i].gq; c.label = v[i].label;
+        c._pad[0] = c._pad[1] = c._pad[2] = 0;
+        calls[i] = c;
+      }
+    } else HIP_TRY(hipMemcpy(calls, E->d_calls, sizeof(pm_geno_call) * np * counts[3], hipMemcpyDeviceToHost));
+  }
+  return PM_OK;
+}
+
 int pm_engine_run(pm_engine* E, int32_t n, const uint8_t* pl, const uint32_t* dm, const uint8_t* ref, int32_t on_device,
                   pm_site_result* res, pm_geno_call* calls, int32_t* n_rows) {
   if (!E || n < 0 || n > E->max_batch || !res || !n_rows) { pm_set_last_error("pm_engine_run: invalid arguments"); return PM_EINVAL; }
   *n_rows = 0;
   if (n == 0) return PM_OK;
+  if (!on_device) {   // host inputs: submit + collect
+    int rc = pm_engine_submit(E, n, pl, dm, ref);
+    if (rc) { E->pending_n = -1; return rc; }
+    return pm_engine_collect(E, res, calls, n_rows);
+  }
   HIP_TRY(hipSetDevice(E->device));
   const size_t np = E->n_person;
-  const uint8_t* spl = pl;   // person-major GLF records (host or device)
-  const uint32_t* ddm = dm;
-  const uint8_t* dref = ref;
-  if (!on_device) {
-    HIP_TRY(hipMemcpyAsync(E->d_stage, pl, (size_t)n * np * 10, hipMemcpyHostToDevice, E->stream));
-    if (!E->vcf)   // (vcf_mode reads no depth: dm is neither copied nor needed, and may be NULL)
-      HIP_TRY(hipMemcpyAsync(E->d_dm, dm, (size_t)n * np * 4, hipMemcpyHostToDevice, E->stream));
-    HIP_TRY(hipMemcpyAsync(E->d_ref, ref, (size_t)n, hipMemcpyHostToDevice, E->stream));
-    spl = E->d_stage; ddm = E->d_dm; dref = E->d_ref;
-  }
-  int rc = pm_engine_to_planar(E, n, spl, E->d_pl);   // the engine's genotype-planar layout
+  int rc = pm_engine_to_planar(E, n, pl, E->d_pl);   // the engine's genotype-planar layout
   if (rc) return rc;
-  rc = run_pipeline(E, n, E->d_pl, ddm, dref, E->d_res, E->d_calls);
+  rc = run_pipeline(E, n, E->d_pl, dm, ref, E->d_res, E->d_calls);
   if (rc) return rc;
   rc = pm_engine_sync(E);
   if (rc) return rc;
@@ -1106,7 +1176,7 @@ int pm_engine_run(pm_engine* E, int32_t n, const uint8_t* pl, const uint32_t* dm
   HIP_TRY(hipMemcpy(counts, E->d_counts, sizeof(counts), hipMemcpyDeviceToHost));
   *n_rows = counts[3];
   if (calls && counts[3] > 0) {
-    if (E->vcf) {   // 4-B rows on the device (pm_vcf_call), expanded into the caller's pm_geno_call rows
+    if (E->vcf) {
       const size_t nr = np * (size_t)counts[3];
       std::vector<pm_vcf_call> v(nr);
       HIP_TRY(hipMemcpy(v.data(), E->d_calls, sizeof(pm_vcf_call) * nr, hipMemcpyDeviceToHost));
@@ -1163,6 +1233,19 @@ int pm_engine_synth(pm_engine* E, int32_t n, uint64_t seed, uint64_t off, uint8_
   hipLaunchKernelGGL(k_synth, dim3((unsigned)((total + tb - 1) / tb)), dim3(tb), 0, E->stream, A, n, seed, off, d_pl, d_dm, d_ref);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(E->stream));
+  return PM_OK;
+}
+
+int pm_host_alloc(uint64_t bytes, void** p) {
+  if (!p) return PM_EINVAL;
+  *p = nullptr;
+  if (bytes == 0) return PM_OK;
+  HIP_TRY(hipHostMalloc(p, bytes, hipHostMallocDefault));
+  return PM_OK;
+}
+
+int pm_host_free(void* p) {
+  if (p) HIP_TRY(hipHostFree(p));
   return PM_OK;
 }
 

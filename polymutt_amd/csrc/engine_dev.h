@@ -39,6 +39,9 @@
 #ifndef PM_HOIST_CHUNK
 #define PM_HOIST_CHUNK 4
 #endif
+#ifndef PM_QD_MONO
+#define PM_QD_MONO 1
+#endif
 #ifndef PM_POLY_WAVES
 #define PM_POLY_WAVES 2
 #endif
@@ -1752,7 +1755,7 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
         // cfg-1 item (a1 = ref, geno11 = (ref, ref)) has just hoisted.  One product over the slots and lanes, one log10;
         // stored with the previous item's results (before the next prefetch in vmcnt order).
         double mono_dn = 0.0;
-        const bool mdn = A.mono_dn == 2 && cfg == 1;
+        const bool mdn = PM_QD_MONO && A.mono_dn == 2 && cfg == 1;
         if (mdn) {
           double m; int e;
           lane_poly_top<S>((const double(*)[5])cond, m, e);
@@ -1993,144 +1996,157 @@ __device__ __forceinline__ void load_dwords(const uint32_t* p, uint32_t* out) {
 // (NucFamGenotypeLikelihood.cpp:502-546).  SERIAL (PM_NUM_EXACT): the mono sum -PL/10 is accumulated in
 // the reference's person order (VEC = 1, lanes ascending via ballot); otherwise it is -(Sum PL)/10 from
 // the exact integer sum -- correctly rounded, within ~1e-14 relative of the serial sum.
+// PREP_SPW sites per wave, one after the other (a block of 4 waves takes 4 x PREP_SPW consecutive sites), so the
+// block-level work -- one returning atomic that reserves the block's Brent items (the sites' items then go to
+// consecutive slots in site order) and at most 9 counter atomics -- is shared by 4 x PREP_SPW sites.  (One
+// same-address atomic per site serialised k_prep: 262 144 returning atomics on counts[0] per batch.)
+#define PREP_SPW 8
 template <int VEC, bool SERIAL>
 __global__ void __launch_bounds__(256) k_prep(DevArgs A) {
   __shared__ unsigned long long s_c[9];
   __shared__ double s_lk[256];
   __shared__ double s_M[100];
+  __shared__ int s_nit[4 * PREP_SPW], s_pre[4 * PREP_SPW];   // items per site of the block (0: none), exclusive prefix
+  __shared__ int s_base;
   if (threadIdx.x < 9) s_c[threadIdx.x] = 0;
   if (A.mono_dn == 1) {
     s_lk[threadIdx.x] = A.lktab[threadIdx.x];
     if (threadIdx.x < 100) s_M[threadIdx.x] = A.M[threadIdx.x];
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int site = wave;
-  bool valid = false;
-  if (site < A.n) {
-    const int rb = A.ref[site];
-    const int r = A.vcf ? (rb & 15) : rb, alt = rb >> 4;
-    const int np = A.n_person;
-    const uint8_t* pl = A.pl + (size_t)site * np * 10;
-    const uint32_t* dm = A.dm + (size_t)site * np;
-    const bool okref = r >= 1 && r <= 4 && (!A.vcf || (alt >= 1 && alt <= 4 && alt != r));
-    const int h = okref ? d_gi(r, r) : 0;
-    long long dsum = 0, mqsum = 0, nsd = 0, plsum = 0;
-    double mono = 0.0;
-    // lean --denovo: MonomorphismLogLikelihood_denovo (the cfg-0 item: CalcAllFamLogLikelihood at f = 1).
-    // SetParentPrior(1) = (1, 0, ..., 0), so each nuclear family contributes cond[0] = (Prod_kids
-    // CalcDenovoMutLk(geno11)) * F11 * M11 (:1041-1132, :1553-1562): a product of per-person factors --
-    // founders lk[geno11], kids their g11 dot product -- taken here as one normalised product per site.
-    // (mono_dn == 2: the cfg-1 QUAD item forms it instead; k_prep then reads only dm and the hom-ref plane)
-    const bool mdn = A.mono_dn == 1 && okref;
-    double dm_m = 1.0;
-    int dm_e = 0;
-    const uint8_t* plane_h = pl + (size_t)h * np;
-    for (int base = 0; base < np; base += 64 * VEC) {
-      const int p0 = base + lane * VEC;
-      uint32_t x[VEC];
-      uint8_t hr[VEC];
-      if (p0 < np) {   // np % VEC == 0: a lane's VEC persons are all present or all absent
-        if (!A.vcf) load_dwords<VEC>(dm + p0, x);
-        else {   // the VCF path has no read depth or mapping quality (PedVCF / FamilyLikelihoodSeq_VCF): dm is not read
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // the list and the items of a called site (main.cpp:327-437 order: quick pre-filter, else the pedigree model)
+  const int list = (A.vcf || !A.unrelated) ? 0 : 1;
+  const int k0 = A.vcf ? 1 : A.unrelated ? 1 : (A.denovo && !A.mono_dn) ? 0 : 1;   // first cfg (cfg 0: de novo mono)
+  const int nit_called = A.vcf ? 1 : A.unrelated ? 3 : 4 - k0;
+  const int site0 = blockIdx.x * 4 * PREP_SPW;
+  for (int j = 0; j < PREP_SPW; j++) {
+    const int sl = w * PREP_SPW + j, site = site0 + sl;
+    bool valid = false;
+    if (site < A.n) {
+      const int rb = A.ref[site];
+      const int r = A.vcf ? (rb & 15) : rb, alt = rb >> 4;
+      const int np = A.n_person;
+      const uint8_t* pl = A.pl + (size_t)site * np * 10;
+      const uint32_t* dm = A.dm + (size_t)site * np;
+      const bool okref = r >= 1 && r <= 4 && (!A.vcf || (alt >= 1 && alt <= 4 && alt != r));
+      const int h = okref ? d_gi(r, r) : 0;
+      long long dsum = 0, mqsum = 0, nsd = 0, plsum = 0;
+      double mono = 0.0;
+      // lean --denovo: MonomorphismLogLikelihood_denovo (the cfg-0 item: CalcAllFamLogLikelihood at f = 1).
+      // SetParentPrior(1) = (1, 0, ..., 0), so each nuclear family contributes cond[0] = (Prod_kids
+      // CalcDenovoMutLk(geno11)) * F11 * M11 (:1041-1132, :1553-1562): a product of per-person factors --
+      // founders lk[geno11], kids their g11 dot product -- taken here as one normalised product per site.
+      // (mono_dn == 2: the cfg-1 QUAD item forms it instead; k_prep then reads only dm and the hom-ref plane)
+      const bool mdn = A.mono_dn == 1 && okref;
+      double dm_m = 1.0;
+      int dm_e = 0;
+      const uint8_t* plane_h = pl + (size_t)h * np;
+      for (int base = 0; base < np; base += 64 * VEC) {
+        const int p0 = base + lane * VEC;
+        uint32_t x[VEC];
+        uint8_t hr[VEC];
+        if (p0 < np) {   // np % VEC == 0: a lane's VEC persons are all present or all absent
+          if (!A.vcf) load_dwords<VEC>(dm + p0, x);
+          else {   // the VCF path has no read depth or mapping quality (PedVCF / FamilyLikelihoodSeq_VCF): dm is not read
 #pragma unroll
-          for (int k = 0; k < VEC; k++) x[k] = 0;
+            for (int k = 0; k < VEC; k++) x[k] = 0;
+          }
+          load_bytes<VEC>(plane_h + p0, hr);
+        } else {
+#pragma unroll
+          for (int k = 0; k < VEC; k++) { x[k] = 0; hr[k] = 0; }
         }
-        load_bytes<VEC>(plane_h + p0, hr);
-      } else {
-#pragma unroll
-        for (int k = 0; k < VEC; k++) { x[k] = 0; hr[k] = 0; }
-      }
-#pragma unroll
-      for (int k = 0; k < VEC; k++) {
-        const int d = (int)(x[k] & 0xFFFFFF);
-        dsum += d; mqsum += (x[k] >> 24); nsd += d > 0;
-        plsum += hr[k];
-      }
-      if constexpr (SERIAL) {   // VEC == 1: lanes in ascending person order
-        unsigned long long m = __ballot(hr[0] != 0);   // zero terms add -0.0: no change to a sum starting at +0.0
-        const double t = -(double)hr[0] / 10;
-        while (m) {
-          const int l = __ffsll((long long)m) - 1;
-          m &= m - 1;
-          mono += __shfl(t, l, 64);
-        }
-      }
-      if (mdn && p0 < np) {
-        uint8_t fo[VEC];
-        load_bytes<VEC>((const uint8_t*)A.is_founder + p0, fo);
-        uint8_t kb[10][VEC];
-#pragma unroll
-        for (int g = 0; g < 10; g++) load_bytes<VEC>(pl + (size_t)g * np + p0, kb[g]);
 #pragma unroll
         for (int k = 0; k < VEC; k++) {
-          double fct;
-          if (fo[k]) fct = s_lk[hr[k]];
-          else {
-            fct = 0.0;
-#pragma unroll
-            for (int g = 0; g < 10; g++) fct += s_M[h * 10 + g] * s_lk[kb[g][k]];
+          const int d = (int)(x[k] & 0xFFFFFF);
+          dsum += d; mqsum += (x[k] >> 24); nsd += d > 0;
+          plsum += hr[k];
+        }
+        if constexpr (SERIAL) {   // VEC == 1: lanes in ascending person order
+          unsigned long long m = __ballot(hr[0] != 0);   // zero terms add -0.0: no change to a sum starting at +0.0
+          const double t = -(double)hr[0] / 10;
+          while (m) {
+            const int l = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            mono += __shfl(t, l, 64);
           }
-          int xe;
-          dm_m = frexp(dm_m * fct, &xe);
-          dm_e += xe;
+        }
+        if (mdn && p0 < np) {
+          uint8_t fo[VEC];
+          load_bytes<VEC>((const uint8_t*)A.is_founder + p0, fo);
+          uint8_t kb[10][VEC];
+#pragma unroll
+          for (int g = 0; g < 10; g++) load_bytes<VEC>(pl + (size_t)g * np + p0, kb[g]);
+#pragma unroll
+          for (int k = 0; k < VEC; k++) {
+            double fct;
+            if (fo[k]) fct = s_lk[hr[k]];
+            else {
+              fct = 0.0;
+#pragma unroll
+              for (int g = 0; g < 10; g++) fct += s_M[h * 10 + g] * s_lk[kb[g][k]];
+            }
+            int xe;
+            dm_m = frexp(dm_m * fct, &xe);
+            dm_e += xe;
+          }
         }
       }
-    }
-    if (mdn) {
-      wave_prod(dm_m, dm_e);
+      if (mdn) {
+        wave_prod(dm_m, dm_e);
+        if (lane == 0) {
+          A.raw[(size_t)site * 8] = log10_mant(dm_m, dm_e);
+          A.minv[site * 8] = 0.0;
+          A.evals[site * 8] = 1;
+        }
+      }
+      if constexpr (!SERIAL) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) plsum += __shfl_xor(plsum, o, 64);
+        mono = plsum ? -(double)plsum / 10 : 0.0;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) { dsum += __shfl_xor(dsum, o, 64); mqsum += __shfl_xor(mqsum, o, 64); nsd += __shfl_xor(nsd, o, 64); }
       if (lane == 0) {
-        A.raw[(size_t)site * 8] = log10_mant(dm_m, dm_e);
-        A.minv[site * 8] = 0.0;
-        A.evals[site * 8] = 1;
+        pm_site_result O;
+        memset(&O, 0, sizeof(O));
+        O.maxidx = -2; O.call_row = -1; O.ab = 0.5; O.denovo_lr = -1;
+        A.mono_plain[site] = mono;
+        if (!okref) O.status = PM_SITE_BAD_REF;
+        else {
+          atomicAdd(&s_c[r], 1ull);
+          const int td = (int)dsum, n = (int)nsd;
+          double avgmq = 0., ps = 0.;
+          if (n > 0) { avgmq = (double)mqsum / (double)n; ps = (double)n / (double)np; }
+          O.total_depth = td; O.num_samp_with_data = n; O.avg_map_qual = avgmq; O.perc_samp_with_data = ps;
+          int st = 0;   // filters, main.cpp:345-348 (the VCF path has none)
+          if (A.vcf) st = 0;
+          else if (td < A.min_total_depth) st = PM_SITE_MIN_DEPTH;
+          else if (A.max_total_depth > 0 && td > A.max_total_depth) st = PM_SITE_MAX_DEPTH;
+          else if (ps * 100 < A.min_ps) st = PM_SITE_MIN_PS;
+          else if (avgmq < A.min_map_quality) st = PM_SITE_MIN_MAPQ;
+          if (st) { O.status = st; atomicAdd(&s_c[4 + st], 1ull); }
+          else { O.status = PM_SITE_CALLED; valid = true; }
+        }
+        A.res[site] = O;
       }
     }
-    if constexpr (!SERIAL) {
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) plsum += __shfl_xor(plsum, o, 64);
-      mono = plsum ? -(double)plsum / 10 : 0.0;
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) { dsum += __shfl_xor(dsum, o, 64); mqsum += __shfl_xor(mqsum, o, 64); nsd += __shfl_xor(nsd, o, 64); }
-    if (lane == 0) {
-      pm_site_result O;
-      memset(&O, 0, sizeof(O));
-      O.maxidx = -2; O.call_row = -1; O.ab = 0.5; O.denovo_lr = -1;
-      A.mono_plain[site] = mono;
-      if (!okref) O.status = PM_SITE_BAD_REF;
-      else {
-        atomicAdd(&s_c[r], 1ull);
-        const int td = (int)dsum, n = (int)nsd;
-        double avgmq = 0., ps = 0.;
-        if (n > 0) { avgmq = (double)mqsum / (double)n; ps = (double)n / (double)np; }
-        O.total_depth = td; O.num_samp_with_data = n; O.avg_map_qual = avgmq; O.perc_samp_with_data = ps;
-        int st = 0;   // filters, main.cpp:345-348 (the VCF path has none)
-        if (A.vcf) st = 0;
-        else if (td < A.min_total_depth) st = PM_SITE_MIN_DEPTH;
-        else if (A.max_total_depth > 0 && td > A.max_total_depth) st = PM_SITE_MAX_DEPTH;
-        else if (ps * 100 < A.min_ps) st = PM_SITE_MIN_PS;
-        else if (avgmq < A.min_map_quality) st = PM_SITE_MIN_MAPQ;
-        if (st) { O.status = st; atomicAdd(&s_c[4 + st], 1ull); }
-        else { O.status = PM_SITE_CALLED; valid = true; }
-      }
-      A.res[site] = O;
-      if (valid && A.vcf) {   // PedVCF.cpp:131: PolymorphismLogLikelihood(ref, alt), one Brent
-        const int slot = atomicAdd(&A.counts[0], 1);
-        A.items[0][slot] = (site << 3) | 1;
-      } else if (valid && A.unrelated) {   // --quick_call pre-filter first (main.cpp:354-437)
-        const int slot = atomicAdd(&A.counts[1], 3);
-        for (int k = 0; k < 3; k++) A.items[1][slot + k] = (site << 3) | (k + 1);
-      } else if (valid) {
-        const int k0 = (A.denovo && !A.mono_dn) ? 0 : 1;   // cfg 0: de novo monomorphism (unless done above)
-        const int nit = 4 - k0;
-        const int slot = atomicAdd(&A.counts[0], nit);
-        for (int k = 0; k < nit; k++) A.items[0][slot + k] = (site << 3) | (k + k0);
-      }
-    }
+    if (lane == 0) s_nit[sl] = valid ? nit_called : 0;
   }
   __syncthreads();
-  if (threadIdx.x < 9 && s_c[threadIdx.x]) atomicAdd(&A.counters[threadIdx.x], s_c[threadIdx.x]);
+  if (threadIdx.x == 0) {   // the block's items: one reservation, then consecutive slots in site order
+    int t = 0;
+    for (int i = 0; i < 4 * PREP_SPW; i++) { s_pre[i] = t; t += s_nit[i]; }
+    s_base = t ? atomicAdd(&A.counts[list], t) : 0;
+    for (int i = 0; i < 9; i++) if (s_c[i]) atomicAdd(&A.counters[i], s_c[i]);
+  }
+  __syncthreads();
+  // lane i of wave w writes item i of each of its sites (at most 4 items per site)
+  for (int j = 0; j < PREP_SPW; j++) {
+    const int sl = w * PREP_SPW + j;
+    if (lane < s_nit[sl]) A.items[list][s_base + s_pre[sl] + lane] = ((site0 + sl) << 3) | (lane + k0);
+  }
 }
 
 // CalcVarPosterior (:1693-1749); returns maxidx, sets vpp/qual/alleles

@@ -101,6 +101,10 @@ EXPORTS = {
     "pm_engine_run": (i32, [C.c_void_p, i32, C.c_void_p, C.c_void_p, C.c_void_p, i32, C.c_void_p, C.c_void_p, P(i32)]),
     "pm_engine_run_device": (i32, [C.c_void_p, i32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "pm_engine_sync": (i32, [C.c_void_p]),
+    "pm_engine_submit": (i32, [C.c_void_p, i32, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "pm_engine_collect": (i32, [C.c_void_p, C.c_void_p, C.c_void_p, P(i32)]),
+    "pm_host_alloc": (i32, [u64, P(C.c_void_p)]),
+    "pm_host_free": (i32, [C.c_void_p]),
     "pm_engine_to_planar": (i32, [C.c_void_p, i32, C.c_void_p, C.c_void_p]),
     "pm_engine_counters": (i32, [C.c_void_p, P(Counters)]),
     "pm_engine_synth": (i32, [C.c_void_p, i32, u64, u64, C.c_void_p, C.c_void_p, C.c_void_p]),
@@ -252,6 +256,25 @@ class Engine:
         rows = i32(0)
         self._check(self.lib.pm_engine_run(self.h, n, _ptr(pl), _ptr(dm), _ptr(ref), 0, _ptr(res), _ptr(calls),
                                            C.byref(rows)))
+        return res, calls[: rows.value]
+
+    def submit(self, pl, dm, ref):
+        """pm_engine_submit: queue a batch of host arrays (kept referenced until collect()); returns at once."""
+        n = len(ref)
+        self._pending = (np.ascontiguousarray(pl, dtype=np.uint8).reshape(n, self.n_person, 10),
+                         np.ascontiguousarray(dm, dtype=np.uint32).reshape(n, self.n_person),
+                         np.ascontiguousarray(ref, dtype=np.uint8))
+        pl, dm, ref = self._pending
+        self._check(self.lib.pm_engine_submit(self.h, n, _ptr(pl), _ptr(dm), _ptr(ref)))
+
+    def collect(self):
+        """pm_engine_collect: wait for the submitted batch; (results[n], calls[rows, n_person]) as run() returns."""
+        n = len(self._pending[2])
+        res = np.zeros(n, dtype=SITE_DTYPE)
+        calls = np.zeros((n, self.n_person), dtype=CALL_DTYPE)
+        rows = i32(0)
+        self._check(self.lib.pm_engine_collect(self.h, _ptr(res), _ptr(calls), C.byref(rows)))
+        self._pending = None
         return res, calls[: rows.value]
 
     def run_device(self, n, d_pl, d_dm, d_ref, d_res=None, d_calls=None):

@@ -3,6 +3,10 @@
 #include <algorithm>
 #include <climits>
 #include <cstring>
+#include <cerrno>
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 namespace pmhost {
 
@@ -64,16 +68,31 @@ void BlockWriter::close() {
 }
 
 // ---------------------------------------------------------------------------------------------
-BlockSiteSource::~BlockSiteSource() { if (fh_) fclose(fh_); }
+BlockSiteSource::~BlockSiteSource() { if (fd_ >= 0) ::close(fd_); }
 
-void BlockSiteSource::get(void* p, size_t n) {
-  if (n && fread(p, 1, n, fh_) != n) throw FatalError("block file " + path_ + " is truncated\n");
+void BlockSiteSource::readAt(void* p, uint64_t off, size_t n) const {
+  char* d = (char*)p;
+  while (n > 0) {
+    const ssize_t got = ::pread(fd_, d, n, (off_t)off);
+    if (got < 0 && errno == EINTR) continue;
+    if (got <= 0) throw FatalError("block file " + path_ + " is truncated\n");
+    d += got; off += (uint64_t)got; n -= (size_t)got;
+  }
 }
 
-void BlockSiteSource::open(const std::string& path, int n_person) {
+void BlockSiteSource::get(void* p, size_t n) {
+  readAt(p, off_, n);
+  off_ += n;
+}
+
+void BlockSiteSource::open(const std::string& path, int n_person, int threads) {
   path_ = path;
-  fh_ = fopen(path.c_str(), "rb");
-  if (!fh_) throw FatalError("block file " + path + " can not be opened!\n");
+  fd_ = ::open(path.c_str(), O_RDONLY);
+  if (fd_ < 0) throw FatalError("block file " + path + " can not be opened!\n");
+  struct stat st;
+  if (fstat(fd_, &st) != 0) throw FatalError("block file " + path + " can not be opened!\n");
+  size_ = (uint64_t)st.st_size;
+  posix_fadvise(fd_, 0, 0, POSIX_FADV_SEQUENTIAL);
   char magic[4];
   uint32_t h[3];
   get(magic, 4); get(h, sizeof(h));
@@ -82,22 +101,26 @@ void BlockSiteSource::open(const std::string& path, int n_person) {
     throw FatalError(path + ": block file has " + std::to_string(h[0]) + " persons, the pedigree " + std::to_string(n_person) + "\n");
   np_ = n_person;
   // index (trailer: u64 index_offset "PMBE")
-  const long here = ftell(fh_);
-  if (fseek(fh_, -12, SEEK_END) == 0) {
+  if (size_ >= off_ + 12) {
     uint64_t at = 0;
     char end[4];
-    get(&at, 8); get(end, 4);
-    if (memcmp(end, "PMBE", 4) == 0 && fseek(fh_, (long)at, SEEK_SET) == 0) {
+    readAt(&at, size_ - 12, 8); readAt(end, size_ - 4, 4);
+    if (memcmp(end, "PMBE", 4) == 0 && at + 8 <= size_) {
       char tag[4];
       uint32_t nb = 0;
-      get(tag, 4); get(&nb, 4);
+      readAt(tag, at, 4); readAt(&nb, at + 4, 4);
       if (memcmp(tag, "PIDX", 4) == 0) {
         index_.resize(nb);
-        for (auto& e : index_) { get(&e.section, 4); get(&e.n, 4); get(&e.first_pos, 4); get(&e.last_pos, 4); get(&e.offset, 8); }
+        uint64_t o = at + 8;
+        for (auto& e : index_) {
+          readAt(&e.section, o, 4); readAt(&e.n, o + 4, 4); readAt(&e.first_pos, o + 8, 4); readAt(&e.last_pos, o + 12, 4);
+          readAt(&e.offset, o + 16, 8);
+          o += 24;
+        }
       }
     }
   }
-  fseek(fh_, here, SEEK_SET);
+  if (threads > 1) pool_.reset(new TaskPool(threads));
 }
 
 bool BlockSiteSource::nextSection() {
@@ -105,18 +128,20 @@ bool BlockSiteSource::nextSection() {
   if (inSection_) skipSection();
   while (inSection_) loadBlock();
   char tag[4];
-  if (fread(tag, 1, 4, fh_) != 4 || memcmp(tag, "SECT", 4) != 0) return false;   // "PIDX": no more sections
+  if (off_ + 4 > size_) return false;
+  get(tag, 4);
+  if (memcmp(tag, "SECT", 4) != 0) return false;   // "PIDX": no more sections
   int32_t mp;
   uint32_t len;
   get(&mp, 4); get(&len, 4);
   label_.assign(len, '\0');
-  get(&label_[0], len);
+  if (len) get(&label_[0], len);
   maxPos_ = mp;
   inSection_ = true;
   ended_ = false;
   n_ = cur_ = lastBegin_ = 0;
   section_++;
-  sectionStart_ = (uint64_t)ftell(fh_);
+  sectionStart_ = off_;
   rangeHi_ = INT64_MAX;
   return true;
 }
@@ -137,14 +162,14 @@ bool BlockSiteSource::seek(int64_t lo, int64_t hi) {
   for (const auto& e : index_)
     if ((int64_t)e.section == section_ && (int64_t)e.last_pos >= lo) { at = e.offset; found = true; break; }
   if (!found) at = sectionEnd();   // every block of the section lies below lo
-  if (fseek(fh_, (long)at, SEEK_SET) != 0) throw FatalError("block file " + path_ + ": seek failed\n");
+  off_ = at;
   n_ = cur_ = lastBegin_ = 0;
   return true;
 }
 
 void BlockSiteSource::skipSection() {
   if (index_.empty() || !inSection_) return;   // no index: nextSection reads the rest in order
-  if (fseek(fh_, (long)sectionEnd(), SEEK_SET) != 0) throw FatalError("block file " + path_ + ": seek failed\n");
+  off_ = sectionEnd();
   n_ = cur_ = lastBegin_ = 0;
   loadBlock();   // the "SEND" marker
   ended_ = true;
@@ -165,11 +190,13 @@ bool BlockSiteSource::loadBlock() {
   uint32_t n;
   get(&n, 4);
   n_ = (int)n;
-  pos_.resize(n); ref_.resize(n); pl_.resize((size_t)n * np_ * 10); dm_.resize((size_t)n * np_);
+  pos_.resize(n); ref_.resize(n);
   get(pos_.data(), 4 * (size_t)n);
   get(ref_.data(), n);
-  get(pl_.data(), pl_.size());
-  get(dm_.data(), dm_.size() * 4);
+  plOff_ = off_;   // the rows are read in fill(), straight into the caller's buffers
+  dmOff_ = plOff_ + (uint64_t)n * np_ * 10;
+  off_ = dmOff_ + (uint64_t)n * np_ * 4;
+  if (off_ > size_) throw FatalError("block file " + path_ + " is truncated\n");
   cur_ = lastBegin_ = 0;
   return true;
 }
@@ -179,12 +206,12 @@ int BlockSiteSource::nextSites(int maxSites, int* pos, uint8_t* ref) {
   if (ended_) return 0;
   if (cur_ == n_) {
     if (rangeHi_ != INT64_MAX) {   // the next block (index entries are in file order) starts past the range
-      const uint64_t at = (uint64_t)ftell(fh_);
+      const uint64_t at = off_;
       auto it = std::lower_bound(index_.begin(), index_.end(), at,
                                  [](const BlockIndexEntry& e, uint64_t o) { return e.offset < o; });
       if (it != index_.end() && it->offset == at && (int64_t)it->first_pos >= rangeHi_) { ended_ = true; return 0; }
     }
-    if (!loadBlock()) { ended_ = true; return 0; }
+    if (!loadBlock()) { ended_ = true; lastBegin_ = cur_; return 0; }
   }
   const int k = std::min(maxSites, n_ - cur_);
   for (int i = 0; i < k; i++) { pos[i] = pos_[cur_ + i]; ref[i] = ref_[cur_ + i]; }
@@ -193,13 +220,25 @@ int BlockSiteSource::nextSites(int maxSites, int* pos, uint8_t* ref) {
 }
 
 void BlockSiteSource::fill(const int* rowOf, uint8_t* pl, uint32_t* dm) {
-  for (int i = 0; i < cur_ - lastBegin_; i++) {
-    const int r = rowOf[i];
-    if (r < 0) continue;
-    const int s = lastBegin_ + i;
-    memcpy(pl + (size_t)r * np_ * 10, pl_.data() + (size_t)s * np_ * 10, (size_t)np_ * 10);
-    memcpy(dm + (size_t)r * np_, dm_.data() + (size_t)s * np_, (size_t)np_ * 4);
+  // runs of consecutive destination rows -> one PL and one depth read each, in chunks of <= 4 MB on the pool
+  struct Piece { char* dst; uint64_t off; size_t len; };
+  std::vector<Piece> pieces;
+  const size_t rpl = (size_t)np_ * 10, rdm = (size_t)np_ * 4, chunk = (size_t)4 << 20;
+  auto add = [&](char* dst, uint64_t off, size_t len) {
+    for (size_t o = 0; o < len; o += chunk) pieces.push_back({dst + o, off + o, std::min(chunk, len - o)});
+  };
+  const int cnt = cur_ - lastBegin_;
+  for (int i = 0; i < cnt;) {
+    if (rowOf[i] < 0) { i++; continue; }
+    int j = i + 1;
+    while (j < cnt && rowOf[j] == rowOf[j - 1] + 1) j++;
+    const int s = lastBegin_ + i, r = rowOf[i], m = j - i;
+    add((char*)(pl + (size_t)r * rpl), plOff_ + (uint64_t)s * rpl, (size_t)m * rpl);
+    add((char*)(dm + (size_t)r * np_), dmOff_ + (uint64_t)s * rdm, (size_t)m * rdm);
+    i = j;
   }
+  if (pool_ && pieces.size() > 1) pool_->run((int)pieces.size(), [&](int k) { readAt(pieces[k].dst, pieces[k].off, pieces[k].len); });
+  else for (auto& p : pieces) readAt(p.dst, p.off, p.len);
 }
 
 // ---------------------------------------------------------------------------------------------

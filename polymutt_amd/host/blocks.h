@@ -20,6 +20,7 @@
 #pragma once
 #include <cstdint>
 #include <cstdio>
+#include <memory>
 #include <string>
 #include <vector>
 #include "ingest.h"
@@ -52,9 +53,12 @@ class BlockWriter {
   std::vector<BlockIndexEntry> index_;
 };
 
+// Reads with pread at an explicit file offset: a block's header (positions, refBase) when nextSites reaches it,
+// and the PL / depth rows straight into the caller's batch rows in fill() -- one read per run of consecutive rows,
+// split into chunks read in parallel on the source's thread pool (no intermediate copy of the 14 B x n_person rows).
 class BlockSiteSource : public SiteStream {
  public:
-  void open(const std::string& path, int n_person);
+  void open(const std::string& path, int n_person, int threads = 1);
   ~BlockSiteSource();
   bool nextSection() override;
   const std::string& label() const override { return label_; }
@@ -71,23 +75,27 @@ class BlockSiteSource : public SiteStream {
  private:
   bool loadBlock();   // false at the section end marker
   uint64_t sectionEnd() const;   // file offset of the current section's "SEND" (index required)
-  void get(void* p, size_t n);
-  FILE* fh_ = nullptr;
+  void get(void* p, size_t n);   // n bytes at off_, advancing it
+  void readAt(void* p, uint64_t off, size_t n) const;
+  int fd_ = -1;
+  uint64_t off_ = 0, size_ = 0;
   std::string path_;
   int np_ = 0;
   std::string label_;
   int maxPos_ = 0;
   bool inSection_ = false, ended_ = true;
-  // the loaded block and the cursor into it; the last nextSites call covered [lastBegin_, cur_)
+  // the loaded block (its header, and the file offsets of its PL and depth rows) and the cursor into it; the last
+  // nextSites call covered [lastBegin_, cur_)
   std::vector<int> pos_;
-  std::vector<uint8_t> ref_, pl_;
-  std::vector<uint32_t> dm_;
+  std::vector<uint8_t> ref_;
+  uint64_t plOff_ = 0, dmOff_ = 0;
   int n_ = 0, cur_ = 0, lastBegin_ = 0;
   std::vector<BlockIndexEntry> index_;
   int64_t section_ = -1;        // the current section's number (the index's section field)
   uint64_t sectionStart_ = 0;   // file offset of the current section's first block (or its "SEND")
   long blocksRead_ = 0;
   int64_t rangeHi_ = INT64_MAX;   // seek's hi: no block starting at or past it is read
+  std::unique_ptr<TaskPool> pool_;
 };
 
 // Converts the GLF site stream of `ped` (index file glfIndexFile) into a .pmb file; returns the site count.

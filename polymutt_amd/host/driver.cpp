@@ -46,7 +46,7 @@ Options parse_command_line(int argc, char** argv) {
       {"pos", 's', &o.positionFile}, {"all_sites", 'b', &o.all_sites}, {"gl_off", 'b', &o.gl_off},
       {"quick_call", 'b', &o.quick_call},
       // engine options (not in the reference)
-      {"gpu", 'i', &o.device}, {"batch", 'i', &o.batch}, {"io_threads", 'i', &o.io_threads},
+      {"gpu", 'i', &o.device}, {"batch", 'i', &o.batch}, {"io_threads", 'i', &o.io_threads}, {"engines", 'i', &o.engines},
       {"in_blocks", 's', &o.blocksIn}, {"glf2blocks", 's', &o.blocksOut}, {"block_sites", 'i', &o.blockSites}, {"exact_log10", 'b', &o.exact_log10}, {"numerics", 's', &o.numerics},
   };
   auto assign = [](Flag& f, const char* v) {
@@ -96,6 +96,13 @@ Options parse_command_line(int argc, char** argv) {
 namespace {
 
 }  // namespace
+
+void* SiteEvaluator::host_alloc(size_t bytes) {
+  void* p = malloc(bytes ? bytes : 1);
+  if (!p) throw FatalError("out of host memory\n");
+  return p;
+}
+void SiteEvaluator::host_free(void* p) { free(p); }
 
 int default_io_threads(const Options& opt) {
   return opt.io_threads > 0 ? opt.io_threads : std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
@@ -175,17 +182,34 @@ class Channel {
   std::deque<T> q_;
 };
 
+// One batch of sites: the dense block rows the engine reads (in the evaluator's host memory -- page-locked for the
+// HIP engine, so its copies run asynchronously), the results and the genotype rows.
 struct Batch {
-  int n = 0, cap = 0, np = 0;
-  std::vector<uint8_t> pl, ref;
-  std::vector<uint32_t> dm;
+  int n = 0, cap = 0, np = 0, rows = 0;
+  SiteEvaluator* ev = nullptr;
+  uint8_t *pl = nullptr, *ref = nullptr;
+  uint32_t* dm = nullptr;
+  pm_site_result* res = nullptr;
+  pm_geno_call* calls = nullptr;
   std::vector<int> pos;
-  std::vector<pm_site_result> res;
-  std::vector<pm_geno_call> calls;
-  void init(int capacity, int nperson) {
-    cap = capacity; np = nperson; n = 0;
-    pl.resize((size_t)cap * np * 10); dm.resize((size_t)cap * np); ref.resize(cap); pos.resize(cap);
-    res.resize(cap); calls.resize((size_t)cap * np);
+  Batch() = default;
+  Batch(const Batch&) = delete;
+  Batch& operator=(const Batch&) = delete;
+  ~Batch() { release(); }
+  void init(SiteEvaluator& e, int capacity, int nperson) {
+    release();
+    ev = &e; cap = capacity; np = nperson; n = 0;
+    pl = (uint8_t*)e.host_alloc((size_t)cap * np * 10);
+    dm = (uint32_t*)e.host_alloc((size_t)cap * np * 4);
+    ref = (uint8_t*)e.host_alloc((size_t)cap);
+    res = (pm_site_result*)e.host_alloc(sizeof(pm_site_result) * (size_t)cap);
+    calls = (pm_geno_call*)e.host_alloc(sizeof(pm_geno_call) * (size_t)cap * np);
+    pos.assign(cap, 0);
+  }
+  void release() {
+    if (!ev) return;
+    for (void* p : {(void*)pl, (void*)dm, (void*)ref, (void*)res, (void*)calls}) ev->host_free(p);
+    pl = ref = nullptr; dm = nullptr; res = nullptr; calls = nullptr; ev = nullptr;
   }
 };
 
@@ -246,7 +270,7 @@ int run_polymutt_sharded(const Options& opt, const Pedigree& ped, SiteEvaluator&
   if (lead) printf("Analysis started on %s\n", ctime(&t0));
   const int np = (int)ped.column_pid.size();
   Batch B;
-  B.init(opt.batch > 0 ? opt.batch : 4096, np);
+  B.init(eval, opt.batch > 0 ? opt.batch : 4096, np);
   enum { K_ENTRIES = 16, K_OUT, K_REC, K_START, K_END, K_FIRST_END, K };
   bool earlier = false;        // a site of an earlier section (any shard) reached CalcPostProb
   int64_t outputs = 0;         // OutputVCF calls over all shards: the header exists iff > 0
@@ -281,14 +305,14 @@ int run_polymutt_sharded(const Options& opt, const Pedigree& ped, SiteEvaluator&
     auto flush = [&]() {
       if (B.n == 0) return;
       int rows = 0;
-      eval.run(B.n, B.pl.data(), B.dm.data(), B.ref.data(), B.res.data(), B.calls.data(), &rows);
+      eval.run(B.n, B.pl, B.dm, B.ref, B.res, B.calls, &rows);
       for (int i = 0; i < B.n; i++) {
         const pm_site_result& r = B.res[i];
         if (!r.emit) continue;
         n_out++;
-        const uint8_t* pl = B.pl.data() + (size_t)i * np * 10;
-        const uint32_t* dm = B.dm.data() + (size_t)i * np;
-        W.output(label, B.pos[i], B.ref[i], r, r.call_row >= 0 ? B.calls.data() + (size_t)r.call_row * np : nullptr, pl, dm);
+        const uint8_t* pl = B.pl + (size_t)i * np * 10;
+        const uint32_t* dm = B.dm + (size_t)i * np;
+        W.output(label, B.pos[i], B.ref[i], r, r.call_row >= 0 ? B.calls + (size_t)r.call_row * np : nullptr, pl, dm);
         if (r.emit != 1) continue;
         if (n_rec++ == 0) {   // the shard's first record: keep its site for a possible re-run
           first_end = ftell(fh);
@@ -312,7 +336,7 @@ int run_polymutt_sharded(const Options& opt, const Pedigree& ped, SiteEvaluator&
         B.ref[i] = wref[k];
         rowOf[k] = i;
       }
-      src.fill(rowOf.data(), B.pl.data(), B.dm.data());
+      src.fill(rowOf.data(), B.pl, B.dm);
       if (B.n == B.cap) flush();
       if (past || src.ended()) break;
     }
@@ -434,7 +458,7 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, c
   if (!opt.blocksIn.empty()) {   // dense indexed blocks (blocks.h)
     auto* b = new BlockSiteSource;
     srcp.reset(b);
-    b->open(opt.blocksIn, (int)ped.column_pid.size());
+    b->open(opt.blocksIn, (int)ped.column_pid.size(), default_io_threads(opt));
   } else {   // PedigreeGLF with parallel decode (ingest.h)
     auto* g = new ParallelSiteSource;
     srcp.reset(g);
@@ -457,8 +481,7 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, c
   printf("Analysis started on %s\n", ctime(&t0));
 
   const int np = (int)ped.column_pid.size();
-  Batch B;
-  B.init(opt.batch > 0 ? opt.batch : 4096, np);
+  Batch B;   // (the serial loop's buffer; the pipeline has its own pool)
   int out_cnt = 0;
   size_t chrDone = 0;
   double t_ingest = 0, t_eval = 0, t_out = 0;   // PM_TIMING=1: host-side breakdown on stderr
@@ -473,22 +496,23 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, c
     return label == opt.chrX ? PM_CHR_X : label == opt.chrY ? PM_CHR_Y : label == opt.MT ? PM_CHR_MT : PM_CHR_AUTO;
   };
   if (!opt.force_call && !getenv("PM_SERIAL")) {
-    // Three stages: ingest (producer thread: GLF decode + merge, or block reads, into
-    // batch buffers) -> engine (this thread: one pm_engine_run per batch, in order) -> VCF writer thread
-    // (the batch's records, then the section summary).  Three batch buffers rotate, so the ingest of batch
-    // k+1 and the formatting of batch k-1 overlap the engine on batch k.  Output order is the serial one.
+    // Three stages: ingest (producer thread: GLF decode + merge, or parallel block reads,
+    // into page-locked batch buffers) -> engine (this thread: batches submitted in order to the evaluator, which
+    // keeps up to in_flight() of them running on separate engines / HIP streams, and collected in order) -> VCF
+    // writer thread (the batch's records formatted in parallel and written in order, then the section summary).
+    // in_flight() + 3 batch buffers rotate, so the ingest of later batches, the copies and kernels of several
+    // batches and the formatting of earlier ones overlap.  Output order is the serial one.
     // (--pos runs stop after the listed sites, main.cpp:593; they take the serial loop below.)
     enum { M_SECTION, M_BATCH, M_END, M_DONE };
     struct Msg { int kind; Batch* b; std::string label; int chrom; int entries; pm_counters C; };
-    const int cap = B.cap;
+    const int cap = opt.batch > 0 ? opt.batch : 4096;
     std::vector<std::unique_ptr<Batch>> pool;
     Channel<Batch*> freeq;
-    for (int i = 0; i < 3; i++) {
+    for (int i = 0; i < 3 + std::max(1, eval.in_flight()); i++) {
       pool.emplace_back(new Batch);
-      pool.back()->init(cap, np);
+      pool.back()->init(eval, cap, np);
       freeq.push(pool.back().get());
     }
-    B = Batch();   // the serial path's buffer is not used
     Channel<Msg> toEngine, toWriter;
     std::atomic<bool> abort{false};
     std::exception_ptr perr, eerr, werr;
@@ -518,7 +542,7 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, c
               b->ref[i] = wref[k];
               rowOf[k] = i;
             }
-            src.fill(rowOf.data(), b->pl.data(), b->dm.data());
+            src.fill(rowOf.data(), b->pl, b->dm);
             t_ingest += now_s() - ti;
             if (b->n == b->cap) {
               toEngine.push({M_BATCH, b, label, chrom, 0, {}});
@@ -537,6 +561,10 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, c
       toEngine.push({M_DONE, nullptr, "", 0, 0, {}});
     });
     std::thread writer([&] {
+      // a batch's records are formatted in parallel (VcfWriter::format) into per-chunk buffers, then written in order
+      TaskPool fmt_pool(default_io_threads(opt));
+      std::vector<std::string> chunks;
+      std::vector<int> recs;
       for (;;) {
         Msg m = toWriter.pop();
         if (m.kind == M_DONE) break;
@@ -545,12 +573,29 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, c
             const double t1 = now_s();
             W.chrom = m.chrom;
             const Batch& b = *m.b;
+            recs.clear();
+            bool any = false;
             for (int i = 0; i < b.n; i++) {
-              const pm_site_result& r = b.res[i];
-              if (!r.emit) continue;
-              W.output(m.label, b.pos[i], b.ref[i], r, r.call_row >= 0 ? b.calls.data() + (size_t)r.call_row * np : nullptr,
-                       b.pl.data() + (size_t)i * np * 10, b.dm.data() + (size_t)i * np);
+              any = any || b.res[i].emit != 0;   // (a suppressed de novo record writes the header too, :1868)
+              if (b.res[i].emit == 1) recs.push_back(i);
             }
+            if (any && !W.header_written) W.header();
+            const int nc = std::min((int)recs.size(), 4 * fmt_pool.threads());
+            if ((int)chunks.size() < nc) chunks.resize(nc);
+            auto format_chunk = [&](int c) {
+              std::string& out = chunks[c];
+              out.clear();
+              for (size_t k = (size_t)c * recs.size() / nc; k < (size_t)(c + 1) * recs.size() / nc; k++) {
+                const int i = recs[k];
+                const pm_site_result& r = b.res[i];
+                W.format(out, m.label, b.pos[i], b.ref[i], r, b.calls + (size_t)r.call_row * np, b.pl + (size_t)i * np * 10,
+                         b.dm + (size_t)i * np);
+              }
+            };
+            if (nc > 1) fmt_pool.run(nc, format_chunk);
+            else if (nc == 1) format_chunk(0);
+            for (int c = 0; c < nc; c++) fwrite(chunks[c].data(), 1, chunks[c].size(), vcf);
+            if (nc) fflush(vcf);
             t_out += now_s() - t1;
           } else if (m.kind == M_END && !werr) {
             print_summary(m.label, m.entries, m.C, t0);
@@ -563,9 +608,31 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, c
         if (m.kind == M_BATCH) freeq.push(m.b);
       }
     });
+    std::deque<Msg> inflight;   // submitted, not yet collected (submission order)
+    auto retire = [&]() {       // collect the oldest batch and hand it to the writer
+      Msg m = std::move(inflight.front());
+      inflight.pop_front();
+      const double te = now_s();
+      try {
+        m.b->rows = eval.collect();
+      } catch (...) {
+        freeq.push(m.b);
+        throw;
+      }
+      t_eval += now_s() - te;
+      toWriter.push(std::move(m));
+    };
     for (;;) {   // engine stage
       Msg m = toEngine.pop();
       if (m.kind == M_DONE) {
+        try {
+          while (!inflight.empty() && !eerr) retire();
+        } catch (...) {
+          eerr = std::current_exception();
+          abort = true;
+        }
+        for (auto& x : inflight) freeq.push(x.b);
+        inflight.clear();
         toWriter.push(m);
         break;
       }
@@ -574,15 +641,18 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, c
         continue;
       }
       try {
-        if (m.kind == M_SECTION) eval.begin_section(m.chrom);
-        else if (m.kind == M_BATCH) {
-          int rows = 0;
+        if (m.kind == M_SECTION) {
+          while (!inflight.empty()) retire();
+          eval.begin_section(m.chrom);
+        } else if (m.kind == M_BATCH) {
+          while (!inflight.empty() && (int)inflight.size() >= eval.in_flight()) retire();
           const double te = now_s();
           Batch& b = *m.b;
-          eval.run(b.n, b.pl.data(), b.dm.data(), b.ref.data(), b.res.data(), b.calls.data(), &rows);
+          eval.submit(b.n, b.pl, b.dm, b.ref, b.res, b.calls);
           t_eval += now_s() - te;
-          toWriter.push(m);
+          inflight.push_back(std::move(m));
         } else if (m.kind == M_END) {
+          while (!inflight.empty()) retire();
           eval.counters(&m.C);
           toWriter.push(m);
         }
@@ -590,6 +660,8 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, c
         eerr = std::current_exception();
         abort = true;
         if (m.kind == M_BATCH) freeq.push(m.b);
+        for (auto& x : inflight) freeq.push(x.b);
+        inflight.clear();
       }
     }
     producer.join();
@@ -600,6 +672,7 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, c
     return 0;
   }
 
+  B.init(eval, opt.batch > 0 ? opt.batch : 4096, np);
   while (src.nextSection()) {
     if (!chrSel.empty() && chrDone >= chrSelCount) break;
     const std::string label = src.label();
@@ -615,14 +688,14 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, c
       if (B.n == 0) return;
       int rows = 0;
       const double t0 = now_s();
-      eval.run(B.n, B.pl.data(), B.dm.data(), B.ref.data(), B.res.data(), B.calls.data(), &rows);
+      eval.run(B.n, B.pl, B.dm, B.ref, B.res, B.calls, &rows);
       const double t1 = now_s();
       t_eval += t1 - t0;
       for (int i = 0; i < B.n && !stop; i++) {
         const pm_site_result& r = B.res[i];
         if (!r.emit) continue;
-        W.output(label, B.pos[i], B.ref[i], r, r.call_row >= 0 ? B.calls.data() + (size_t)r.call_row * np : nullptr, B.pl.data() + (size_t)i * np * 10,
-                 B.dm.data() + (size_t)i * np);
+        W.output(label, B.pos[i], B.ref[i], r, r.call_row >= 0 ? B.calls + (size_t)r.call_row * np : nullptr, B.pl + (size_t)i * np * 10,
+                 B.dm + (size_t)i * np);
         out_cnt++;
         if (opt.force_call && out_cnt >= (int)positionMap.size()) stop = true;   // main.cpp:593 returns without a summary
       }
@@ -648,7 +721,7 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, c
         B.ref[i] = wref[s];
         rowOf[s] = i;
       }
-      src.fill(rowOf.data(), B.pl.data(), B.dm.data());
+      src.fill(rowOf.data(), B.pl, B.dm);
       t_ingest += now_s() - ti;
       if (B.n == B.cap) flush();
       if (stop || src.ended()) break;

@@ -21,6 +21,7 @@ struct Options {
   std::string numerics = "poly";
   double denovo_rate = 1.5e-08, denovo_tstv = 2.0, denovo_llr = 0.01;
   int device = 0, batch = 4096;
+  int engines = 2;      // --engines: engine instances (HIP streams) with a batch in flight each (pipelined CLI)
   int io_threads = 0;   // GLF decode threads (0: min(16, hardware threads))
   std::string blocksIn, blocksOut;   // --in_blocks FILE (.pmb input in place of -g), --glf2blocks FILE (convert)
   int blockSites = 4096;
@@ -42,6 +43,26 @@ class SiteEvaluator {
   virtual void counters(pm_counters* out) = 0;
   // famlk[0]'s stale posterior state at a shard start (pm_engine_set_posterior_carry)
   virtual void set_posterior_carry(bool seen) = 0;
+  // Batches in flight (the pipelined CLI): submit() starts a batch -- res / calls are filled by the matching
+  // collect(), which returns its row count; batches are collected in submission order, and at most in_flight()
+  // are outstanding.  The default runs the batch inside submit().
+  virtual int in_flight() const { return 1; }
+  virtual void submit(int n, const uint8_t* pl, const uint32_t* dm, const uint8_t* ref, pm_site_result* res, pm_geno_call* calls) {
+    int rows = 0;
+    run(n, pl, dm, ref, res, calls, &rows);
+    done_.push_back(rows);
+  }
+  virtual int collect() {
+    const int rows = done_.front();
+    done_.erase(done_.begin());
+    return rows;
+  }
+  // Host memory for the batch buffers (the engine: page-locked, for asynchronous copies)
+  virtual void* host_alloc(size_t bytes);
+  virtual void host_free(void* p);
+
+ private:
+  std::vector<int> done_;
 };
 
 // A run split over processes (one per GPU; polymutt_amd/launch.py): rank `rank` of `world` analyses a

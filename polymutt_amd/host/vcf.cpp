@@ -46,9 +46,17 @@ void VcfWriter::output(const std::string& label, int pos1, int refBase, const pm
                        const uint8_t* pl, const uint32_t* dm) {
   if (!header_written) header();
   if (r.emit != 1) return;   // OutputVCF_denovo returns before the record when denovoLR < minLLR (:1868)
+  line_.clear();
+  format(line_, label, pos1, refBase, r, calls, pl, dm);
+  fwrite(line_.data(), 1, line_.size(), fh);
+  fflush(fh);
+}
+
+void VcfWriter::format(std::string& L, const std::string& label, int pos1, int refBase, const pm_site_result& r,
+                       const pm_geno_call* calls, const uint8_t* pl, const uint32_t* dm) const {
   const int n = (int)ped->column_pid.size();
   const bool refIsA1 = refBase == r.allele1;
-  char info[512];
+  char info[512], head[1024];
   std::string alt;
   auto label_of = [&](const pm_geno_call& c) -> const char* {
     switch (c.label) {
@@ -79,11 +87,13 @@ void VcfWriter::output(const std::string& label, int pos1, int refBase, const pm
     if (r.is_mono) { INFO += ";BA="; INFO += kBases[r.allele2]; }
     if (refIsA1) alt = std::string(1, kBases[r.is_mono ? r.allele1 : r.allele2]);
     else alt = std::string(1, kBases[r.allele1]) + "," + kBases[r.allele2];
-    fprintf(fh, "%s\t%d\t%s\t%c\t%s\t%d\t%s\t%s\t%s", label.c_str(), pos1, ".", kBases[refBase], alt.c_str(), int(r.poly_qual + 0.5), ".",
-            INFO.c_str(), gl_off ? "GT:GQ:DP:DS" : "GT:GQ:DP:DS:PL");
+    L += label;   // (the label and INFO appended whole: no length limit)
+    snprintf(head, sizeof(head), "\t%d\t%s\t%c\t%s\t%d\t%s\t", pos1, ".", kBases[refBase], alt.c_str(), int(r.poly_qual + 0.5), ".");
+    L += head;
+    L += INFO;
+    L += gl_off ? "\tGT:GQ:DP:DS" : "\tGT:GQ:DP:DS:PL";
     const int g11 = GI(r.allele1, r.allele1), g12 = GI(r.allele1, r.allele2), g22 = GI(r.allele2, r.allele2);
-    std::string& L = line_;   // "\t%s:%d:%d:%.2f[:%u,%u,%u]" per person, formatted without stdio
-    L.clear();
+    // "\t%s:%d:%d:%.2f[:%u,%u,%u]" per person, formatted without stdio
     for (int p = 0; p < n; p++) {
       const pm_geno_call& c = calls[p];
       L.push_back('\t');
@@ -101,8 +111,6 @@ void VcfWriter::output(const std::string& label, int pos1, int refBase, const pm
       }
     }
     L.push_back('\n');
-    fwrite(L.data(), 1, L.size(), fh);
-    fflush(fh);
   } else {
     const int a2 = r.denovo_mono ? r.allele1 : r.allele2;
     if (singleNuclear())
@@ -113,10 +121,10 @@ void VcfWriter::output(const std::string& label, int pos1, int refBase, const pm
                r.avg_map_qual, r.af, r.denovo_lr);
     if (refIsA1) alt = std::string(1, kBases[a2]);
     else alt = std::string(1, kBases[r.allele1]) + "," + kBases[a2];
-    fprintf(fh, "%s\t%d\t%s\t%c\t%s\t%d\t%s\t%s\t%s", label.c_str(), pos1, ".", kBases[refBase], alt.c_str(), int(r.poly_qual + 0.5), ".", info,
-            gl_off ? "GT:GQ:DP" : "GT:GQ:DP:PL");
-    std::string& L = line_;
-    L.clear();
+    L += label;
+    snprintf(head, sizeof(head), "\t%d\t%s\t%c\t%s\t%d\t%s\t%s\t%s", pos1, ".", kBases[refBase], alt.c_str(), int(r.poly_qual + 0.5), ".",
+             info, gl_off ? "GT:GQ:DP" : "GT:GQ:DP:PL");
+    L += head;
     for (int p = 0; p < n; p++) {
       const pm_geno_call& c = calls[p];
       L.push_back('\t');
@@ -132,8 +140,6 @@ void VcfWriter::output(const std::string& label, int pos1, int refBase, const pm
       }
     }
     L.push_back('\n');
-    fwrite(L.data(), 1, L.size(), fh);
-    fflush(fh);
   }
 }
 

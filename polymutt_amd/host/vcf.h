@@ -23,6 +23,10 @@ struct VcfWriter {
   void output(const std::string& label, int pos1, int refBase, const pm_site_result& r, const pm_geno_call* calls,
               const uint8_t* pl, const uint32_t* dm);
   void header();   // written by output() on first use; a sharded run's lead writes it once at the merge
+  // The record text of an emitted site (r.emit == 1) appended to `out`, as output() writes it (no header, no I/O;
+  // safe to call from several threads at once: the pipelined CLI formats a batch's records in parallel)
+  void format(std::string& out, const std::string& label, int pos1, int refBase, const pm_site_result& r,
+              const pm_geno_call* calls, const uint8_t* pl, const uint32_t* dm) const;
 
  private:
   bool singleNuclear() const;

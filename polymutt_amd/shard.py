@@ -25,7 +25,7 @@ def allreduce_counters(counters, device=None):
     import torch
     import torch.distributed as dist
     t = torch.as_tensor(np.asarray(counters, dtype=np.int64).copy(), device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_available() and dist.is_initialized():   # (also at one rank: an RCCL group of one still runs it)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return t.cpu().numpy()
 
@@ -35,6 +35,6 @@ def max_over_ranks(value, device=None):
     import torch
     import torch.distributed as dist
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_available() and dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

@@ -4,6 +4,9 @@
 #pragma once
 #include <cstdio>
 #include <cstdlib>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 #include "../../oracle/pm_oracle.h"
 #include "../../polymutt_amd/host/driver.h"
 
@@ -31,7 +34,12 @@ class OracleEvaluator : public pmhost::SiteEvaluator {
 };
 
 inline pmhost::EvaluatorFactory oracle_factory() {
-  return [](const pm_pedigree& v, const pm_params& par, const pmhost::Options&) {
+  return [](const pm_pedigree& v, const pm_params& par, const pmhost::Options& opt) {
+#ifdef _OPENMP
+    if (opt.nthreads > 0) omp_set_num_threads(opt.nthreads);   // main.cpp:156 (default 1, :72)
+#else
+    (void)opt;
+#endif
     return std::unique_ptr<pmhost::SiteEvaluator>(new OracleEvaluator(v, par));
   };
 }

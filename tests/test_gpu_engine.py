@@ -2,6 +2,7 @@
 golden VCFs.  Marked gpu; run on an MI355X with `pytest -m gpu`."""
 import os
 import subprocess
+import sys
 
 import ctypes as C
 
@@ -169,7 +170,7 @@ def test_quad_plan_matches_oracle(built, tmp_path, monkeypatch, nfam, nsites):
     against the oracle too.  300 / 600 families end in a partial slot row (phantom families), 512 / 1024 fill the
     64 x 8 / 64 x 16 plans exactly; planted de novo kids give cfg-7 items as well.  On the QUAD plan the de novo
     monomorphism likelihood (cfg 0) comes from the cfg-1 items' hoisted f^4 coefficients; PM_MONO_DN_PREP=1 forms
-    it in k_prep from all ten planes instead: both against the oracle, and within 1e-13 of each other."""
+    it in k_prep from all ten planes instead: both against the oracle, and within 1e-12 (relative; 1e-13 absolute) of each other."""
     d = str(tmp_path / "qd")
     pm.synth_write_dataset(d, "quad+dn", nfam, nsites, 17)
     ped = pm.Pedigree(os.path.join(d, "test.dat"), os.path.join(d, "test.ped"))
@@ -191,7 +192,7 @@ def test_quad_plan_matches_oracle(built, tmp_path, monkeypatch, nfam, nsites):
             monkeypatch.delenv(env)
     a, b = got[""], got["PM_MONO_DN_PREP"]
     called = a["status"] == 0   # PM_SITE_CALLED
-    np.testing.assert_allclose(a["varllk"][called, 0], b["varllk"][called, 0], rtol=1e-13, atol=0)
+    np.testing.assert_allclose(a["varllk"][called, 0], b["varllk"][called, 0], rtol=1e-12, atol=1e-13)
 
 
 @pytest.mark.parametrize("numerics", [pm.NUM_PRODUCT, pm.NUM_POLY])
@@ -364,3 +365,57 @@ def test_headline_full_batch_properties(built, denovo):
     if not denovo:   # records: the polymorphic calls past the posterior cutoff, one per ts / tv / other count
         assert (r_big["maxidx"][emitted] >= 1).all()
         assert int(emitted.sum()) == int(c_big[10:15].sum())
+
+
+def test_bench_rccl_group_of_one(built):
+    """bench.py --rccl on the one GPU of the box: the RCCL ("nccl") process group is initialised at one rank and the
+    section counters' all-reduce, the barriers and the max-over-ranks timing run through it on the device -- the
+    collective path of the multi-GPU bench (src/main.cpp:264-282's summary), exercised without a second GPU."""
+    import json
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--rccl", "--steps", "3", "--warmup", "1",
+                        "--batch", "8192", "--calib-steps", "1", "--no-cpu-baseline"], capture_output=True, text=True,
+                       timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    print("collective_backend:", line["collective_backend"], "rccl_world:", line["rccl_world"])
+    assert line["collective_backend"] == "nccl" and line["rccl_world"] == 1
+    assert line["counters"]["sites"] == 3 * 8192 and line["value"] > 0
+
+
+@pytest.mark.parametrize("engines,batch", [(1, 4096), (3, 1000), (2, 257)])
+def test_cli_pipelined_engines_reproduce_golden(built, tmp_path, engines, batch):
+    """The pipelined CLI with several engines in flight (pm_engine_submit / pm_engine_collect on separate HIP streams,
+    page-locked batch buffers, records formatted in parallel and written in order) reproduces the reference's
+    example goldens for any engine count and batch size (81 016 sites: 20-316 batches), plain and --denovo."""
+    for args, golden in [(["-p", "test.ped", "-d", "test.dat", "-g", "test.gif", "-c", "0.9", "--minDepth", "150",
+                           "--maxDepth", "200"], "test.out.vcf.body.gz"),
+                         (["-p", "test.ped", "-d", "test.dat", "-g", "test.gif", "--denovo", "--rate_denovo", "1.5e-07"],
+                          "test.denovo.out.vcf")]:
+        out = tmp_path / "out.vcf"
+        r = subprocess.run([pm.BIN_PATH] + args + ["--out_vcf", str(out), "--engines", str(engines), "--batch", str(batch)],
+                           cwd=EXAMPLE, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        got = [l for l in out.read_text().splitlines() if not l.startswith("##")]
+        assert got == _golden_body(golden), golden
+
+
+def test_engine_submit_collect_matches_run(built):
+    """pm_engine_submit / pm_engine_collect with two engines' batches in flight at once give the same bytes as
+    pm_engine_run, batch by batch (the CLI's pipelined engine stage)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    ped = bench.nuclear_pedigree(pm, 300, 2)
+    pl, dm, ref = pm.synth_block_host(ped, 1024, 5)
+    for denovo in (0, 1):
+        params = pm.Params.defaults(denovo=denovo)
+        engs = [pm.Engine(ped, params, max_batch=512) for _ in range(2)]
+        want = [engs[0].run(pl[k * 512:(k + 1) * 512], dm[k * 512:(k + 1) * 512], ref[k * 512:(k + 1) * 512]) for k in range(2)]
+        for k in range(2):
+            engs[k].begin_section(pm.PM_CHR_AUTO)
+            engs[k].submit(pl[k * 512:(k + 1) * 512], dm[k * 512:(k + 1) * 512], ref[k * 512:(k + 1) * 512])
+        got = [engs[k].collect() for k in range(2)]
+        for (a, ac), (b, bc) in zip(got, want):
+            assert a.tobytes() == b.tobytes() and ac.tobytes() == bc.tobytes()
+        for e in engs:
+            e.close()

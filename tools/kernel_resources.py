@@ -61,9 +61,9 @@ def kernels(co):
 
 
 def main():
-    lib = sys.argv[1] if len(sys.argv) > 1 and sys.argv[1].endswith(".so") else \
+    lib = sys.argv[1] if len(sys.argv) > 1 and sys.argv[1].endswith((".so", ".o")) else \
         os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "polymutt_amd", "lib", "libpolymutt.so")
-    pats = [a for a in sys.argv[1:] if not a.endswith(".so")]
+    pats = [a for a in sys.argv[1:] if not a.endswith((".so", ".o"))]
     demangle = "c++filt"
     for co in code_objects(lib):
         for r in kernels(co):
