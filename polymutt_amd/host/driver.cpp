@@ -203,12 +203,16 @@ struct Batch {
     dm = (uint32_t*)e.host_alloc((size_t)cap * np * 4);
     ref = (uint8_t*)e.host_alloc((size_t)cap);
     res = (pm_site_result*)e.host_alloc(sizeof(pm_site_result) * (size_t)cap);
-    calls = (pm_geno_call*)e.host_alloc(sizeof(pm_geno_call) * (size_t)cap * np);
+    // (the genotype rows: pageable -- only the emitted rows are copied back, and pinning cap x n_person x 16 B per
+    // batch would dominate start-up; malloc'd pages are touched only as rows arrive)
+    calls = (pm_geno_call*)malloc(sizeof(pm_geno_call) * (size_t)cap * np);
+    if (!calls) throw FatalError("out of host memory\n");
     pos.assign(cap, 0);
   }
   void release() {
     if (!ev) return;
-    for (void* p : {(void*)pl, (void*)dm, (void*)ref, (void*)res, (void*)calls}) ev->host_free(p);
+    for (void* p : {(void*)pl, (void*)dm, (void*)ref, (void*)res}) ev->host_free(p);
+    free(calls);
     pl = ref = nullptr; dm = nullptr; res = nullptr; calls = nullptr; ev = nullptr;
   }
 };

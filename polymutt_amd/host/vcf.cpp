@@ -93,24 +93,28 @@ void VcfWriter::format(std::string& L, const std::string& label, int pos1, int r
     L += INFO;
     L += gl_off ? "\tGT:GQ:DP:DS" : "\tGT:GQ:DP:DS:PL";
     const int g11 = GI(r.allele1, r.allele1), g12 = GI(r.allele1, r.allele2), g22 = GI(r.allele2, r.allele2);
-    // "\t%s:%d:%d:%.2f[:%u,%u,%u]" per person, formatted without stdio
+    // "\t%s:%d:%d:%.2f[:%u,%u,%u]" per person, formatted without stdio into reserved room (<= 96 chars a person)
+    const size_t at = L.size();
+    L.resize(at + (size_t)n * 96 + 2);
+    char* o = &L[at];
     for (int p = 0; p < n; p++) {
       const pm_geno_call& c = calls[p];
-      L.push_back('\t');
-      L += label_of(c);
-      L.push_back(':');
-      fmt_int(L, (int)c.gq);
-      L.push_back(':');
-      fmt_int(L, (int)(dm[p] & 0xFFFFFF));
-      L.push_back(':');
-      fmt_fixed(L, c.dosage, 2);
+      *o++ = '\t';
+      put_str(o, label_of(c));
+      *o++ = ':';
+      put_int(o, (int)c.gq);
+      *o++ = ':';
+      put_uint(o, dm[p] & 0xFFFFFF);
+      *o++ = ':';
+      put_fixed2(o, c.dosage);
       if (!gl_off) {
-        L.push_back(':'); fmt_uint(L, pl[p * 10 + g11]);
-        L.push_back(','); fmt_uint(L, pl[p * 10 + g12]);
-        L.push_back(','); fmt_uint(L, pl[p * 10 + g22]);
+        *o++ = ':'; put_uint(o, pl[p * 10 + g11]);
+        *o++ = ','; put_uint(o, pl[p * 10 + g12]);
+        *o++ = ','; put_uint(o, pl[p * 10 + g22]);
       }
     }
-    L.push_back('\n');
+    *o++ = '\n';
+    L.resize(o - L.data());
   } else {
     const int a2 = r.denovo_mono ? r.allele1 : r.allele2;
     if (singleNuclear())
@@ -125,21 +129,25 @@ void VcfWriter::format(std::string& L, const std::string& label, int pos1, int r
     snprintf(head, sizeof(head), "\t%d\t%s\t%c\t%s\t%d\t%s\t%s\t%s", pos1, ".", kBases[refBase], alt.c_str(), int(r.poly_qual + 0.5), ".",
              info, gl_off ? "GT:GQ:DP" : "GT:GQ:DP:PL");
     L += head;
+    const size_t at = L.size();
+    L.resize(at + (size_t)n * 96 + 2);
+    char* o = &L[at];
     for (int p = 0; p < n; p++) {
       const pm_geno_call& c = calls[p];
-      L.push_back('\t');
-      L += label_of(c);
-      L.push_back(':');
-      fmt_int(L, (int)c.gq);
-      L.push_back(':');
-      fmt_int(L, (int)(dm[p] & 0xFFFFFF));
+      *o++ = '\t';
+      put_str(o, label_of(c));
+      *o++ = ':';
+      put_int(o, (int)c.gq);
+      *o++ = ':';
+      put_uint(o, dm[p] & 0xFFFFFF);
       if (!gl_off) {
-        L.push_back(':');
-        for (int g = 0; g < 9; g++) { fmt_uint(L, pl[p * 10 + g]); L.push_back(','); }
-        fmt_uint(L, pl[p * 10 + 9]);
+        *o++ = ':';
+        for (int g = 0; g < 9; g++) { put_uint(o, pl[p * 10 + g]); *o++ = ','; }
+        put_uint(o, pl[p * 10 + 9]);
       }
     }
-    L.push_back('\n');
+    *o++ = '\n';
+    L.resize(o - L.data());
   }
 }
 

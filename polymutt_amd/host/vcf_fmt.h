@@ -64,4 +64,39 @@ inline void fmt_fixed(std::string& out, double v, int prec) {
   }
 }
 
+// Raw-pointer variants for the per-genotype columns (the caller reserves the room: at most 20 chars per integer)
+inline void put_uint(char*& o, uint32_t v) {
+  if (v < 10) { *o++ = char('0' + v); return; }
+  if (v < 100) { *o++ = char('0' + v / 10); *o++ = char('0' + v % 10); return; }
+  char b[12];
+  int n = 0;
+  do { b[n++] = char('0' + v % 10); v /= 10; } while (v);
+  while (n) *o++ = b[--n];
+}
+inline void put_int(char*& o, int32_t v) {
+  if (v < 0) { *o++ = '-'; put_uint(o, (uint32_t)(-(int64_t)v)); }
+  else put_uint(o, (uint32_t)v);
+}
+inline void put_str(char*& o, const char* s) { while (*s) *o++ = *s++; }
+
+// printf("%.2f", v): the double product v * 100 is within ~1e-14 relative of the exact one, so unless its fraction
+// lies within 1e-7 of one half (where the exact binary value decides, ties to even) rounding it gives printf's
+// digits; those near-ties, and values outside [0, 1e6), take fmt_fixed's exact path.
+inline void put_fixed2(char*& o, double v) {
+  if (!std::signbit(v) && v < 1e6) {   // (-0.0 prints "-0.00"; q < 1e8: its rounding error < 2.3e-8, below the margin)
+    const double q = v * 100.0, fl = std::floor(q), fr = q - fl;
+    if (std::fabs(fr - 0.5) > 1e-7) {
+      const uint64_t r = (uint64_t)fl + (fr > 0.5 ? 1 : 0);
+      put_uint(o, (uint32_t)(r / 100));
+      *o++ = '.';
+      const uint32_t c = (uint32_t)(r % 100);
+      *o++ = char('0' + c / 10); *o++ = char('0' + c % 10);
+      return;
+    }
+  }
+  std::string t;
+  fmt_fixed(t, v, 2);
+  for (char c : t) *o++ = c;
+}
+
 }  // namespace pmhost

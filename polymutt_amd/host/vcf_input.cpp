@@ -12,7 +12,10 @@
 #include <cstring>
 #include <map>
 #include <string>
+#include <thread>
 #include <vector>
+#include "ingest.h"
+#include "vcf_fmt.h"
 
 namespace pmhost {
 namespace {
@@ -252,33 +255,40 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
   State st;
   st.calls.assign(np, pm_geno_call{0.0, 0, 0, PM_LBL_VCF_DIPLOID, {0, 0, 0}});
 
-  auto write_record = [&](FILE* fo, const Pending& r, bool fresh, const pm_site_result* Rs, const pm_geno_call* C) {
-    if (fresh) {   // mono/poly -> QUAL (PedVCF.cpp:136-152), with the reference's operator-precedence slip
-      const double mono = Rs->varllk[0], poly = Rs->varllk[1];
-      double llk_alt, llk_ref;
-      if (!r.indel) {
-        llk_alt = log10((prior * (is_ts(r.a1, r.a2) ? 1 : 0)) ? prior_ts : prior_tv) + poly;
-        llk_ref = log10(1 - prior) + mono;
-      } else {
-        llk_alt = log10(prior) + poly;
-        llk_ref = log10(1 - prior) + mono;
-      }
-      if (llk_alt - llk_ref > 10) st.qual = 10.0 * (llk_alt - llk_ref);
-      else {
-        const double posterior = 1 / (1 + pow(10, llk_ref - llk_alt));
-        st.qual = -10 * log10(1 - posterior);
-      }
-      st.min = Rs->af;
-      for (int p = 0; p < np; p++) st.calls[p] = C[p];
+  // The state a record is printed with: its own (a computed record) or the previous computed record's (a record
+  // without data, PedVCF.cpp:113-122): QUAL, the AF minimiser and every person's call.
+  struct RecState { double qual, min; const pm_geno_call* calls; };
+  auto fresh_state = [&](const Pending& r, const pm_site_result* Rs, const pm_geno_call* C) {
+    // mono/poly -> QUAL (PedVCF.cpp:136-152), with the reference's operator-precedence slip
+    const double mono = Rs->varllk[0], poly = Rs->varllk[1];
+    double llk_alt, llk_ref;
+    if (!r.indel) {
+      llk_alt = log10((prior * (is_ts(r.a1, r.a2) ? 1 : 0)) ? prior_ts : prior_tv) + poly;
+      llk_ref = log10(1 - prior) + mono;
+    } else {
+      llk_alt = log10(prior) + poly;
+      llk_ref = log10(1 - prior) + mono;
     }
-    // OutputVCF (FamilyLikelihoodSeq_VCF.cpp:412-521)
+    RecState S;
+    if (llk_alt - llk_ref > 10) S.qual = 10.0 * (llk_alt - llk_ref);
+    else {
+      const double posterior = 1 / (1 + pow(10, llk_ref - llk_alt));
+      S.qual = -10 * log10(1 - posterior);
+    }
+    S.min = Rs->af;
+    S.calls = C;
+    return S;
+  };
+  // OutputVCF (FamilyLikelihoodSeq_VCF.cpp:412-521): one record's text appended to `out` (no shared state: the
+  // records of a batch are formatted in parallel)
+  auto format_record = [&](std::string& out, const Pending& r, const RecState& S) {
     const std::string& L = r.line;
     int AC = 0, totalDepth = 0;
     bool missing = false;
     Span f;
     for (size_t i = 0; i < samples.size(); i++) {
       if (col_person[i] < 0) continue;
-      AC += st.calls[col_person[i]].best;
+      AC += S.calls[col_person[i]].best;
       int dp = 0;
       if (r.dp_idx > 0) {
         missing = get_field(L, r.cols[9 + i], r.dp_idx, f);
@@ -288,33 +298,64 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
       totalDepth += dp;
     }
     auto fld = [&](int k) { return L.substr(r.cols[k].b, r.cols[k].e - r.cols[k].b); };
-    fprintf(fo, "%s\t%s\t%s\t%s\t%s\t%.2f\t%s\tAF=%.2f;AC=%d;DP=%d\t%s", fld(0).c_str(), fld(1).c_str(), fld(2).c_str(),
-            fld(3).c_str(), fld(4).c_str(), st.qual, fld(6).c_str(), 1 - st.min, AC, totalDepth,
-            fs.PL_idx > 0 ? "GT:GQ:DP:PL" : "GT:GQ:DP:GL");
+    char head[256];
+    out += fld(0); out += '\t'; out += fld(1); out += '\t'; out += fld(2); out += '\t'; out += fld(3); out += '\t';
+    out += fld(4);
+    snprintf(head, sizeof(head), "\t%.2f\t", S.qual);
+    out += head;
+    out += fld(6);
+    snprintf(head, sizeof(head), "\tAF=%.2f;AC=%d;DP=%d\t%s", 1 - S.min, AC, totalDepth, fs.PL_idx > 0 ? "GT:GQ:DP:PL" : "GT:GQ:DP:GL");
+    out += head;
     for (size_t i = 0; i < samples.size(); i++) {
       const int p = col_person[i];
       if (p < 0) continue;
-      const pm_geno_call& c = st.calls[p];
+      const pm_geno_call& c = S.calls[p];
       const std::string lab = label_text(c);
-      fprintf(fo, "\t%s:%d:", (c.gq > 0 || lab == ".") ? lab.c_str() : "./.", (int)c.gq);
-      std::string dps = ".";
+      out += '\t';
+      out += (c.gq > 0 || lab == ".") ? lab : std::string("./.");
+      out += ':';
+      fmt_int(out, (int)c.gq);
+      out += ':';
       if (r.dp_idx > 0) {
         missing = get_field(L, r.cols[9 + i], r.dp_idx, f);
-        if (!missing) dps = L.substr(f.b, f.e - f.b);
-      }
-      fprintf(fo, "%s:", missing ? "." : dps.c_str());
+        if (missing) out += '.';
+        else out.append(L, f.b, f.e - f.b);
+      } else out += missing ? "." : ".";
+      out += ':';
       missing = get_field(L, r.cols[9 + i], fs.PL_idx > 0 ? fs.PL_idx : fs.GL_idx, f);
-      fprintf(fo, "%s", missing ? "." : L.substr(f.b, f.e - f.b).c_str());
+      if (missing) out += '.';
+      else out.append(L, f.b, f.e - f.b);
     }
-    fprintf(fo, "\n");
+    out += '\n';
+  };
+  // the lead records of a shard, printed with the carried state, one at a time
+  auto write_record = [&](FILE* fo, const Pending& r) {
+    RecState S{st.qual, st.min, st.calls.data()};
+    std::string t;
+    format_record(t, r, S);
+    fwrite(t.data(), 1, t.size(), fo);
   };
 
+  TaskPool pool(std::max(1, std::min(16, opt.io_threads > 0 ? opt.io_threads : (int)std::thread::hardware_concurrency())));
+  std::vector<std::string> texts;
+  std::vector<RecState> states;
   auto flush = [&]() {
     int rows = 0;
     if (nb > 0) eval.run(nb, pl.data(), dm.data(), ref.data(), res.data(), calls.data(), &rows);
-    for (auto& r : pend) {
-      if (r.computed) write_record(out, r, true, &res[r.slot], calls.data() + (size_t)res[r.slot].call_row * np);
-      else write_record(out, r, false, nullptr, nullptr);
+    // the state each record prints with (sequential: a record without data takes the last computed one's)
+    states.resize(pend.size());
+    RecState cur{st.qual, st.min, st.calls.data()};
+    for (size_t k = 0; k < pend.size(); k++) {
+      const Pending& r = pend[k];
+      if (r.computed) cur = fresh_state(r, &res[r.slot], calls.data() + (size_t)res[r.slot].call_row * np);
+      states[k] = cur;
+    }
+    if (texts.size() < pend.size()) texts.resize(pend.size());
+    pool.run((int)pend.size(), [&](int k) { texts[k].clear(); format_record(texts[k], pend[k], states[k]); });
+    for (size_t k = 0; k < pend.size(); k++) fwrite(texts[k].data(), 1, texts[k].size(), out);
+    if (!pend.empty()) {   // the last state carries into the next batch
+      st.qual = cur.qual; st.min = cur.min;
+      if (cur.calls != st.calls.data()) std::copy(cur.calls, cur.calls + np, st.calls.begin());
     }
     pend.clear();
     nb = 0;
@@ -381,33 +422,25 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
     }
   }
 
-  Span f;
-  for (;;) {
-    if (in.tell() >= hi || !in.next(line)) break;
-    if (line.empty() || line[0] == '#') continue;
-    Pending r;
-    r.line.swap(line);
-    if (first)   // FillPenetrance on the first record (:270-282) ...
-      for (size_t i = 0; i < samples.size(); i++) {
-        if (col_person[i] < 0) { printf("Sample ID \"%s\" not included in the analysis!\n", samples[i].c_str()); continue; }
-        n_samples_with_data++;
-      }
-    const int kind = classify(r);
+  // Chunks of records: read and classified in order (the FORMAT bookkeeping carries from record to record), their
+  // PL / GL fields parsed in parallel into per-record rows, then handled in order as the reference does.
+  const int CH = 256;
+  std::vector<Pending> chunk(CH);
+  std::vector<int> kinds(CH), withdata(CH);
+  std::vector<std::string> perr(CH);
+  std::vector<uint8_t> rows((size_t)CH * np * 10);
+  // FillPenetrance's per-sample loop (:338-382) for record k of the chunk: phred bytes of (geno11, geno12, geno22)
+  auto parse_row = [&](int k) {
+    const Pending& r = chunk[k];
     const std::string& L = r.line;
-    auto fld = [&](int k) { return L.substr(r.cols[k].b, r.cols[k].e - r.cols[k].b); };
-    if (first) {   // ... then VarCallFromVCF's banner (:117)
-      printf("Total samples in both VCF and PED files: %d\n\n", n_samples_with_data);
-      first = false;
-    }
-    if (kind < 0) bad_allele++;
-    if (kind <= 0) continue;   // OutputVCF returns at once for these records (:419)
-
-    // penetrances / log-likelihoods of the record (:318-366) into a dense block row
-    const int slot = nb;
-    uint8_t* row = pl.data() + (size_t)slot * np * 10;
+    uint8_t* row = rows.data() + (size_t)k * np * 10;
     memset(row, 0, (size_t)np * 10);
     const int g0 = gi(r.a1, r.a1), g1 = gi(r.a1, r.a2), g2 = gi(r.a2, r.a2);
-    int withdata = 0;
+    const int gix[3] = {g0, g1, g2};
+    const bool isPL = fs.PL_idx > 0;
+    int wd = 0;
+    perr[k].clear();
+    Span f;
     for (size_t i = 0; i < samples.size(); i++) {
       const int p = col_person[i];
       if (p < 0) continue;
@@ -416,46 +449,90 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
       int nv = 0, b = f.b;
       for (int q = f.b; q <= f.e; q++)
         if (q == f.e || L[q] == ',') {
-          if (nv < 3) v[nv] = strtod(std::string(L, b, q - b).c_str(), nullptr);
+          if (nv < 3) {
+            // a plain decimal integer (the usual PL) without strtod; anything else through strtod as the reference's
+            // String::AsDouble
+            int d = 0, t = b;
+            bool plain = isPL && q > b && q - b <= 9;
+            for (; plain && t < q; t++) {
+              const char ch = L[t];
+              if (ch < '0' || ch > '9') plain = false;
+              else d = d * 10 + (ch - '0');
+            }
+            v[nv] = plain ? (double)d : strtod(std::string(L, b, q - b).c_str(), nullptr);
+          }
           nv++;
           b = q + 1;
         }
-      if (nv != 3)
-        throw FatalError("GL or PL filed does not have 3 values separated by commas at: " + fld(0) + " " + fld(1) + "!\n");
-      if (v[0] != 0.0 || v[1] != 0.0 || v[2] != 0.0) withdata++;
-      const int gix[3] = {g0, g1, g2};
-      for (int k = 0; k < 3; k++) {
-        const int phred = (int)(fs.PL_idx > 0 ? v[k] : -10 * v[k]);   // PL2LK(int(...)) (:361-363, :57-63)
-        if (phred < 0) throw FatalError("Phred-scaled likelihood " + std::to_string(phred) + " can not be negative\n");
-        row[(size_t)p * 10 + gix[k]] = (uint8_t)(phred > 255 ? 255 : phred);
+      if (nv != 3) {
+        perr[k] = "GL or PL filed does not have 3 values separated by commas at: " + L.substr(r.cols[0].b, r.cols[0].e - r.cols[0].b) +
+                  " " + L.substr(r.cols[1].b, r.cols[1].e - r.cols[1].b) + "!\n";
+        break;
       }
+      if (v[0] != 0.0 || v[1] != 0.0 || v[2] != 0.0) wd++;
+      bool bad = false;
+      for (int q = 0; q < 3; q++) {
+        const int phred = (int)(isPL ? v[q] : -10 * v[q]);   // PL2LK(int(...)) (:361-363, :57-63)
+        if (phred < 0) { perr[k] = "Phred-scaled likelihood " + std::to_string(phred) + " can not be negative\n"; bad = true; break; }
+        row[(size_t)p * 10 + gix[q]] = (uint8_t)(phred > 255 ? 255 : phred);
+      }
+      if (bad) break;
     }
-    // chromosome class of the record (PedVCF.cpp:121-124)
-    const std::string chrom = fld(0);
-    const int cls = chrom == opt.chrX ? PM_CHR_X : chrom == opt.chrY ? PM_CHR_Y : chrom == opt.MT ? PM_CHR_MT : PM_CHR_AUTO;
-    if (withdata == 0) {   // written with the previous record's QUAL / AF / genotypes (:113)
-      if (lead && !computed_any) {   // ... which an earlier rank computed: written after the exchange
-        fprintf(lead, "%d\t%s\n", r.dp_idx, r.line.c_str());   // (with its DP index snapshot)
-        n_lead++;
-      } else pend.push_back(std::move(r));
-      continue;
+    withdata[k] = wd;
+  };
+  bool eof = false;
+  while (!eof) {
+    int nc = 0;
+    while (nc < CH) {
+      if (in.tell() >= hi || !in.next(line)) { eof = true; break; }
+      if (line.empty() || line[0] == '#') continue;
+      Pending& r = chunk[nc];
+      r = Pending();
+      r.line.swap(line);
+      if (first)   // FillPenetrance on the first record (:270-282) ...
+        for (size_t i = 0; i < samples.size(); i++) {
+          if (col_person[i] < 0) { printf("Sample ID \"%s\" not included in the analysis!\n", samples[i].c_str()); continue; }
+          n_samples_with_data++;
+        }
+      kinds[nc] = classify(r);
+      if (first) {   // ... then VarCallFromVCF's banner (:117)
+        printf("Total samples in both VCF and PED files: %d\n\n", n_samples_with_data);
+        first = false;
+      }
+      nc++;
     }
-    computed_any = true;
-    if (cls != cur_chrom) {
-      if (nb > 0) {   // the row is already packed in `slot`; move it to slot 0 after the flush
-        std::vector<uint8_t> keep(row, row + (size_t)np * 10);
-        flush();
-        memcpy(pl.data(), keep.data(), keep.size());
-      } else if (!pend.empty()) flush();
-      eval.begin_section(cls);
-      cur_chrom = cls;
+    pool.run(nc, [&](int k) { if (kinds[k] > 0) parse_row(k); });
+    for (int k = 0; k < nc; k++) {
+      const int kind = kinds[k];
+      if (kind < 0) bad_allele++;
+      if (kind <= 0) continue;   // OutputVCF returns at once for these records (:419)
+      if (!perr[k].empty()) throw FatalError(perr[k]);
+      Pending& r = chunk[k];
+      const std::string& L = r.line;
+      // chromosome class of the record (PedVCF.cpp:121-124)
+      const std::string chrom = L.substr(r.cols[0].b, r.cols[0].e - r.cols[0].b);
+      const int cls = chrom == opt.chrX ? PM_CHR_X : chrom == opt.chrY ? PM_CHR_Y : chrom == opt.MT ? PM_CHR_MT : PM_CHR_AUTO;
+      if (withdata[k] == 0) {   // written with the previous record's QUAL / AF / genotypes (:113)
+        if (lead && !computed_any) {   // ... which an earlier rank computed: written after the exchange
+          fprintf(lead, "%d\t%s\n", r.dp_idx, r.line.c_str());   // (with its DP index snapshot)
+          n_lead++;
+        } else pend.push_back(std::move(r));
+        continue;
+      }
+      computed_any = true;
+      if (cls != cur_chrom) {
+        if (nb > 0 || !pend.empty()) flush();
+        eval.begin_section(cls);
+        cur_chrom = cls;
+      }
+      memcpy(pl.data() + (size_t)nb * np * 10, rows.data() + (size_t)k * np * 10, (size_t)np * 10);
+      r.computed = true;
+      r.slot = nb;
+      ref[nb] = (uint8_t)(r.a1 | (r.a2 << 4));
+      nb++;
+      pend.push_back(std::move(r));
+      if (nb == B) flush();
     }
-    r.computed = true;
-    r.slot = nb;
-    ref[nb] = (uint8_t)(r.a1 | (r.a2 << 4));
-    nb++;
-    pend.push_back(std::move(r));
-    if (nb == B) flush();
   }
   flush();
   if (!sharded) {
@@ -496,7 +573,7 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
       r.dp_idx = atoi(line.c_str());
       r.line.assign(line, tab + 1, std::string::npos);
       split(r.line, '\t', r.cols);
-      write_record(lo_out, r, false, nullptr, nullptr);
+      write_record(lo_out, r);
     }
     fclose(lo_out);
     remove(lead_in.c_str());

@@ -15,6 +15,12 @@ int main(int argc, char** argv) {
     pmhost::fmt_fixed(s, v, prec);
     snprintf(ref, sizeof(ref), "%.*f", prec, v);
     if (s != ref) { if (bad < 10) printf("MISMATCH %.17g prec %d: %s vs %s\n", v, prec, s.c_str(), ref); bad++; }
+    if (prec == 2) {   // the raw-pointer fast path of the genotype columns (put_fixed2)
+      char buf[128], *o = buf;
+      pmhost::put_fixed2(o, v);
+      *o = 0;
+      if (strcmp(buf, ref) != 0) { if (bad < 10) printf("MISMATCH put_fixed2 %.17g: %s vs %s\n", v, buf, ref); bad++; }
+    }
   };
   for (int k = -2000; k <= 2000; k++)   // exact decimal ties and their neighbours
     for (int prec = 0; prec <= 4; prec++) {
@@ -31,8 +37,17 @@ int main(int argc, char** argv) {
     check(v, 2);
     if (i % 7 == 0) check(-v, 2);
   }
+  std::uniform_real_distribution<double> wide(0.0, 2e6);
+  for (long i = 0; i < n / 4; i++) check(wide(rng), 2);   // (both sides of put_fixed2's fast-path range)
   std::string s;
   for (long v : {0L, 7L, 10L, 255L, 16777215L, -1L, -123456L}) { s.clear(); pmhost::fmt_int(s, v); snprintf(ref, sizeof(ref), "%ld", v); if (s != ref) bad++; }
+  for (long v : {0L, 7L, 10L, 99L, 100L, 255L, 16777215L, -1L, -123456L, 2147483647L}) {
+    char buf[32], *o = buf;
+    pmhost::put_int(o, (int32_t)v);
+    *o = 0;
+    snprintf(ref, sizeof(ref), "%ld", v);
+    if (strcmp(buf, ref) != 0) bad++;
+  }
   printf("%s %ld mismatches\n", bad ? "FAIL" : "OK", bad);
   return bad ? 1 : 0;
 }
