@@ -223,6 +223,18 @@ def peel_ops(ped_view, n_states):
     return total, n_ext
 
 
+def ep_eval_ops(ped_view):
+    """FP64 operations k_brent's EP instantiation executes per objective evaluation for the extended families (the
+    polynomial form, es_poly_eval): t = f / g or g / f (2), D Horner steps (multiply + add), D multiplies for the
+    base power, one for the product, and the (mantissa, exponent) product (2): 3 D + 5 per family, D = 2 x founders
+    on autosomes."""
+    import polymutt_amd as pm
+    v = ped_view
+    kinds = np.ctypeslib.as_array(v.fam_kind, shape=(v.n_fam,))
+    founders = np.ctypeslib.as_array(v.fam_founders, shape=(v.n_fam,))
+    return int(sum(3 * 2 * int(founders[f]) + 5 for f in range(v.n_fam) if kinds[f] == pm.FAM_EXTENDED))
+
+
 def pmc_traffic():
     """HBM bytes per k_brent dispatch from the newest committed PMC summary (profiles/rNN_pmc.json: the default
     workload on one engine, tools/profile_round.sh)."""
@@ -412,8 +424,13 @@ def main():
     if n_ext:
         kid_sum = 0   # (ext10 / roof shapes: every family is extended)
 
+    # extended families with the default (POLY) numerics: k_brent evaluates the hoisted polynomials, so its executed
+    # operations are counted (ep_eval_ops), and the hoisting is a kernel of its own with its own roofline below
+    ep = n_ext > 0
+    ext_eval_ops = ep_eval_ops(ped) if ep else ext_ops
+
     def brent_ops(st):
-        return st.evals * (19 * n_nuc + 17 + ext_ops) + st.items * (18 * n_nuc + 36 * kid_sum)
+        return st.evals * (19 * n_nuc + 17 + ext_eval_ops) + st.items * (18 * n_nuc + 36 * kid_sum)
 
     ops = brent_ops(ks)
     # one-engine calibration: k_brent's own launch times (nothing overlaps a launch on a single stream)
@@ -460,8 +477,11 @@ def main():
                                         if cal is not None else "timed region",
                          "achieved_wall": ops / elapsed / 1e12, "frac_wall": ops / elapsed / 1e12 / FP64_NONFMA_TOPS,
                          "peak_measured_issue_rate": peak_meas,
-                         "op_model": "SURVEY 8(d): evals x (19 nNuc + 17 + peel ops) + items x (18 nNuc + 36 kids)",
-                         "peel_ops_per_eval": ext_ops, "evals": ks.evals, "items": ks.items,
+                         "op_model": ("executed: evals x (19 nNuc + 17 + sum over extended families of (3 D + 5)) + items x "
+                                      "(18 nNuc + 36 kids); the coefficient hoisting is roofline_es_hoist") if ep else
+                                     "SURVEY 8(d): evals x (19 nNuc + 17 + peel ops) + items x (18 nNuc + 36 kids)",
+                         "peel_ops_per_eval": ext_ops, "ext_eval_ops": ext_eval_ops if ep else None,
+                         "evals": ks.evals, "items": ks.items,
                          "phase_split": phase_split(ref_st),
                          "ops_per_site": ops / max(1, ks.sites), "log10_per_s": ks.evals * nf / elapsed},
             "roofline_hbm": {"bound": "hbm", "kernel": "k_brent", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS,
@@ -474,6 +494,18 @@ def main():
                          "transitions": int(counters[10]), "transversions": int(counters[11]),
                          "nocall": int(counters[15])},
         }
+        if ep:   # the EP hoisting kernel (es_hoist_wave / es_hoist_jit): ops counted by the schedule compiler
+            hs = ref_st
+            h_ms = hs.es_hoist_ms / max(1, hs.es_hoist_launches)
+            h_ops = hs.es_hoist_ops / max(1, hs.es_hoist_launches)
+            h_t = h_ops / (h_ms * 1e-3) / 1e12 if h_ms > 0 and h_ops > 0 else None
+            out["roofline_es_hoist"] = {
+                "bound": "fp64-valu", "kernel": "es_hoist_wave" if args.denovo else "es_hoist_jit",
+                "achieved": h_t, "peak": FP64_NONFMA_TOPS, "unit": "TFLOP/s (non-FMA FP64 ops)",
+                "frac": h_t / FP64_NONFMA_TOPS if h_t else None, "ops_per_launch": h_ops, "avg_launch_ms": h_ms,
+                "launches": hs.es_hoist_launches, "ms_per_step": hs.es_hoist_ms / max(1, args.calib_steps),
+                "op_model": "FP64 operations of the generated peel (each mul, add or fma one), per family shape and "
+                            "variant, times the hoisted (item, family) pairs"}
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(args)
             out["cpu_baseline"] = cb

@@ -273,6 +273,12 @@ typedef struct {
                             the frequency-independent family terms, summed over the items' blocks (lane 0's clock) */
   int64_t eval_wave_ns;  /* ... and in the Brent loop (objective evaluations + updates) */
   int64_t timed_items;   /* items the two fields above cover */
+  /* extended families in polynomial form (EP): the coefficient hoisting that precedes each Brent chunk, timed apart
+     from the Brent launches (kernel_ms / launches above exclude it) */
+  int64_t es_hoist_launches;
+  double  es_hoist_ms;
+  double  es_hoist_ops;  /* its FP64 operations (each mul, add or fma one), counted by the schedule compiler per family
+                            shape and variant; 0 when the generic kernel ran (PM_NO_JIT) */
 } pm_kernel_stats;
 int pm_engine_kernel_stats(pm_engine *eng, pm_kernel_stats *out, int32_t reset);
 

@@ -98,6 +98,9 @@ struct pm_engine {
   // stats
   pm_kernel_stats stats{};
   std::vector<std::pair<hipEvent_t, hipEvent_t>> brent_events;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> es_events;   // the EP hoisting launches (schedule compiler or k_es_hoist)
+  double es_item_ops[3] = {0, 0, 0};   // FP64 ops of one item's hoisting over the lane plan's extended families, by variant
+  bool es_ops_known = false;           // (the compiled kernels report them; the generic k_es_hoist does not)
 };
 
 static void geno_mut_matrix(double mu, double tstv, double* out) {   // src/MutationModel.cpp:15-90
@@ -273,6 +276,7 @@ void pm_engine_destroy(pm_engine* E) {
   for (auto& pl : E->d_jit_slots)
     for (int* b : pl) if (b) hipFree(b);
   for (auto& pr : E->brent_events) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
+  for (auto& pr : E->es_events) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
   if (E->h_res) hipHostFree(E->h_res);
   if (E->h_counts) hipHostFree(E->h_counts);
   if (E->ev0) hipEventDestroy(E->ev0);
@@ -902,10 +906,18 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
       } else (void)hipGetLastError();
     }
   }
-  hipEvent_t a, b;
-  HIP_TRY(hipEventCreate(&a));
-  HIP_TRY(hipEventCreate(&b));
-  HIP_TRY(hipEventRecord(a, E->stream));
+  // HIP events around every Brent launch (and, for EP, every hoisting launch: pm_kernel_stats reports the two apart)
+  auto mark = [&](std::vector<std::pair<hipEvent_t, hipEvent_t>>& v, bool begin) -> int {
+    if (begin) {
+      hipEvent_t a, b;
+      HIP_TRY(hipEventCreate(&a));
+      HIP_TRY(hipEventCreate(&b));
+      v.push_back({a, b});
+      HIP_TRY(hipEventRecord(a, E->stream));
+    } else HIP_TRY(hipEventRecord(v.back().second, E->stream));
+    return PM_OK;
+  };
+  int mrc;
   if (ep) {   // chunks of the list (the coefficient buffer holds es_chunk items): k_es_hoist, then the chunk's Brent items
     void (*hoist)(DevArgs, int) = A.denovo ? k_es_hoist<true> : k_es_hoist<false>;
     const size_t hlds = (size_t)E->hoist_waves * (E->poly_coef + E->hoist_tmp) * sizeof(double);
@@ -914,9 +926,17 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
     const int hgrid = E->n_cu * std::max(1, std::min(8, (int)((160 * 1024) / (hlds + stat))));
     const int max_items = 4 * E->last_n;
     const pmjit::Kernel* K = jit_kernel(E);
+    E->es_ops_known = K != nullptr;
+    if (K) {   // one item's hoisting ops over the plan's extended families (slot shapes), by variant
+      for (int v = 0; v < 3; v++) {
+        E->es_item_ops[v] = 0;
+        for (int sg : K->slot_sig) E->es_item_ops[v] += K->shape_ops[v].empty() ? 0.0 : K->shape_ops[v][sg];
+      }
+    }
     for (int it0 = 0; it0 < max_items; it0 += E->es_chunk) {
       A.es_it0 = it0;
       A.es_it1 = (int)std::min<long long>((long long)it0 + E->es_chunk, INT_MAX);
+      if ((mrc = mark(E->es_events, true))) return mrc;
       if (K) {   // compiled schedule: one thread (--denovo: one wave) per (item, family)
         const int plan = E->use_plan1 ? 1 : 0, ns = (int)K->slot_e.size();
         const int* tab = E->d_jit_slots[plan][E->chrom];
@@ -934,15 +954,18 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
         else HIP_TRY(hipModuleLaunchKernel(K->fn, E->n_cu * 8, 1, 1, 256, 1, 1, 0, E->stream, params, nullptr));
       } else hipLaunchKernelGGL(hoist, dim3(hgrid), dim3(64 * E->hoist_waves), hlds, E->stream, A, list);
       HIP_TRY(hipGetLastError());
+      if ((mrc = mark(E->es_events, false))) return mrc;
+      if ((mrc = mark(E->brent_events, true))) return mrc;
       hipLaunchKernelGGL(fn, dim3(grid), dim3(T), shmem, E->stream, A, list);
       HIP_TRY(hipGetLastError());
+      if ((mrc = mark(E->brent_events, false))) return mrc;
     }
   } else {
+    if ((mrc = mark(E->brent_events, true))) return mrc;
     hipLaunchKernelGGL(fn, dim3(grid), dim3(T), shmem, E->stream, A, list);
+    HIP_TRY(hipGetLastError());
+    if ((mrc = mark(E->brent_events, false))) return mrc;
   }
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(b, E->stream));
-  E->brent_events.push_back({a, b});
   return PM_OK;
 }
 
@@ -1056,6 +1079,14 @@ static int collect_stats(pm_engine* E) {
     hipEventDestroy(pr.first); hipEventDestroy(pr.second);
   }
   E->brent_events.clear();
+  for (auto& pr : E->es_events) {
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, pr.first, pr.second));
+    E->stats.es_hoist_ms += ms;
+    E->stats.es_hoist_launches++;
+    hipEventDestroy(pr.first); hipEventDestroy(pr.second);
+  }
+  E->es_events.clear();
   return PM_OK;
 }
 
@@ -1074,6 +1105,14 @@ static int finish_batch(pm_engine* E, const int* counts) {
   E->stats.site_visits += (int64_t)counts[0] / (E->vcf ? 1 : (E->par.denovo && !mono_dn_in_prep(E)) ? 4 : 3) + counts[1] / 3 +
                           counts[2] + counts[9];
   E->stats.sites += E->last_n;
+  if (E->es_ops_known && (E->use_plan1 ? E->n_ext1 : E->n_ext) > 0) {
+    // hoisted items by variant: under --denovo list 0 holds cfg 0 (the top variant) and cfgs 1-3 (10-state) per site,
+    // list 1 cfgs 4-6 (10-state), list 2 the cfg-7 re-optimisation (bi-allelic); otherwise every item is bi-allelic
+    const double* o = E->es_item_ops;
+    if (E->par.denovo && !E->vcf)
+      E->stats.es_hoist_ops += counts[0] / 4 * o[2] + (counts[0] - counts[0] / 4) * o[1] + counts[1] * o[1] + counts[2] * o[0];
+    else E->stats.es_hoist_ops += ((double)counts[0] + counts[1] + counts[2]) * o[0];
+  }
   int rc = collect_stats(E);
   if (rc) return rc;
   if (counts[5]) { pm_set_last_error("ScalarMinimizer::Brent got stuck"); return PM_EBRENT; }

@@ -29,10 +29,12 @@ std::string lit(double x) {   // exact hexadecimal literal
 struct Gen {
   std::string code;
   int nv = 0;
+  long ops = 0;   // FP64 operations emitted (each mul, add or fma one; table loads not counted)
   std::map<std::string, std::string> memo;   // expression -> value: identical computations share one value
   std::string def(const std::string& expr) {
     auto it = memo.find(expr);
     if (it != memo.end()) return it->second;
+    if (expr.compare(0, 3, "lk[") != 0) ops++;
     std::string v = "v" + std::to_string(nv++);
     code += "  const double " + v + " = " + expr + ";\n";
     memo[expr] = v;
@@ -96,7 +98,7 @@ std::string shape_key(const Family& F) {
 }
 
 // One family shape's hoisting as a device function: the polynomial of FamilyLikelihoodES' BA peel in (f, g).
-std::string gen_family(const Family& F, int chrom, const double (*T)[27], const std::string& name) {
+std::string gen_family(const Family& F, int chrom, const double (*T)[27], const std::string& name, double* ops) {
   Gen G;
   const int n = F.n;
   const bool X = chrom == PM_CHR_X, Y = chrom == PM_CHR_Y, MT = chrom == PM_CHR_MT;
@@ -180,6 +182,7 @@ std::string gen_family(const Family& F, int chrom, const double (*T)[27], const 
                     "int os, int dcap) {\n" + G.code;
   for (int a = 0; a <= L.d; a++) out += "  out[" + std::to_string(a) + " * os] = " + (L.c[a].empty() ? "0.0" : L.c[a]) + ";\n";
   out += "  out[(dcap - 1) * os] = " + std::to_string(L.d) + ".0;\n}\n";
+  *ops = (double)G.ops;
   return out;
 }
 
@@ -445,7 +448,9 @@ struct WaveGen {
   }
 };
 
-std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const std::string& name, int* ws_doubles) {
+// ops: the FP64 operations the generated phases perform (summed over their work elements: the useful lane-operations,
+// whatever the lanes' occupancy)
+std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const std::string& name, int* ws_doubles, double* ops) {
   const int n = F.n;
   const bool X = chrom == PM_CHR_X, Y = chrom == PM_CHR_Y, MT = chrom == PM_CHR_MT;
   // degrees through the peel (poly_layout's rule), capacities, temporaries (type 3 only: the W(i, j) products)
@@ -528,8 +533,21 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
   };
   size_t si = 0;
   int fin = -1;
+  double nops = 0;
   for (const int2& St : F.steps) {
     const StepDeg g = sd[si++];
+    {   // this step's FP64 operations
+      const int type = St.x & 255, slot = (St.y >> 8) & 255, create = (St.y >> 16) & 1;
+      const double ns = NS;
+      if (type == 1) nops += ns * ns * ((g.a + 1) * ns + (create ? 0 : (g.a + 1) * (g.b + 1)));
+      else if (type == 2) {
+        const int ds = g.a + g.b;
+        nops += ns * ((slot == 255 ? (ds + 1) * ns : ns * (g.a + 1) * (g.b + 1)) + (g.c + 1) * (ds + 1));
+      } else {
+        const int dw = g.a + g.b + g.c;
+        nops += ns * ns * (g.a + 1) * (g.b + 1) * (g.c + 1) * (slot == 255 ? 1 : 2) + ns * (ns * ns * (dw + 1) + (g.e + 1) * (dw + 1));
+      }
+    }
     const int type = St.x & 255, from0 = (St.x >> 8) & 255, from1 = (St.x >> 16) & 255, to0 = (St.x >> 24) & 255;
     const int slot = (St.y >> 8) & 255, create = (St.y >> 16) & 1, fa2mo = (St.y >> 17) & 1;
     fin = to0;
@@ -619,6 +637,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
     }
   }
   const int D = dP[fin];
+  *ops = nops + (double)(D + 1) * NS;
   code += "  for (int a = lane; a <= " + S(D) + "; a += 64) {\n    double s = 0.0;\n#pragma unroll\n    for (int i = 0; i < " + nsS +
           "; i++) s += W[" + S(po[fin]) + " + i * " + S(capP[fin]) + " + a];\n    out[(size_t)a * os] = s;\n  }\n"
           "  if (lane == 0) out[(size_t)(dcap - 1) * os] = " + S(D) + ".0;\n  wave_sync();\n";
@@ -733,6 +752,7 @@ int pack_steps(const pm_pedigree* ped, int f, int ns, std::vector<int2>& out) {
 
 std::string generate(int chrom, const std::vector<Family>& fams, const double (*tba)[27], Kernel* out, bool denovo) {
   std::map<std::string, int> shape_of;
+  for (auto& v : out->shape_ops) v.clear();
   std::vector<std::string> names, bodies, post_names, post_bodies, wave_names, wave_bodies;
   int ws = 1;
   std::vector<std::pair<int, int>> order;   // (shape, index into fams)
@@ -744,18 +764,20 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
       id = (int)names.size();
       shape_of[key] = id;
       names.push_back("fam" + std::to_string(id));
+      double o3[3] = {0, 0, 0};
       if (!denovo) {
-        bodies.push_back(gen_family(fams[i], chrom, tba, names.back()));
+        bodies.push_back(gen_family(fams[i], chrom, tba, names.back(), &o3[0]));
         post_names.push_back("post" + std::to_string(id));
         post_bodies.push_back(gen_post_family(fams[i], chrom, tba, post_names.back()));
       } else {   // variants 3 id + {0 bi-allelic, 1 10-state, 2 top}
         for (int v = 0; v < 3; v++) {
           int w = 0;
           wave_names.push_back("wfam" + std::to_string(id) + "_" + std::to_string(v));
-          wave_bodies.push_back(gen_wave_family(fams[i], chrom, v == 0 ? 3 : 10, v == 2, wave_names.back(), &w));
+          wave_bodies.push_back(gen_wave_family(fams[i], chrom, v == 0 ? 3 : 10, v == 2, wave_names.back(), &w, &o3[v]));
           ws = std::max(ws, w);
         }
       }
+      for (int v = 0; v < 3; v++) out->shape_ops[v].push_back(o3[v]);
     } else id = it->second;
     order.push_back({id, (int)i});
   }

@@ -64,6 +64,9 @@ struct Kernel {
   int n_shapes = 0;
   double compile_ms = 0;
   bool wave = false;         // --denovo: es_hoist_wave, one (item, family) per wave, blockDim = 64 wpb
+  // FP64 operations of one (item, family) hoisting per shape, by variant: 0 bi-allelic, 1 10-state (de novo items),
+  // 2 top (the de novo monomorphism item); the bi-allelic engines fill variant 0 only
+  std::vector<double> shape_ops[3];
   int wpb = 0, ws = 0;       // waves per block, workspace doubles per wave
 };
 

@@ -76,7 +76,7 @@ class Counters(C.Structure):
 class KernelStats(C.Structure):
     _fields_ = [("launches", i64), ("kernel_ms", f64), ("evals", i64), ("fam_evals", i64), ("items", i64),
                 ("sites", i64), ("site_visits", i64), ("hoist_wave_ns", i64), ("eval_wave_ns", i64),
-                ("timed_items", i64)]
+                ("timed_items", i64), ("es_hoist_launches", i64), ("es_hoist_ms", f64), ("es_hoist_ops", f64)]
 
 
 SITE_DTYPE = np.dtype([
