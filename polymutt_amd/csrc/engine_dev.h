@@ -2403,29 +2403,6 @@ __device__ __forceinline__ void d_emit_vcf(const DevArgs& A, const double* s_gq,
   ((pm_vcf_call*)A.calls)[idx] = c;
 }
 
-// GQ of post[best] = n / d (d > 0) without the IEEE division: d_gq only compares q = 1 - pb with two thresholds and
-// pb with the 100 cut, so the quotient from the hardware reciprocal and one Newton step (within 2 ulp of n / d)
-// decides them unless q or pb lies within 2^-48 of a compared value -- then the IEEE quotient is taken (rare,
-// divergent).  The same GQ as d_gq(n / d) for every n, d.
-__device__ __forceinline__ int d_gq_quot(double n, double d, const double* thr) {
-  double y = __builtin_amdgcn_rcp(d);
-  y = fma(y, fma(-d, y, 1.0), y);
-  const double pb = n * y, q = 1. - pb;
-  const int g = (int)(-10.0f * __log10f((float)q) + 0.5f);
-  const int base = min(max(g - 1, 0), 98);
-  const double t0 = thr[base], t1 = thr[base + 1];
-  const double eps = 0x1p-48;
-  if (fabs(q - t0) <= eps || fabs(q - t1) <= eps || fabs(pb - 0.9999999999) <= eps) return d_gq(n / d, thr);
-  const int k = base + (q < t0 ? 1 : 0) + (q < t1 ? 1 : 0);
-  return pb > 0.9999999999 ? 100 : k;
-}
-__device__ __forceinline__ void d_emit_vcf_quot(const DevArgs& A, const double* s_gq, size_t idx, double n, double d, int best,
-                                                int8_t label) {
-  pm_vcf_call c;
-  c.best = (int8_t)best; c.gq = (int8_t)(d != 0.0 ? d_gq_quot(n, d, s_gq) : d_gq(0.0, s_gq)); c.label = label; c.pad = 0;
-  ((pm_vcf_call*)A.calls)[idx] = c;
-}
-
 // likelihoodKidGenotype, :1334-1443
 __device__ void d_kid_geno(int chrom, const uint8_t* pl, int np, const double* lk, int p0, int n, const int8_t* sexv, int g11, int g12,
                            int g22, int kid, int k, double* out) {
@@ -2539,7 +2516,7 @@ __device__ __forceinline__ void lean_nuc_post(const DevArgs& A, const double* s_
     if constexpr (VCF) {   // one quotient: post[best]
       const int best = d_best3(q11, q12, q22);
       const double qb = best == 0 ? q11 : best == 1 ? q12 : q22;
-      d_emit_vcf_quot(A, s_gq, out + p0 + j, qb, sum, best, PM_LBL_VCF_DIPLOID);
+      d_emit_vcf(A, s_gq, out + p0 + j, sum != 0 ? qb / sum : 0.0, best, PM_LBL_VCF_DIPLOID);
       continue;
     }
     double post[3] = {0, 0, 0};
@@ -2582,14 +2559,15 @@ __device__ __forceinline__ void lean_nuc_post(const DevArgs& A, const double* s_
       // when its g is within a rounding of g[b], so the other divisions are done only then
       const int b = d_best3(g[0], g[1], g[2]);
       const double gb = b == 0 ? g[0] : b == 1 ? g[1] : g[2];
-      const double near = gb * (1.0 - 1e-12);
-      if (sum != 0.0 && ((b >= 1 && g[0] >= near) || (b == 2 && g[1] >= near))) {   // a possible tie of the quotients
-        const double pb = gb / sum;
-        int best = b;
+      double pb = 0.0;
+      int best = b;
+      if (sum != 0.0) {
+        pb = gb / sum;
+        const double near = gb * (1.0 - 1e-12);
         if (b >= 1 && g[0] >= near && g[0] / sum == pb) best = 0;
         else if (b == 2 && g[1] >= near && g[1] / sum == pb) best = 1;
-        d_emit_vcf(A, s_gq, out + p0 + j, pb, best, PM_LBL_VCF_DIPLOID);
-      } else d_emit_vcf_quot(A, s_gq, out + p0 + j, gb, sum, b, PM_LBL_VCF_DIPLOID);
+      }
+      d_emit_vcf(A, s_gq, out + p0 + j, pb, best, PM_LBL_VCF_DIPLOID);
       continue;
     }
     double post[3] = {0, 0, 0};
