@@ -99,7 +99,8 @@ struct pm_engine {
   pm_kernel_stats stats{};
   std::vector<std::pair<hipEvent_t, hipEvent_t>> brent_events;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> es_events;   // the EP hoisting launches (schedule compiler or k_es_hoist)
-  double es_item_ops[3] = {0, 0, 0};   // FP64 ops of one item's hoisting over the lane plan's extended families, by variant
+  double es_item_ops[6] = {0, 0, 0, 0, 0, 0};   // FP64 ops of one item's hoisting over the lane plan's extended families, by variant
+  bool es_grouped = false;             // es_hoist_wave tasks are a site's de novo items (the leaf steps taken once)
   bool es_ops_known = false;           // (the compiled kernels report them; the generic k_es_hoist does not)
 };
 
@@ -597,6 +598,7 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
       // hoisted coefficients of a chunk of items: <= 1 GiB, at most every item a batch can enqueue in one list (4 per site)
       const size_t per_item = (size_t)std::max({E->max_ext * E->T, E->max_ext1 * std::max(1, E->T1), 1}) * E->poly_dcap * sizeof(double);
       E->es_chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)4 * std::max(1, max_batch), ((size_t)1 << 30) / per_item));
+      if (E->es_chunk >= 12) E->es_chunk -= E->es_chunk % 12;   // whole sites of lists 0 and 1 per chunk (grouped tasks)
       DALLOC(E->d_es_coef, (size_t)E->es_chunk * per_item / sizeof(double));
     }
     // workspace: the Brent grids and the posterior grid are capped so each needs <= 1 GiB
@@ -928,7 +930,7 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
     const pmjit::Kernel* K = jit_kernel(E);
     E->es_ops_known = K != nullptr;
     if (K) {   // one item's hoisting ops over the plan's extended families (slot shapes), by variant
-      for (int v = 0; v < 3; v++) {
+      for (int v = 0; v < 6; v++) {
         E->es_item_ops[v] = 0;
         for (int sg : K->slot_sig) E->es_item_ops[v] += K->shape_ops[v].empty() ? 0.0 : K->shape_ops[v][sg];
       }
@@ -948,9 +950,18 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
         J.dcap = A.poly_dcap; J.vcf = A.vcf; J.res_words = sizeof(pm_site_result) / 4;
         J.res_a1 = offsetof(pm_site_result, allele1) / 4; J.res_a2 = offsetof(pm_site_result, allele2) / 4;
         J.denovo = A.denovo;
+        // a site's de novo items are consecutive in lists 0 (cfgs 0-3, or 1-3 when k_prep / the QUAD item takes the
+        // monomorphism) and 1 (cfgs 4-6): one task takes them together, the 10-state leaf steps once
+        J.group = 0;
+        if (K->wave && A.denovo && !A.vcf && !getenv("PM_ES_NOGROUP")) {
+          if (list == 0) J.group = A.mono_dn ? 3 : 4;
+          else if (list == 1) J.group = 3;
+        }
+        if (list == 0) E->es_grouped = J.group > 1;   // (finish_batch's op count: lists 0 and 1 group alike)
         void* params[] = {&J};
         if (K->wave)
-          HIP_TRY(hipModuleLaunchKernel(K->fn, E->n_cu * std::max(1, 16 / K->wpb), 1, 1, 64 * K->wpb, 1, 1, 0, E->stream, params, nullptr));
+          HIP_TRY(hipModuleLaunchKernel(K->fn, E->n_cu * (K->blocks_per_cu > 0 ? K->blocks_per_cu : std::max(1, 16 / K->wpb)), 1, 1,
+                                        64 * K->wpb, 1, 1, 0, E->stream, params, nullptr));
         else HIP_TRY(hipModuleLaunchKernel(K->fn, E->n_cu * 8, 1, 1, 256, 1, 1, 0, E->stream, params, nullptr));
       } else hipLaunchKernelGGL(hoist, dim3(hgrid), dim3(64 * E->hoist_waves), hlds, E->stream, A, list);
       HIP_TRY(hipGetLastError());
@@ -1109,7 +1120,9 @@ static int finish_batch(pm_engine* E, const int* counts) {
     // hoisted items by variant: under --denovo list 0 holds cfg 0 (the top variant) and cfgs 1-3 (10-state) per site,
     // list 1 cfgs 4-6 (10-state), list 2 the cfg-7 re-optimisation (bi-allelic); otherwise every item is bi-allelic
     const double* o = E->es_item_ops;
-    if (E->par.denovo && !E->vcf)
+    if (E->par.denovo && !E->vcf && E->es_grouped)   // a task: one leaf prefix, then the rest per 10-state item
+      E->stats.es_hoist_ops += counts[0] / 4 * (o[3] + o[5] + 3 * o[4]) + counts[1] / 3 * (o[3] + 3 * o[4]) + counts[2] * o[0];
+    else if (E->par.denovo && !E->vcf)
       E->stats.es_hoist_ops += counts[0] / 4 * o[2] + (counts[0] - counts[0] / 4) * o[1] + counts[1] * o[1] + counts[2] * o[0];
     else E->stats.es_hoist_ops += ((double)counts[0] + counts[1] + counts[2]) * o[0];
   }

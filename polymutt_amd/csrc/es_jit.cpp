@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -192,7 +193,7 @@ struct Args {
   const int* items; const int* counts; const uint8_t* ref; const int* res; const uint8_t* pl; const double* lktab;
   double* coef; const int* slot_e; const int* slot_sig; const int* slot_p0;
   const double* T10; const double* T10dn; const double* tba;
-  int list, it0, it1, nslots, np, T, max_ext, dcap, vcf, res_words, res_a1, res_a2, denovo;
+  int list, it0, it1, nslots, np, T, max_ext, dcap, vcf, res_words, res_a1, res_a2, denovo, group;
 };
 __device__ __forceinline__ int gi(int b1, int b2) {
   return b1 < b2 ? (b1 - 1) * (10 - b1) / 2 + (b2 - b1) : (b2 - 1) * (10 - b2) / 2 + (b1 - b2);
@@ -441,6 +442,10 @@ extern "C" __global__ void __launch_bounds__(256) es_post_jit(PostArgs A) {
 // phase is a few unrolled multiply-adds per lane between wave-level barriers, with no schedule or layout loads
 // and no run-time divisions.  Variants per shape: 10-state (de novo items), bi-allelic (cfg-7 items), and "top"
 // (the de novo monomorphism item: the f^D coefficient only, every degree 0).
+// The de novo transmission rows of a type-1 step's pairs: from the (cache-resident) global table, or held in 20
+// registers for the whole kernel (PM_ES_TR=reg: 149 VGPRs, 3 waves per SIMD; capped at 128 with 19 spilled)
+bool g_tr_regs = false;
+
 struct WaveGen {
   std::string code;
   void loop(int N, const std::string& body) {   // lanes over N elements x, then a wave barrier
@@ -450,22 +455,32 @@ struct WaveGen {
 
 // ops: the FP64 operations the generated phases perform (summed over their work elements: the useful lane-operations,
 // whatever the lanes' occupancy)
-std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const std::string& name, int* ws_doubles, double* ops) {
+// part (10-state variants only): 0 the whole peel; 1 the cfg-independent prefix -- the 10-state penetrances of
+// non-founders no step changes and the type-1 steps that peel them into marriage partials no cfg-dependent step
+// writes (leaf steps, run first: nothing they read or write is touched by an earlier step) -- and 2 the rest (the
+// other persons' partials, the other steps, the final sum).  Part 1 once and part 2 per item give part 0's values for
+// the de novo items of one site (they differ only in the founder priors' genotypes; the top variant's leaf steps are
+// the same degree-0 products).  Parts lay out the workspace by the 10-state variant's degrees, top or not.
+std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const std::string& name, int* ws_doubles, double* ops,
+                            int part = 0, int multi = 1) {
   const int n = F.n;
   const bool X = chrom == PM_CHR_X, Y = chrom == PM_CHR_Y, MT = chrom == PM_CHR_MT;
   // degrees through the peel (poly_layout's rule), capacities, temporaries (type 3 only: the W(i, j) products)
   std::vector<int> d0(n), dP(n), capP(n);
-  for (int i = 0; i < n; i++) {
-    const bool fo = F.founder[i] && i < F.nf;
-    const int sx = F.sex[i];
-    const int dfull = !fo ? 0 : (Y && sx == FEMALE) ? 0 : (((X || Y) && sx == MALE) || MT) ? 1 : 2;
-    d0[i] = dP[i] = top ? 0 : dfull;
-    capP[i] = dP[i] + 1;
-  }
   std::map<int, int> dM, capM;
   int tmp = 1;
   struct StepDeg { int a, b, c, e; };
   std::vector<StepDeg> sd;
+  for (int pass = (part && top) ? 0 : 1; pass < 2; pass++) {   // (pass 0: the 10-state variant's capacities)
+  const bool tp = pass == 1 && top;
+  sd.clear(); dM.clear();
+  for (int i = 0; i < n; i++) {
+    const bool fo = F.founder[i] && i < F.nf;
+    const int sx = F.sex[i];
+    const int dfull = !fo ? 0 : (Y && sx == FEMALE) ? 0 : (((X || Y) && sx == MALE) || MT) ? 1 : 2;
+    d0[i] = dP[i] = tp ? 0 : dfull;
+    capP[i] = std::max(pass ? capP[i] : 0, dP[i] + 1);
+  }
   for (const int2& S : F.steps) {
     const int type = S.x & 255, from0 = (S.x >> 8) & 255, from1 = (S.x >> 16) & 255, to0 = (S.x >> 24) & 255;
     const int slot = (S.y >> 8) & 255, create = (S.y >> 16) & 1;
@@ -486,24 +501,89 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
     }
     sd.push_back(g);
   }
+  }
+  // leaf steps (part 1) and the persons only they read; pristine[s]: the founder "from" of step s still holds its
+  // prior x penetrance partial (3 non-zero states), so a type-2 step sums over those 3 states only
+  const int nst = (int)F.steps.size();
+  std::vector<char> leaf(nst, 0), leafp(n, 0), pristine(nst, 0);
+  if (NS == 10) {
+    auto ty = [&](int k) { return F.steps[k].x & 255; };
+    auto fr = [&](int k) { return (F.steps[k].x >> 8) & 255; };
+    auto to = [&](int k) { return (F.steps[k].x >> 24) & 255; };
+    auto sl = [&](int k) { return (F.steps[k].y >> 8) & 255; };
+    auto fo = [&](int i) { return F.founder[i] && i < F.nf; };
+    std::vector<char> isto(n, 0), touched(n, 0);
+    for (int k = 0; k < nst; k++)
+      if (ty(k) != 1) isto[to(k)] = 1;
+    for (int k = 0; k < nst; k++) {
+      if (ty(k) == 2 && fo(fr(k)) && !touched[fr(k)] && !top) pristine[k] = 1;
+      if (ty(k) != 1) touched[to(k)] = 1;
+      // a leaf step reads a non-founder's penetrance partial that no step ever changes
+      if (ty(k) == 1 && !fo(fr(k)) && !isto[fr(k)]) leaf[k] = 1;
+    }
+    // ... into a marriage partial that only leaf steps write, and that no step reads before the last of them
+    for (bool changed = true; changed;) {
+      changed = false;
+      std::map<int, int> nonleaf_writer;
+      for (int k = 0; k < nst; k++)
+        if (ty(k) == 1 && !leaf[k]) nonleaf_writer[sl(k)] = 1;
+      for (int k = 0; k < nst; k++) {
+        if (leaf[k] && nonleaf_writer.count(sl(k))) { leaf[k] = 0; changed = true; }
+        if (ty(k) == 1 || sl(k) == 255) continue;
+        for (int k2 = k + 1; k2 < nst; k2++)
+          if (leaf[k2] && ty(k2) == 1 && sl(k2) == sl(k)) { leaf[k2] = 0; changed = true; }
+      }
+    }
+    for (int k = 0; k < nst; k++)
+      if (leaf[k]) leafp[fr(k)] = 1;
+  }
+  // workspace layout: persons' partials, marriage partials, the type-3 products.  Parts put the leaf prefix's
+  // regions first (a task's items share them) and give each of the M items of a part-2 function its own copy of the
+  // rest, cb = c * NSZ doubles further on
+  const int M = part == 2 ? std::max(1, multi) : 1;
+  std::map<int, int> leafs;   // the marriage slots the leaf steps write
+  for (int k = 0; k < nst; k++)
+    if (leaf[k]) leafs[(F.steps[k].y >> 8) & 255] = 1;
   std::vector<int> po(n);
-  int off = 0;
-  for (int i = 0; i < n; i++) { po[i] = off; off += NS * capP[i]; }
   std::map<int, int> mo;
-  for (auto& m : capM) { mo[m.first] = off; off += NS * NS * m.second; }
-  const int TB = off;
-  *ws_doubles = off + tmp;
+  int off = 0, LSZ = 0;
+  for (int L = part ? 1 : 0; L >= 0; L--) {
+    for (int i = 0; i < n; i++)
+      if (!part || leafp[i] == L) { po[i] = off; off += NS * capP[i]; }
+    for (auto& m : capM)
+      if (!part || (int)leafs.count(m.first) == L) { mo[m.first] = off; off += NS * NS * m.second; }
+    if (L == 1) LSZ = off;
+  }
+  const int TB = off, NSZ = off + tmp - LSZ;
+  *ws_doubles = LSZ + M * NSZ;
   auto S = [](long v) { return std::to_string(v); };
   const std::string nsS = S(NS), nsq = S(NS * NS), R = S((NS * NS + 63) / 64);
-  std::string code;
+  const bool mc = part == 2;   // offsets of the item's own regions carry cb
+  auto PO = [&](int i) { return mc && !leafp[i] ? "(" + S(po[i]) + " + cb)" : S(po[i]); };
+  auto MOf = [&](int s) { return mc && !leafs.count(s) ? "(" + S(mo[s]) + " + cb)" : S(mo[s]); };
+  const std::string TBs = mc ? "(" + S(TB) + " + cb)" : S(TB);
+  // a phase with lanes over (item c, index var < N); part 2: c's genotypes (packed 8 bits per item) and offset cb
+  auto lanes = [&](int N, const std::string& var, const std::string& body) -> std::string {
+    if (!mc) return "  for (int " + var + " = lane; " + var + " < " + S(N) + "; " + var + " += 64) {\n" + body + "  }\n";
+    return "  for (int x_ = lane; x_ < " + S(M * N) + "; x_ += 64) {\n    const int c = x_ / " + S(N) + ", " + var + " = x_ - c * " +
+           S(N) + ", cb = c * " + S(NSZ) + ";\n    const int g11 = (gg11 >> (8 * c)) & 255, g12 = (gg12 >> (8 * c)) & 255, "
+           "g22 = (gg22 >> (8 * c)) & 255;\n    (void)g11; (void)g12; (void)g22; (void)cb;\n" + body + "  }\n";
+  };
+  // a phase with lanes over the pairs e: every item's work in the lane, unrolled
+  auto items = [&](const std::string& body) -> std::string {
+    if (!mc) return body;
+    return "#pragma unroll\n      for (int c = 0; c < " + S(M) + "; c++) {\n      const int cb = c * " + S(NSZ) + ";\n" + body + "      }\n";
+  };
+  std::string code = mc ? "" : "  const int g11 = gg11, g12 = gg12, g22 = gg22;\n  (void)g11; (void)g12; (void)g22;\n";
   // InitializePartials x SetFounderPriors, one person at a time (lanes over its states)
   for (int i = 0; i < n; i++) {
+    if ((part == 1 && !leafp[i]) || (part == 2 && leafp[i])) continue;
     const bool fo = F.founder[i] && i < F.nf;
     const int sx = F.sex[i];
     const bool yf = NS == 3 && Y && sx == FEMALE;
     const int dfull = !fo ? 0 : (Y && sx == FEMALE) ? 0 : (((X || Y) && sx == MALE) || MT) ? 1 : 2;
     const int d = d0[i];
-    std::string b = "    const int o = " + S(po[i]) + " + x * " + S(capP[i]) + ";\n";
+    std::string b = "    const int o = " + PO(i) + " + x * " + S(capP[i]) + ";\n";
     for (int a = 0; a <= d; a++) b += "    W[o + " + S(a) + "] = 0.0;\n";
     if (NS == 3) {
       b += "    const double pen = lk[(x == 0 ? P11 : x == 1 ? P12 : P22)[p0 + " + S(i) + "]];\n";
@@ -514,14 +594,14 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
       else b += "    if (x != 1) W[o + (x == 0 ? 1 : 0)] = pen;\n";
     } else {
       b += "    const double pen = lk[pl[(size_t)x * np + p0 + " + S(i) + "]];\n";
-      b += "    const int q = x == g11 ? 0 : x == g12 ? 1 : x == g22 ? 2 : 3;\n";
+      b += "    const int q = x == g11 ? 0 : x == g12 ? 1 : x == g22 ? 2 : 3;\n    (void)q;\n";
       if (!fo) b += "    W[o] = pen;\n";
       else if (top && dfull > 0) b += "    if (q == 0) W[o] = pen;\n";
       else if (d == 2) b += "    if (q != 3) W[o + 2 - q] = q == 1 ? 2 * pen : pen;\n";
       else if (d == 1) b += "    if (q == 0 || q == 2) W[o + (q == 0 ? 1 : 0)] = pen;\n";
       else b += "    if (q != 3) W[o] = pen;\n";
     }
-    code += "  for (int x = lane; x < " + nsS + "; x += 64) {\n" + b + "  }\n";
+    code += lanes(NS, "x", b);
   }
   code += "  wave_sync();\n";
   // T(e = i NS + j, k) of an offspring: 10-state rows of the lane's pair(s) in registers (trow, the de novo
@@ -535,14 +615,18 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
   int fin = -1;
   double nops = 0;
   for (const int2& St : F.steps) {
+    const int kstep = (int)si;
     const StepDeg g = sd[si++];
-    {   // this step's FP64 operations
+    fin = (St.x >> 24) & 255;
+    if ((part == 1 && !leaf[kstep]) || (part == 2 && leaf[kstep])) continue;
+    {   // this step's FP64 operations (per item)
       const int type = St.x & 255, slot = (St.y >> 8) & 255, create = (St.y >> 16) & 1;
       const double ns = NS;
       if (type == 1) nops += ns * ns * ((g.a + 1) * ns + (create ? 0 : (g.a + 1) * (g.b + 1)));
       else if (type == 2) {
         const int ds = g.a + g.b;
-        nops += ns * ((slot == 255 ? (ds + 1) * ns : ns * (g.a + 1) * (g.b + 1)) + (g.c + 1) * (ds + 1));
+        if (pristine[kstep]) nops += ns * ((g.a == 1 ? 2 : 3) * (slot == 255 ? 1 : (g.b + 1)) + (g.c + 1) * (ds + 1));
+        else nops += ns * ((slot == 255 ? (ds + 1) * ns : ns * (g.a + 1) * (g.b + 1)) + (g.c + 1) * (ds + 1));
       } else {
         const int dw = g.a + g.b + g.c;
         nops += ns * ns * (g.a + 1) * (g.b + 1) * (g.c + 1) * (slot == 255 ? 1 : 2) + ns * (ns * ns * (dw + 1) + (g.e + 1) * (dw + 1));
@@ -550,18 +634,16 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
     }
     const int type = St.x & 255, from0 = (St.x >> 8) & 255, from1 = (St.x >> 16) & 255, to0 = (St.x >> 24) & 255;
     const int slot = (St.y >> 8) & 255, create = (St.y >> 16) & 1, fa2mo = (St.y >> 17) & 1;
-    fin = to0;
     if (type == 1) {   // lanes over the pairs e: S(e) = sum_k T(e, k) P_off[k] in registers, then M(e) *= S(e) in place
-      const int off_ = from0, csex = F.sex[off_], pcap = capP[off_], mcap = capM[slot], MO = mo[slot];
-      std::string b = "#pragma unroll\n  for (int r = 0; r < " + R + "; r++) {\n    const int e = lane + 64 * r;\n    if (e < " + nsq + ") {\n";
-      b += "      double s[" + S(g.a + 1) + "];\n";
+      const int off_ = from0, csex = F.sex[off_], pcap = capP[off_], mcap = capM[slot];
+      std::string b = "      double s[" + S(g.a + 1) + "];\n";
       for (int a = 0; a <= g.a; a++) {
         b += "      s[" + S(a) + "] = 0.0;\n";
         b += "#pragma unroll\n      for (int k = 0; k < " + nsS + "; k++) s[" + S(a) + "] = fma(" +
-             (NS == 10 ? std::string("(r == 0 ? tr0[k] : tr1[k])") : tt(csex, "e", "k", false)) + ", W[" + S(po[off_]) + " + k * " +
+             (NS == 10 ? std::string(g_tr_regs ? "(r == 0 ? tr0[k] : tr1[k])" : "t10dn[e * 10 + k]") : tt(csex, "e", "k", false)) + ", W[" + PO(off_) + " + k * " +
              S(pcap) + " + " + S(a) + "], s[" + S(a) + "]);\n";
       }
-      const std::string me = S(MO) + " + e * " + S(mcap);
+      const std::string me = MOf(slot) + " + e * " + S(mcap);
       if (create) {
         for (int a = 0; a <= g.a; a++) b += "      W[" + me + " + " + S(a) + "] = s[" + S(a) + "];\n";
       } else {
@@ -574,81 +656,106 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
           b += "      W[" + me + " + " + S(a) + "] = " + acc + ";\n";
         }
       }
-      b += "    }\n  }\n  wave_sync();\n";
-      code += b;
+      code += "#pragma unroll\n  for (int r = 0; r < " + R + "; r++) {\n    const int e = lane + 64 * r;\n    if (e < " + nsq + ") {\n" + items(b) +
+              "    }\n  }\n  wave_sync();\n";
     } else if (type == 2) {   // lanes over i: S(i) = sum_j P_from[j] M(j, i) in registers, then P_to[i] *= S(i) in place
       const int sf = from0, stt = to0, fcap = capP[sf], tcap = capP[stt];
       const int ds = g.a + g.b;
-      std::string b = "  for (int i = lane; i < " + nsS + "; i += 64) {\n    double s[" + S(ds + 1) + "];\n";
+      std::string b = "    double s[" + S(ds + 1) + "];\n";
       for (int a = 0; a <= ds; a++) b += "    s[" + S(a) + "] = 0.0;\n";
-      if (slot == 255) {
+      if (pristine[kstep]) {
+        // the founder's partial is prior x penetrance: state g11 / g12 / g22 holds one monomial, at coefficient
+        // 2 - q (degree 2: q = 0, 1, 2), 1 / - / 0 (degree 1: no geno12) or 0 (degree 0); the other states are zero.
+        // The sum visits j in the dense loop's order and skips the zero terms (fma(0, g, s) == s), so it is
+        // bit-identical to the dense sum (q in the dense loop's coefficient order u = 0, 1, 2 at one j, should two of
+        // the genotypes coincide)
+        const int d = d0[sf];
+        b += "#pragma unroll\n    for (int j = 0; j < " + nsS + "; j++) {\n";
+        const std::string gq[3] = {"g11", "g12", "g22"};
+        for (int q = 2; q >= 0; q--) {
+          if (d == 1 && q == 1) continue;
+          const int u = d == 2 ? 2 - q : d == 1 ? (q == 0 ? 1 : 0) : 0;
+          b += "      if (j == " + gq[q] + ") {\n        const double f = W[" + PO(sf) + " + j * " + S(fcap) + " + " + S(u) + "];\n";
+          if (slot == 255) b += "        s[" + S(u) + "] += f;\n";
+          else {
+            const int mcap = capM[slot];
+            const std::string me = fa2mo ? "(j * " + nsS + " + i)" : "(i * " + nsS + " + j)";
+            for (int v = 0; v <= g.b; v++)
+              b += "        s[" + S(u + v) + "] = fma(f, W[" + MOf(slot) + " + " + me + " * " + S(mcap) + " + " + S(v) + "], s[" + S(u + v) + "]);\n";
+          }
+          b += "      }\n";
+        }
+        b += "    }\n";
+      } else if (slot == 255) {
         for (int a = 0; a <= ds; a++)
-          b += "#pragma unroll\n    for (int j = 0; j < " + nsS + "; j++) s[" + S(a) + "] += W[" + S(po[sf]) + " + j * " + S(fcap) + " + " +
+          b += "#pragma unroll\n    for (int j = 0; j < " + nsS + "; j++) s[" + S(a) + "] += W[" + PO(sf) + " + j * " + S(fcap) + " + " +
                S(a) + "];\n";
       } else {
-        const int mcap = capM[slot], MO = mo[slot];
+        const int mcap = capM[slot];
         const std::string me = fa2mo ? "(j * " + nsS + " + i)" : "(i * " + nsS + " + j)";
         b += "#pragma unroll\n    for (int j = 0; j < " + nsS + "; j++) {\n";
-        for (int u = 0; u <= g.a; u++) b += "      const double f" + S(u) + " = W[" + S(po[sf]) + " + j * " + S(fcap) + " + " + S(u) + "];\n";
-        for (int v = 0; v <= g.b; v++) b += "      const double g" + S(v) + " = W[" + S(MO) + " + " + me + " * " + S(mcap) + " + " + S(v) + "];\n";
+        for (int u = 0; u <= g.a; u++) b += "      const double f" + S(u) + " = W[" + PO(sf) + " + j * " + S(fcap) + " + " + S(u) + "];\n";
+        for (int v = 0; v <= g.b; v++) b += "      const double g" + S(v) + " = W[" + MOf(slot) + " + " + me + " * " + S(mcap) + " + " + S(v) + "];\n";
         for (int u = 0; u <= g.a; u++)
           for (int v = 0; v <= g.b; v++) b += "      s[" + S(u + v) + "] = fma(f" + S(u) + ", g" + S(v) + ", s[" + S(u + v) + "]);\n";
         b += "    }\n";
       }
       b += "    double t[" + S(g.c + 1) + "];\n";
-      for (int c = 0; c <= g.c; c++) b += "    t[" + S(c) + "] = W[" + S(po[stt]) + " + i * " + S(tcap) + " + " + S(c) + "];\n";
+      for (int c = 0; c <= g.c; c++) b += "    t[" + S(c) + "] = W[" + PO(stt) + " + i * " + S(tcap) + " + " + S(c) + "];\n";
       for (int a = 0; a <= g.c + ds; a++) {
         std::string acc;
         for (int c = std::max(0, a - ds); c <= std::min(a, g.c); c++)
           acc = acc.empty() ? "t[" + S(c) + "] * s[" + S(a - c) + "]" : "fma(t[" + S(c) + "], s[" + S(a - c) + "], " + acc + ")";
-        b += "    W[" + S(po[stt]) + " + i * " + S(tcap) + " + " + S(a) + "] = " + acc + ";\n";
+        b += "    W[" + PO(stt) + " + i * " + S(tcap) + " + " + S(a) + "] = " + acc + ";\n";
       }
-      b += "  }\n  wave_sync();\n";
-      code += b;
+      code += lanes(NS, "i", b) + "  wave_sync();\n";
     } else {   // W(e) = P_fa[i] M(e) P_mo[j] -> LDS; lanes over k: S(k) = sum_e T(e, k) W(e), P_off[k] *= S(k) in place
       const int fa = from0, mo_ = from1, off_ = to0, csex = F.sex[off_];
       const int dw = g.a + g.b + g.c, ww = dw + 1;
-      std::string b = "#pragma unroll\n  for (int r = 0; r < " + R + "; r++) {\n    const int e = lane + 64 * r;\n    if (e < " + nsq + ") {\n"
-                      "      const int i = e / " + nsS + ", j = e - i * " + nsS + ";\n      double w[" + S(ww) + "];\n";
+      std::string b = "      const int i = e / " + nsS + ", j = e - i * " + nsS + ";\n      double w[" + S(ww) + "];\n";
       for (int a = 0; a <= dw; a++) b += "      w[" + S(a) + "] = 0.0;\n";
       for (int u = 0; u <= g.a; u++)
         for (int v = 0; v <= g.b; v++)
           for (int c = 0; c <= g.c; c++) {
-            const std::string m = slot == 255 ? "" : " * W[" + S(mo[slot]) + " + e * " + S(capM[slot]) + " + " + S(v) + "]";
-            b += "      w[" + S(u + v + c) + "] = fma(W[" + S(po[fa]) + " + i * " + S(capP[fa]) + " + " + S(u) + "]" + m + ", W[" +
-                 S(po[mo_]) + " + j * " + S(capP[mo_]) + " + " + S(c) + "], w[" + S(u + v + c) + "]);\n";
+            const std::string m = slot == 255 ? "" : " * W[" + MOf(slot) + " + e * " + S(capM[slot]) + " + " + S(v) + "]";
+            b += "      w[" + S(u + v + c) + "] = fma(W[" + PO(fa) + " + i * " + S(capP[fa]) + " + " + S(u) + "]" + m + ", W[" +
+                 PO(mo_) + " + j * " + S(capP[mo_]) + " + " + S(c) + "], w[" + S(u + v + c) + "]);\n";
           }
-      for (int a = 0; a <= dw; a++) b += "      W[" + S(TB) + " + e * " + S(ww) + " + " + S(a) + "] = w[" + S(a) + "];\n";
-      b += "    }\n  }\n  wave_sync();\n";
-      b += "  for (int k = lane; k < " + nsS + "; k += 64) {\n    double s[" + S(ww) + "];\n";
-      for (int a = 0; a <= dw; a++) b += "    s[" + S(a) + "] = 0.0;\n";
-      b += "    for (int e = 0; e < " + nsq + "; e++) {\n      const double t = " + tt(csex, "e", "k", slot != 255) + ";\n";
-      for (int a = 0; a <= dw; a++) b += "      s[" + S(a) + "] = fma(t, W[" + S(TB) + " + e * " + S(ww) + " + " + S(a) + "], s[" + S(a) + "]);\n";
-      b += "    }\n    double t[" + S(g.e + 1) + "];\n";
-      for (int c = 0; c <= g.e; c++) b += "    t[" + S(c) + "] = W[" + S(po[off_]) + " + k * " + S(capP[off_]) + " + " + S(c) + "];\n";
+      for (int a = 0; a <= dw; a++) b += "      W[" + TBs + " + e * " + S(ww) + " + " + S(a) + "] = w[" + S(a) + "];\n";
+      code += "#pragma unroll\n  for (int r = 0; r < " + R + "; r++) {\n    const int e = lane + 64 * r;\n    if (e < " + nsq + ") {\n" + items(b) +
+              "    }\n  }\n  wave_sync();\n";
+      std::string b2 = "    double s[" + S(ww) + "];\n";
+      for (int a = 0; a <= dw; a++) b2 += "    s[" + S(a) + "] = 0.0;\n";
+      b2 += "    for (int e = 0; e < " + nsq + "; e++) {\n      const double t = " + tt(csex, "e", "k", slot != 255) + ";\n";
+      for (int a = 0; a <= dw; a++) b2 += "      s[" + S(a) + "] = fma(t, W[" + TBs + " + e * " + S(ww) + " + " + S(a) + "], s[" + S(a) + "]);\n";
+      b2 += "    }\n    double t[" + S(g.e + 1) + "];\n";
+      for (int c = 0; c <= g.e; c++) b2 += "    t[" + S(c) + "] = W[" + PO(off_) + " + k * " + S(capP[off_]) + " + " + S(c) + "];\n";
       for (int a = 0; a <= g.e + dw; a++) {
         std::string acc;
         for (int c = std::max(0, a - dw); c <= std::min(a, g.e); c++)
           acc = acc.empty() ? "t[" + S(c) + "] * s[" + S(a - c) + "]" : "fma(t[" + S(c) + "], s[" + S(a - c) + "], " + acc + ")";
-        b += "    W[" + S(po[off_]) + " + k * " + S(capP[off_]) + " + " + S(a) + "] = " + acc + ";\n";
+        b2 += "    W[" + PO(off_) + " + k * " + S(capP[off_]) + " + " + S(a) + "] = " + acc + ";\n";
       }
-      b += "  }\n  wave_sync();\n";
-      code += b;
+      code += lanes(NS, "k", b2) + "  wave_sync();\n";
     }
   }
   const int D = dP[fin];
-  *ops = nops + (double)(D + 1) * NS;
-  code += "  for (int a = lane; a <= " + S(D) + "; a += 64) {\n    double s = 0.0;\n#pragma unroll\n    for (int i = 0; i < " + nsS +
-          "; i++) s += W[" + S(po[fin]) + " + i * " + S(capP[fin]) + " + a];\n    out[(size_t)a * os] = s;\n  }\n"
-          "  if (lane == 0) out[(size_t)(dcap - 1) * os] = " + S(D) + ".0;\n  wave_sync();\n";
+  *ops = M * (nops + (part == 1 ? 0.0 : (double)(D + 1) * NS));
+  if (part != 1) {
+    code += lanes(D + 1, "a", "    double s = 0.0;\n#pragma unroll\n    for (int i = 0; i < " + nsS + "; i++) s += W[" + PO(fin) + " + i * " +
+                                  S(capP[fin]) + " + a];\n    out[" + std::string(mc ? "c * ostr + " : "") + "(size_t)a * os] = s;\n");
+    code += "  if (lane < " + S(M) + ") out[" + std::string(mc ? "lane * ostr + " : "") + "(size_t)(dcap - 1) * os] = " + S(D) + ".0;\n  wave_sync();\n";
+  }
   return "__device__ __forceinline__ void " + name +
          "(const uint8_t* __restrict__ pl, size_t np, const uint8_t* __restrict__ P11, const uint8_t* __restrict__ P12, "
-         "const uint8_t* __restrict__ P22, int p0, int g11, int g12, int g22, const double* lk, const double* __restrict__ t10, "
+         "const uint8_t* __restrict__ P22, int p0, int gg11, int gg12, int gg22, const double* lk, const double* __restrict__ t10, "
          "const double* __restrict__ t10dn, const double* tb, const double* tr0, const double* tr1, double* W, int lane, "
-         "double* __restrict__ out, int os, int dcap) {\n" + code + "}\n";
+         "double* __restrict__ out, int os, int dcap, size_t ostr) {\n" + code + "}\n";
 }
 
-std::string gen_wave_kernel(const std::vector<std::string>& fns, int ws, int wpb) {
+// fns: 3 variants per shape (bi-allelic, 10-state, top); parts: per shape the 10-state leaf prefix, the 10-state rest,
+// the top variant's rest and (pps == 4) the 10-state rest of three items at once
+std::string gen_wave_kernel(const std::vector<std::string>& fns, const std::vector<std::string>& parts, int pps, int ws, int wpb) {
   std::string s = R"(
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -657,7 +764,7 @@ __device__ __forceinline__ void wave_sync() {
 }
 )";
   std::string k = R"(
-extern "C" __global__ void __launch_bounds__(64 * WPB) es_hoist_wave(Args A) {   // blockDim = 64 WPB
+extern "C" __global__ void __launch_bounds__(64 * WPB) WPEU es_hoist_wave(Args A) {   // blockDim = 64 WPB
   __shared__ double lk[256], tb[6 * 27];
   __shared__ double ws[WPB][WSIZE];
   for (int i = threadIdx.x; i < 256; i += blockDim.x) lk[i] = A.lktab[i];
@@ -676,10 +783,16 @@ extern "C" __global__ void __launch_bounds__(64 * WPB) es_hoist_wave(Args A) {  
   const double* t10dn = A.T10dn;
   const int nItems = min(A.counts[A.list], A.it1);
   if (nItems <= A.it0) return;
-  const long long units = (long long)(nItems - A.it0) * A.nslots;
+  // a task: G consecutive items of the list -- with A.group, the de novo items of one site (list 0: cfgs 0-3, list 1:
+  // cfgs 4-6), whose 10-state leaf steps are taken once per (site, family) -- on one family
+  const int G = A.group > 1 ? A.group : 1;
+  const long long units = ((long long)(nItems - A.it0) + G - 1) / G * A.nslots;
   for (long long u = (long long)blockIdx.x * WPB + wave; u < units; u += (long long)gridDim.x * WPB) {
     const int uq = (int)(u / A.nslots), k = (int)(u - (long long)uq * A.nslots);
-    const int it = A.it0 + uq;
+    int leaf_site = -1;
+    for (int t = 0; t < G; t++) {
+    const int it = A.it0 + uq * G + t;
+    if (it >= nItems) break;
     const int item = __builtin_amdgcn_readfirstlane(A.items[it]);
     const int site = item >> 3, cfg = item & 7, r = A.ref[site];
     int a1, a2;
@@ -693,17 +806,57 @@ extern "C" __global__ void __launch_bounds__(64 * WPB) es_hoist_wave(Args A) {  
     const uint8_t* P22 = pl + (size_t)g22 * A.np;
     const int e = __builtin_amdgcn_readfirstlane(A.slot_e[k]), q = e / A.T;
     const int sig = __builtin_amdgcn_readfirstlane(A.slot_sig[k]), p0 = __builtin_amdgcn_readfirstlane(A.slot_p0[k]);
-    double* out = A.coef + ((size_t)uq * A.max_ext + q) * A.dcap * A.T + (e - q * A.T);
+    double* out = A.coef + ((size_t)(it - A.it0) * A.max_ext + q) * A.dcap * A.T + (e - q * A.T);
     const int dn = A.denovo && cfg != 7, top = dn && cfg == 0 && !A.vcf;   // variant: 0 bi-allelic, 1 10-state, 2 top
+    if (G > 1 && dn) {
+      if (site != leaf_site) {
+        leaf_site = site;
+        switch (sig) {
+PARTS1        }
+      }
+      if (top) {
+        switch (sig) {
+PARTS3        }
+        continue;
+      }
+      if (MULTI && t + 3 <= G && it + 2 < nItems) {   // the site's three 10-state items at once (lanes over item x state)
+        const int ib = __builtin_amdgcn_readfirstlane(A.items[it + 1]), ic = __builtin_amdgcn_readfirstlane(A.items[it + 2]);
+        if ((ib >> 3) == site && (ic >> 3) == site && (ib & 7) != 0 && (ib & 7) != 7 && (ic & 7) != 0 && (ic & 7) != 7) {
+          int b1, b2, c1, c2;
+          cfg_alleles(ib & 7, r, &b1, &b2);
+          cfg_alleles(ic & 7, r, &c1, &c2);
+          const int G11 = g11 | gi(b1, b1) << 8 | gi(c1, c1) << 16, G12 = g12 | gi(b1, b2) << 8 | gi(c1, c2) << 16,
+                    G22 = g22 | gi(b2, b2) << 8 | gi(c2, c2) << 16;
+          const size_t ostr = (size_t)A.max_ext * A.dcap * A.T;
+          switch (sig) {
+PARTS4          }
+          t += 2;
+          continue;
+        }
+      }
+      switch (sig) {
+PARTS2      }
+      continue;
+    }
+    leaf_site = -1;   // (the other variants' layouts overlay the leaf prefix's partials)
     switch (sig * 3 + (top ? 2 : dn ? 1 : 0)) {
 )";
   k.replace(k.find("WSIZE"), 5, std::to_string(ws));
   for (size_t at; (at = k.find("WPB")) != std::string::npos;) k.replace(at, 3, std::to_string(wpb));
+  k.replace(k.find("MULTI"), 5, pps == 4 ? "true" : "false");
+  k.replace(k.find("WPEU"), 4, g_tr_regs ? "__attribute__((amdgpu_waves_per_eu(4)))" : "");
+  const std::string call = "(pl, A.np, P11, P12, P22, p0, g11, g12, g22, lk, t10, t10dn, tb, tr0, tr1, W, lane, out, A.T, A.dcap, 0); break;\n";
+  const std::string call3 = "(pl, A.np, P11, P12, P22, p0, G11, G12, G22, lk, t10, t10dn, tb, tr0, tr1, W, lane, out, A.T, A.dcap, ostr); break;\n";
+  for (int p = 1; p <= 4; p++) {
+    std::string cases;
+    for (size_t i = 0; p <= pps && pps * i + p - 1 < parts.size(); i++)
+      cases += "        case " + std::to_string(i) + ": " + parts[pps * i + p - 1] + (p == 4 ? call3 : call);
+    const std::string key = "PARTS" + std::to_string(p);
+    k.replace(k.find(key), key.size(), cases);
+  }
   s += k;
-  for (size_t i = 0; i < fns.size(); i++)
-    s += "      case " + std::to_string(i) + ": " + fns[i] +
-         "(pl, A.np, P11, P12, P22, p0, g11, g12, g22, lk, t10, t10dn, tb, tr0, tr1, W, lane, out, A.T, A.dcap); break;\n";
-  s += "    }\n  }\n}\n";
+  for (size_t i = 0; i < fns.size(); i++) s += "      case " + std::to_string(i) + ": " + fns[i] + call;
+  s += "    }\n    }\n  }\n}\n";
   return s;
 }
 
@@ -753,7 +906,13 @@ int pack_steps(const pm_pedigree* ped, int f, int ns, std::vector<int2>& out) {
 std::string generate(int chrom, const std::vector<Family>& fams, const double (*tba)[27], Kernel* out, bool denovo) {
   std::map<std::string, int> shape_of;
   for (auto& v : out->shape_ops) v.clear();
-  std::vector<std::string> names, bodies, post_names, post_bodies, wave_names, wave_bodies;
+  std::vector<std::string> names, bodies, post_names, post_bodies, wave_names, wave_bodies, part_names;
+  // --denovo, PM_ES_MULTI=1: a grouped task's three 10-state items in one pass of the wave (the default: one after the other;
+  // the three copies of the workspace cut the waves per CU from 14 to 6, and the kernel takes 1.95 ms instead of 1.16)
+  const char* em = getenv("PM_ES_MULTI");
+  const int pps = (em && em[0] == '1') ? 4 : 3;
+  const char* etr = getenv("PM_ES_TR");
+  g_tr_regs = etr && !strcmp(etr, "reg");
   int ws = 1;
   std::vector<std::pair<int, int>> order;   // (shape, index into fams)
   for (size_t i = 0; i < fams.size(); i++) {
@@ -764,7 +923,7 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
       id = (int)names.size();
       shape_of[key] = id;
       names.push_back("fam" + std::to_string(id));
-      double o3[3] = {0, 0, 0};
+      double o3[6] = {0, 0, 0, 0, 0, 0};
       if (!denovo) {
         bodies.push_back(gen_family(fams[i], chrom, tba, names.back(), &o3[0]));
         post_names.push_back("post" + std::to_string(id));
@@ -776,8 +935,16 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
           wave_bodies.push_back(gen_wave_family(fams[i], chrom, v == 0 ? 3 : 10, v == 2, wave_names.back(), &w, &o3[v]));
           ws = std::max(ws, w);
         }
+        for (int p = 1; p <= pps; p++) {   // the leaf prefix, the 10-state rest, the top rest, the 3-item rest (grouped tasks)
+          int w = 0;
+          double o = 0;
+          part_names.push_back("wfam" + std::to_string(id) + (p == 1 ? "_leaf" : p == 2 ? "_rest" : p == 3 ? "_toprest" : "_rest3"));
+          wave_bodies.push_back(gen_wave_family(fams[i], chrom, 10, p == 3, part_names.back(), &w, p < 4 ? &o3[2 + p] : &o, p == 1 ? 1 : 2,
+                                                p == 4 ? 3 : 1));
+          ws = std::max(ws, w);
+        }
       }
-      for (int v = 0; v < 3; v++) out->shape_ops[v].push_back(o3[v]);
+      for (int v = 0; v < 6; v++) out->shape_ops[v].push_back(o3[v]);
     } else id = it->second;
     order.push_back({id, (int)i});
   }
@@ -800,9 +967,10 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
   } else {
     // waves per block: as many workspace slices as fit the 64 KB of static LDS next to the tables
     const int tables = (256 + 6 * 27) * 8;
-    out->wpb = std::max(1, std::min(8, (64 * 1024 - tables) / (ws * 8)));
+    // (one wave per SIMD: the occupancy comes from blocks per CU, build() asks the runtime for them)
+    out->wpb = std::max(1, std::min(4, (64 * 1024 - tables) / (ws * 8)));
     if ((64 * 1024 - tables) / (ws * 8) < 1) out->wpb = 0;   // a family too large for one slice: the engine's generic kernel
-    std::string wk = gen_wave_kernel(wave_names, ws, std::max(1, out->wpb));
+    std::string wk = gen_wave_kernel(wave_names, part_names, pps, ws, std::max(1, out->wpb));
     const size_t at = wk.find("extern \"C\"");   // device helpers first, then the family functions, then the kernel
     src += wk.substr(0, at);
     for (auto& b : wave_bodies) src += b;
@@ -871,6 +1039,11 @@ bool build(int device, int chrom, const std::vector<Family>& fams, const double 
   if (!ok) {
     *err = "hipModuleGetFunction of the generated kernels failed";
     return false;
+  }
+  if (denovo) {   // resident blocks per CU (VGPRs and LDS): the launch's grid
+    int nb = 0;
+    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, out->fn, 64 * out->wpb, 0) != hipSuccess) nb = 0;
+    out->blocks_per_cu = nb;
   }
   out->compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return true;

@@ -38,7 +38,8 @@ struct Args {
   const double* T10;         // FamilyLikelihoodES::transmission [10][10][10] (es_hoist_wave)
   const double* T10dn;       // transmission_denovo
   const double* tba;         // transmission_BA tables [5][27]
-  int list, it0, it1, nslots, np, T, max_ext, dcap, vcf, res_words, res_a1, res_a2, denovo;
+  int list, it0, it1, nslots, np, T, max_ext, dcap, vcf, res_words, res_a1, res_a2, denovo,
+      group;                 // es_hoist_wave: items per task (the de novo items of one site share the leaf steps), 0/1 none
 };
 
 // Arguments of the generated posterior kernel es_post_jit (CalcPostProb_SingleExtendedPed_BA for every emitted row
@@ -65,9 +66,11 @@ struct Kernel {
   double compile_ms = 0;
   bool wave = false;         // --denovo: es_hoist_wave, one (item, family) per wave, blockDim = 64 wpb
   // FP64 operations of one (item, family) hoisting per shape, by variant: 0 bi-allelic, 1 10-state (de novo items),
-  // 2 top (the de novo monomorphism item); the bi-allelic engines fill variant 0 only
-  std::vector<double> shape_ops[3];
+  // 2 top (the de novo monomorphism item), 3 the leaf prefix of a grouped task, 4 / 5 its 10-state / top rest (3 + 4 ==
+  // 1, 3 + 5 == 2); the bi-allelic engines fill variant 0 only
+  std::vector<double> shape_ops[6];
   int wpb = 0, ws = 0;       // waves per block, workspace doubles per wave
+  int blocks_per_cu = 0;     // es_hoist_wave blocks resident per CU (the runtime's occupancy; 0 unknown)
 };
 
 // Packs family f's ES_Peeling schedule (pm_pedigree.steps) with its marriage-partial slots resolved the way the

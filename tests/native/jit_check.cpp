@@ -55,9 +55,15 @@ int main(int argc, char** argv) {
     std::string err;
     const auto t0 = std::chrono::steady_clock::now();
     if (!pmjit::compile(src, &code, &err)) { fprintf(stderr, "class %d: %s\n", cls, err.c_str()); return 1; }
+    if (!emit.empty() && cls == 0) {   // the code object too (register and LDS use: llvm-readelf --notes)
+      FILE* fh = fopen(((dn ? emit + ".dn" : emit) + ".co").c_str(), "wb");
+      if (fh) { fwrite(code.data(), 1, code.size(), fh); fclose(fh); }
+    }
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    printf("class %d shapes %d families %zu source %zu code %zu compile_ms %.0f%s\n", cls, K.n_shapes, fams.size(), src.size(),
-           code.size(), ms, dn ? (" denovo wpb " + std::to_string(K.wpb) + " ws " + std::to_string(K.ws)).c_str() : "");
+    std::string ops;   // FP64 operations per (item, family) of shape 0, by variant
+    for (int v = 0; v < 6; v++) ops += " " + std::to_string((long long)(K.shape_ops[v].empty() ? 0 : K.shape_ops[v][0]));
+    printf("class %d shapes %d families %zu source %zu code %zu compile_ms %.0f%s ops%s\n", cls, K.n_shapes, fams.size(), src.size(),
+           code.size(), ms, dn ? (" denovo wpb " + std::to_string(K.wpb) + " ws " + std::to_string(K.ws)).c_str() : "", ops.c_str());
   }
   return 0;
 }
