@@ -586,14 +586,14 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
     std::string b = "    const int o = " + PO(i) + " + x * " + S(capP[i]) + ";\n";
     for (int a = 0; a <= d; a++) b += "    W[o + " + S(a) + "] = 0.0;\n";
     if (NS == 3) {
-      b += "    const double pen = lk[(x == 0 ? P11 : x == 1 ? P12 : P22)[p0 + " + S(i) + "]];\n";
+      b += "    const double pen = PEN[(x == 0 ? g11 : x == 1 ? g12 : g22) * " + S(n) + " + " + S(i) + "];\n";
       if (yf) b += "    W[o] = 1.0;\n";
       else if (!fo) b += "    W[o] = pen;\n";
       else if (top) b += "    if (x == 0) W[o] = pen;\n";
       else if (d == 2) b += "    W[o + 2 - x] = x == 1 ? 2 * pen : pen;\n";
       else b += "    if (x != 1) W[o + (x == 0 ? 1 : 0)] = pen;\n";
     } else {
-      b += "    const double pen = lk[pl[(size_t)x * np + p0 + " + S(i) + "]];\n";
+      b += "    const double pen = PEN[x * " + S(n) + " + " + S(i) + "];\n";
       b += "    const int q = x == g11 ? 0 : x == g12 ? 1 : x == g22 ? 2 : 3;\n    (void)q;\n";
       if (!fo) b += "    W[o] = pen;\n";
       else if (top && dfull > 0) b += "    if (q == 0) W[o] = pen;\n";
@@ -750,12 +750,22 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
          "(const uint8_t* __restrict__ pl, size_t np, const uint8_t* __restrict__ P11, const uint8_t* __restrict__ P12, "
          "const uint8_t* __restrict__ P22, int p0, int gg11, int gg12, int gg22, const double* lk, const double* __restrict__ t10, "
          "const double* __restrict__ t10dn, const double* tb, const double* tr0, const double* tr1, double* W, int lane, "
-         "double* __restrict__ out, int os, int dcap, size_t ostr) {\n" + code + "}\n";
+         "double* __restrict__ out, int os, int dcap, size_t ostr, const double* PEN) {\n" + code + "}\n";
+}
+
+// The site's penetrances of a family, lk[pl[g][p0 + i]] for the 10 genotypes g, into the wave's LDS table PEN[g * n + i]
+// (one coalesced pass per (site, family) instead of a dependent global load per person and variant)
+std::string gen_pen_fill(int n, const std::string& name) {
+  const std::string N = std::to_string(n);
+  return "__device__ __forceinline__ void " + name + "(const uint8_t* __restrict__ pl, size_t np, int p0, const double* lk, double* PEN, "
+         "int lane) {\n  for (int e = lane; e < " + std::to_string(10 * n) + "; e += 64) {\n    const int g = e / " + N + ", i = e - g * " + N +
+         ";\n    PEN[e] = lk[pl[(size_t)g * np + p0 + i]];\n  }\n  wave_sync();\n}\n";
 }
 
 // fns: 3 variants per shape (bi-allelic, 10-state, top); parts: per shape the 10-state leaf prefix, the 10-state rest,
 // the top variant's rest and (pps == 4) the 10-state rest of three items at once
-std::string gen_wave_kernel(const std::vector<std::string>& fns, const std::vector<std::string>& parts, int pps, int ws, int wpb) {
+std::string gen_wave_kernel(const std::vector<std::string>& fns, const std::vector<std::string>& parts, const std::vector<std::string>& pens,
+                            int pps, int ws, int pensz, int wpb) {
   std::string s = R"(
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -766,12 +776,13 @@ __device__ __forceinline__ void wave_sync() {
   std::string k = R"(
 extern "C" __global__ void __launch_bounds__(64 * WPB) WPEU es_hoist_wave(Args A) {   // blockDim = 64 WPB
   __shared__ double lk[256], tb[6 * 27];
-  __shared__ double ws[WPB][WSIZE];
+  __shared__ double ws[WPB][WSIZE + PENSZ];
   for (int i = threadIdx.x; i < 256; i += blockDim.x) lk[i] = A.lktab[i];
   for (int i = threadIdx.x; i < 6 * 27; i += blockDim.x) tb[i] = i < 5 * 27 ? A.tba[i] : 1.0;
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   double* W = ws[wave];
+  double* PEN = W + WSIZE;   // the current (site, family)'s penetrances
   // the de novo transmission rows of this lane's marriage-partial pairs (lane, lane + 64), for every 10-state step
   double tr0[10], tr1[10];
 #pragma unroll
@@ -789,7 +800,7 @@ extern "C" __global__ void __launch_bounds__(64 * WPB) WPEU es_hoist_wave(Args A
   const long long units = ((long long)(nItems - A.it0) + G - 1) / G * A.nslots;
   for (long long u = (long long)blockIdx.x * WPB + wave; u < units; u += (long long)gridDim.x * WPB) {
     const int uq = (int)(u / A.nslots), k = (int)(u - (long long)uq * A.nslots);
-    int leaf_site = -1;
+    int leaf_site = -1, pen_site = -1;
     for (int t = 0; t < G; t++) {
     const int it = A.it0 + uq * G + t;
     if (it >= nItems) break;
@@ -808,6 +819,11 @@ extern "C" __global__ void __launch_bounds__(64 * WPB) WPEU es_hoist_wave(Args A
     const int sig = __builtin_amdgcn_readfirstlane(A.slot_sig[k]), p0 = __builtin_amdgcn_readfirstlane(A.slot_p0[k]);
     double* out = A.coef + ((size_t)(it - A.it0) * A.max_ext + q) * A.dcap * A.T + (e - q * A.T);
     const int dn = A.denovo && cfg != 7, top = dn && cfg == 0 && !A.vcf;   // variant: 0 bi-allelic, 1 10-state, 2 top
+    if (site != pen_site) {
+      pen_site = site;
+      switch (sig) {
+PENS      }
+    }
     if (G > 1 && dn) {
       if (site != leaf_site) {
         leaf_site = site;
@@ -841,12 +857,18 @@ PARTS2      }
     leaf_site = -1;   // (the other variants' layouts overlay the leaf prefix's partials)
     switch (sig * 3 + (top ? 2 : dn ? 1 : 0)) {
 )";
-  k.replace(k.find("WSIZE"), 5, std::to_string(ws));
+  for (size_t at; (at = k.find("WSIZE")) != std::string::npos;) k.replace(at, 5, std::to_string(ws));
+  k.replace(k.find("PENSZ"), 5, std::to_string(pensz));
+  {
+    std::string cases;
+    for (size_t i = 0; i < pens.size(); i++) cases += "        case " + std::to_string(i) + ": " + pens[i] + "(pl, A.np, p0, lk, PEN, lane); break;\n";
+    k.replace(k.find("PENS"), 4, cases);
+  }
   for (size_t at; (at = k.find("WPB")) != std::string::npos;) k.replace(at, 3, std::to_string(wpb));
   k.replace(k.find("MULTI"), 5, pps == 4 ? "true" : "false");
   k.replace(k.find("WPEU"), 4, g_tr_regs ? "__attribute__((amdgpu_waves_per_eu(4)))" : "");
-  const std::string call = "(pl, A.np, P11, P12, P22, p0, g11, g12, g22, lk, t10, t10dn, tb, tr0, tr1, W, lane, out, A.T, A.dcap, 0); break;\n";
-  const std::string call3 = "(pl, A.np, P11, P12, P22, p0, G11, G12, G22, lk, t10, t10dn, tb, tr0, tr1, W, lane, out, A.T, A.dcap, ostr); break;\n";
+  const std::string call = "(pl, A.np, P11, P12, P22, p0, g11, g12, g22, lk, t10, t10dn, tb, tr0, tr1, W, lane, out, A.T, A.dcap, 0, PEN); break;\n";
+  const std::string call3 = "(pl, A.np, P11, P12, P22, p0, G11, G12, G22, lk, t10, t10dn, tb, tr0, tr1, W, lane, out, A.T, A.dcap, ostr, PEN); break;\n";
   for (int p = 1; p <= 4; p++) {
     std::string cases;
     for (size_t i = 0; p <= pps && pps * i + p - 1 < parts.size(); i++)
@@ -906,7 +928,8 @@ int pack_steps(const pm_pedigree* ped, int f, int ns, std::vector<int2>& out) {
 std::string generate(int chrom, const std::vector<Family>& fams, const double (*tba)[27], Kernel* out, bool denovo) {
   std::map<std::string, int> shape_of;
   for (auto& v : out->shape_ops) v.clear();
-  std::vector<std::string> names, bodies, post_names, post_bodies, wave_names, wave_bodies, part_names;
+  std::vector<std::string> names, bodies, post_names, post_bodies, wave_names, wave_bodies, part_names, pen_names;
+  int pensz = 1;
   // --denovo, PM_ES_MULTI=1: a grouped task's three 10-state items in one pass of the wave (the default: one after the other;
   // the three copies of the workspace cut the waves per CU from 14 to 6, and the kernel takes 1.95 ms instead of 1.16)
   const char* em = getenv("PM_ES_MULTI");
@@ -929,6 +952,9 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
         post_names.push_back("post" + std::to_string(id));
         post_bodies.push_back(gen_post_family(fams[i], chrom, tba, post_names.back()));
       } else {   // variants 3 id + {0 bi-allelic, 1 10-state, 2 top}
+        pen_names.push_back("wfam" + std::to_string(id) + "_pen");
+        wave_bodies.push_back(gen_pen_fill(fams[i].n, pen_names.back()));
+        pensz = std::max(pensz, 10 * fams[i].n);
         for (int v = 0; v < 3; v++) {
           int w = 0;
           wave_names.push_back("wfam" + std::to_string(id) + "_" + std::to_string(v));
@@ -968,9 +994,9 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
     // waves per block: as many workspace slices as fit the 64 KB of static LDS next to the tables
     const int tables = (256 + 6 * 27) * 8;
     // (one wave per SIMD: the occupancy comes from blocks per CU, build() asks the runtime for them)
-    out->wpb = std::max(1, std::min(4, (64 * 1024 - tables) / (ws * 8)));
-    if ((64 * 1024 - tables) / (ws * 8) < 1) out->wpb = 0;   // a family too large for one slice: the engine's generic kernel
-    std::string wk = gen_wave_kernel(wave_names, part_names, pps, ws, std::max(1, out->wpb));
+    out->wpb = std::max(1, std::min(4, (64 * 1024 - tables) / ((ws + pensz) * 8)));
+    if ((64 * 1024 - tables) / ((ws + pensz) * 8) < 1) out->wpb = 0;   // a family too large for one slice: the engine's generic kernel
+    std::string wk = gen_wave_kernel(wave_names, part_names, pen_names, pps, ws, pensz, std::max(1, out->wpb));
     const size_t at = wk.find("extern \"C\"");   // device helpers first, then the family functions, then the kernel
     src += wk.substr(0, at);
     for (auto& b : wave_bodies) src += b;
