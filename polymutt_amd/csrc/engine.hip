@@ -65,6 +65,7 @@ struct pm_engine {
   int poly_ws = 0, poly_coef = 0, poly_dcap = 0;
   int hoist_tmp = 0, hoist_waves = 4, es_chunk = 0;   // k_es_hoist: step temporaries per wave, waves per block, items per launch
   double* d_es_coef = nullptr;                        // [es_chunk][max_ext][poly_dcap][T] hoisted coefficients
+  unsigned long long* d_es_prof = nullptr;            // PM_ES_PROF: es_hoist_wave cycles by part
   // the schedule compiler (es_jit.h): per plan (0, 1) and chromosome class, built on first use (0 untried, 1 ok, -1 failed)
   std::vector<int> ext_fam_h, ext_fam1_h, peel_start_h;
   std::vector<int2> steps_h;
@@ -267,6 +268,12 @@ extern "C" {
 void pm_engine_destroy(pm_engine* E) {
   if (!E) return;
   hipSetDevice(E->device);
+  if (E->d_es_prof) {
+    unsigned long long h[5] = {0, 0, 0, 0, 0};
+    if (hipMemcpy(h, E->d_es_prof, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess && (h[0] | h[1] | h[2] | h[3] | h[4]))
+      fprintf(stderr, "PM_ES_PROF wave-cycles pen %llu toprest %llu leaf %llu rest %llu whole %llu\n", h[0], h[1], h[2], h[3], h[4]);
+    (void)hipFree(E->d_es_prof);
+  }
   void* bufs[] = {E->d_units1, E->d_ext_count1, E->d_ext_fam1, E->d_fam_founders, E->d_peel_start, E->d_ext_count, E->d_ext_fam, E->d_is_founder, E->d_steps, E->d_T10,
                   E->d_T10dn, E->d_ws, E->d_tba, E->d_units_q, E->d_poly_start, E->d_poly_lay, E->d_poly_deg, E->d_es_coef, E->d_es_pers, E->d_es_pers1, E->d_fam_perm,
                   E->d_fam_start, E->d_fam_kind, E->d_fa, E->d_mo, E->d_sex, E->d_units, E->d_lktab, E->d_M, E->d_syn,
@@ -952,6 +959,14 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
         J.denovo = A.denovo;
         // a site's de novo items are consecutive in lists 0 (cfgs 0-3, or 1-3 when k_prep / the QUAD item takes the
         // monomorphism) and 1 (cfgs 4-6): one task takes them together, the 10-state leaf steps once
+        J.prof = nullptr;
+        if (getenv("PM_ES_PROF")) {
+          if (!E->d_es_prof) {
+            if (int r = dalloc(&E->d_es_prof, 5)) return r;
+            HIP_TRY(hipMemset(E->d_es_prof, 0, 5 * sizeof(unsigned long long)));
+          }
+          J.prof = E->d_es_prof;
+        }
         J.group = 0;
         if (K->wave && A.denovo && !A.vcf && !getenv("PM_ES_NOGROUP")) {
           if (list == 0) J.group = A.mono_dn ? 3 : 4;

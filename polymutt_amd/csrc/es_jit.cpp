@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <mutex>
 #include "../../include/polymutt_engine.h"
@@ -192,7 +193,7 @@ typedef unsigned char uint8_t;
 struct Args {
   const int* items; const int* counts; const uint8_t* ref; const int* res; const uint8_t* pl; const double* lktab;
   double* coef; const int* slot_e; const int* slot_sig; const int* slot_p0;
-  const double* T10; const double* T10dn; const double* tba;
+  const double* T10; const double* T10dn; const double* tba; unsigned long long* prof;
   int list, it0, it1, nslots, np, T, max_ext, dcap, vcf, res_words, res_a1, res_a2, denovo, group;
 };
 __device__ __forceinline__ int gi(int b1, int b2) {
@@ -445,6 +446,8 @@ extern "C" __global__ void __launch_bounds__(256) es_post_jit(PostArgs A) {
 // The de novo transmission rows of a type-1 step's pairs: from the (cache-resident) global table, or held in 20
 // registers for the whole kernel (PM_ES_TR=reg: 149 VGPRs, 3 waves per SIMD; capped at 128 with 19 spilled)
 bool g_tr_regs = false;
+bool g_prof = false;
+bool g_pack = true;    // PM_ES_PACK=0: independent type-2 steps one phase each   // PM_ES_PROF=1: es_hoist_wave accumulates per-part clock cycles into Args::prof
 
 struct WaveGen {
   std::string code;
@@ -558,7 +561,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
   *ws_doubles = LSZ + M * NSZ;
   auto S = [](long v) { return std::to_string(v); };
   const std::string nsS = S(NS), nsq = S(NS * NS), R = S((NS * NS + 63) / 64);
-  const bool mc = part == 2;   // offsets of the item's own regions carry cb
+  const bool mc = part == 2 && M > 1;   // offsets of the item's own regions carry cb (several items per call)
   auto PO = [&](int i) { return mc && !leafp[i] ? "(" + S(po[i]) + " + cb)" : S(po[i]); };
   auto MOf = [&](int s) { return mc && !leafs.count(s) ? "(" + S(mo[s]) + " + cb)" : S(mo[s]); };
   const std::string TBs = mc ? "(" + S(TB) + " + cb)" : S(TB);
@@ -614,11 +617,13 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
   size_t si = 0;
   int fin = -1;
   double nops = 0;
+  std::vector<char> done(nst, 0);
   for (const int2& St : F.steps) {
     const int kstep = (int)si;
     const StepDeg g = sd[si++];
     fin = (St.x >> 24) & 255;
     if ((part == 1 && !leaf[kstep]) || (part == 2 && leaf[kstep])) continue;
+    const bool emitted = done[kstep];   // (in a fused run of type-1 steps: counted here, emitted with the run's first)
     {   // this step's FP64 operations (per item)
       const int type = St.x & 255, slot = (St.y >> 8) & 255, create = (St.y >> 16) & 1;
       const double ns = NS;
@@ -634,6 +639,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
     }
     const int type = St.x & 255, from0 = (St.x >> 8) & 255, from1 = (St.x >> 16) & 255, to0 = (St.x >> 24) & 255;
     const int slot = (St.y >> 8) & 255, create = (St.y >> 16) & 1, fa2mo = (St.y >> 17) & 1;
+    if (emitted) continue;
     if (type == 1) {   // lanes over the pairs e: S(e) = sum_k T(e, k) P_off[k] in registers, then M(e) *= S(e) in place
       const int off_ = from0, csex = F.sex[off_], pcap = capP[off_], mcap = capM[slot];
       std::string b = "      double s[" + S(g.a + 1) + "];\n";
@@ -656,11 +662,131 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
           b += "      W[" + me + " + " + S(a) + "] = " + acc + ";\n";
         }
       }
+      if (NS == 10 && !mc) {
+        // a run of consecutive type-1 steps (this part's; they only read offspring partials and their own marriage
+        // partial) is one phase: lanes over both pairs (lane, lane + 64 < 100), one pass over k for every step of
+        // the run (each offspring coefficient read from LDS once for the two pairs: wave-uniform broadcasts), then per
+        // marriage partial the steps' products chained in registers and one write -- the same operations in the
+        // same order as step by step
+        std::vector<int> run;
+        for (int k2 = kstep; k2 < nst; k2++) {
+          if ((part == 1 && !leaf[k2]) || (part == 2 && leaf[k2])) continue;
+          if ((F.steps[k2].x & 255) != 1) break;
+          run.push_back(k2);
+        }
+        for (int k2 : run) done[k2] = 1;
+        std::string c1 = "  {\n    const int e1 = lane + 64, e1c = e1 < 100 ? e1 : lane;\n";
+        for (size_t q = 0; q < run.size(); q++) {
+          const int ga = sd[run[q]].a;
+          c1 += "    double s0_" + S(q) + "[" + S(ga + 1) + "], s1_" + S(q) + "[" + S(ga + 1) + "];\n";
+          for (int a = 0; a <= ga; a++) c1 += "    s0_" + S(q) + "[" + S(a) + "] = 0.0;\n    s1_" + S(q) + "[" + S(a) + "] = 0.0;\n";
+        }
+        // (k unrolled by 2 only: fully unrolled, the scheduler hoists every offspring coefficient's LDS read and
+        // spills)
+        c1 += "#pragma unroll 2\n    for (int k = 0; k < 10; k++) {\n";
+        c1 += g_tr_regs ? "      const double t0 = tr0[k], t1 = tr1[k];\n"
+                        : "      const double t0 = t10dn[lane * 10 + k], t1 = t10dn[e1c * 10 + k];\n";
+        for (size_t q = 0; q < run.size(); q++) {
+          const int2 Sq = F.steps[run[q]];
+          const int offq = (Sq.x >> 8) & 255, ga = sd[run[q]].a;
+          for (int a = 0; a <= ga; a++)
+            c1 += "      {\n        const double p = W[" + PO(offq) + " + k * " + S(capP[offq]) + " + " + S(a) + "];\n        s0_" + S(q) + "[" + S(a) +
+                  "] = fma(t0, p, s0_" + S(q) + "[" + S(a) + "]);\n        s1_" + S(q) + "[" + S(a) + "] = fma(t1, p, s1_" + S(q) + "[" + S(a) + "]);\n      }\n";
+        }
+        c1 += "    }\n";
+        // per pair: the marriage partials in the run's order of first use, each chained through its steps
+        std::vector<int> slots;
+        for (int k2 : run) {
+          const int sl2 = (F.steps[k2].y >> 8) & 255;
+          if (std::find(slots.begin(), slots.end(), sl2) == slots.end()) slots.push_back(sl2);
+        }
+        for (int pr = 0; pr < 2; pr++) {
+          const std::string sp = pr ? "s1_" : "s0_", e = pr ? "e1" : "lane";
+          c1 += pr ? "    if (e1 < 100) {\n" : "    {\n";
+          int cid = 0;
+          for (int sl2 : slots) {
+            const std::string mev = MOf(sl2) + " + " + e + " * " + S(capM[sl2]);
+            std::string cur;   // the register array holding the slot's current coefficients
+            int dcur = -1;
+            for (size_t q = 0; q < run.size(); q++) {
+              const int2 Sq = F.steps[run[q]];
+              if (((Sq.y >> 8) & 255) != sl2) continue;
+              const int ga = sd[run[q]].a, gb = sd[run[q]].b, cr = (Sq.y >> 16) & 1;
+              const std::string sq = sp + S(q);
+              if (cr) { cur = sq; dcur = ga; continue; }
+              if (dcur < 0) {   // the slot's coefficients so far, from LDS
+                cur = "m" + S(pr) + "_" + S(cid++);
+                c1 += "      double " + cur + "[" + S(gb + 1) + "];\n";
+                for (int c = 0; c <= gb; c++) c1 += "      " + cur + "[" + S(c) + "] = W[" + mev + " + " + S(c) + "];\n";
+                dcur = gb;
+              }
+              const std::string nx = "m" + S(pr) + "_" + S(cid++);
+              c1 += "      double " + nx + "[" + S(ga + gb + 1) + "];\n";
+              for (int a = 0; a <= ga + gb; a++) {
+                std::string acc;
+                for (int c = std::max(0, a - ga); c <= std::min(a, gb); c++)
+                  acc = acc.empty() ? cur + "[" + S(c) + "] * " + sq + "[" + S(a - c) + "]"
+                                    : "fma(" + cur + "[" + S(c) + "], " + sq + "[" + S(a - c) + "], " + acc + ")";
+                c1 += "      " + nx + "[" + S(a) + "] = " + acc + ";\n";
+              }
+              cur = nx;
+              dcur = ga + gb;
+            }
+            for (int a = 0; a <= dcur; a++) c1 += "      W[" + mev + " + " + S(a) + "] = " + cur + "[" + S(a) + "];\n";
+          }
+          c1 += "    }\n";
+        }
+        c1 += "  }\n  wave_sync();\n";
+        code += c1;
+      } else
       code += "#pragma unroll\n  for (int r = 0; r < " + R + "; r++) {\n    const int e = lane + 64 * r;\n    if (e < " + nsq + ") {\n" + items(b) +
               "    }\n  }\n  wave_sync();\n";
     } else if (type == 2) {   // lanes over i: S(i) = sum_j P_from[j] M(j, i) in registers, then P_to[i] *= S(i) in place
       const int sf = from0, stt = to0, fcap = capP[sf], tcap = capP[stt];
       const int ds = g.a + g.b;
+      // independent type-2 steps of one shape that follow this one (this part's): one phase, 16 lanes per step, the
+      // lane's step selecting its partials' offsets
+      std::vector<int> run{kstep};
+      if (NS == 10 && !mc && g_pack) {
+        auto sig2 = [&](int k2) {
+          const int2 Q = F.steps[k2];
+          const int f2 = (Q.x >> 8) & 255, t2 = (Q.x >> 24) & 255, s2 = (Q.y >> 8) & 255;
+          return std::vector<int>{pristine[k2], sd[k2].a, sd[k2].b, sd[k2].c, s2 == 255, capP[f2], capP[t2], s2 == 255 ? 0 : capM[s2],
+                                  d0[f2]};
+        };
+        const std::vector<int> sg0 = sig2(kstep);
+        for (int k2 = kstep + 1; k2 < nst && run.size() < 4; k2++) {
+          if ((part == 1 && !leaf[k2]) || (part == 2 && leaf[k2])) continue;
+          const int2 Q = F.steps[k2];
+          if ((Q.x & 255) != 2 || sig2(k2) != sg0) break;
+          const int f2 = (Q.x >> 8) & 255, t2 = (Q.x >> 24) & 255;
+          bool indep = true;
+          for (int k3 : run) {
+            const int f3 = (F.steps[k3].x >> 8) & 255, t3 = (F.steps[k3].x >> 24) & 255;
+            if (t2 == t3 || f2 == t3 || f3 == t2) indep = false;
+          }
+          if (!indep) break;
+          run.push_back(k2);
+        }
+      }
+      std::string OF = PO(sf), OT = PO(stt), OM = slot == 255 ? "" : MOf(slot), pre;
+      if (run.size() > 1) {
+        auto sel = [&](const std::function<std::string(int)>& f) {
+          std::string e = f(run.back());
+          for (int q = (int)run.size() - 2; q >= 0; q--) e = "q_ == " + S(q) + " ? " + f(run[q]) + " : " + e;
+          return e;
+        };
+        pre = "      const int of_ = " + sel([&](int k2) { return PO((F.steps[k2].x >> 8) & 255); }) +
+              ";\n      const int ot_ = " + sel([&](int k2) { return PO((F.steps[k2].x >> 24) & 255); }) + ";\n";
+        if (slot != 255) {   // (and the marriage partial's orientation: M(i, j) or M(j, i))
+          pre += "      const int om_ = " + sel([&](int k2) { return MOf((F.steps[k2].y >> 8) & 255); }) + ";\n";
+          pre += "      const int si_ = " + sel([&](int k2) { return std::string((F.steps[k2].y >> 17) & 1 ? "1" : nsS); }) + ", sj_ = " +
+                 sel([&](int k2) { return std::string((F.steps[k2].y >> 17) & 1 ? nsS : "1"); }) + ";\n";
+        }
+        OF = "of_"; OT = "ot_"; OM = "om_";
+        for (int k2 : run) done[k2] = 1;
+      }
+
       std::string b = "    double s[" + S(ds + 1) + "];\n";
       for (int a = 0; a <= ds; a++) b += "    s[" + S(a) + "] = 0.0;\n";
       if (pristine[kstep]) {
@@ -670,45 +796,48 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
         // bit-identical to the dense sum (q in the dense loop's coefficient order u = 0, 1, 2 at one j, should two of
         // the genotypes coincide)
         const int d = d0[sf];
-        b += "#pragma unroll\n    for (int j = 0; j < " + nsS + "; j++) {\n";
+        b += std::string(run.size() > 1 ? "#pragma unroll 2" : "#pragma unroll") + "\n    for (int j = 0; j < " + nsS + "; j++) {\n";
         const std::string gq[3] = {"g11", "g12", "g22"};
         for (int q = 2; q >= 0; q--) {
           if (d == 1 && q == 1) continue;
           const int u = d == 2 ? 2 - q : d == 1 ? (q == 0 ? 1 : 0) : 0;
-          b += "      if (j == " + gq[q] + ") {\n        const double f = W[" + PO(sf) + " + j * " + S(fcap) + " + " + S(u) + "];\n";
+          b += "      if (j == " + gq[q] + ") {\n        const double f = W[" + OF + " + j * " + S(fcap) + " + " + S(u) + "];\n";
           if (slot == 255) b += "        s[" + S(u) + "] += f;\n";
           else {
             const int mcap = capM[slot];
-            const std::string me = fa2mo ? "(j * " + nsS + " + i)" : "(i * " + nsS + " + j)";
+            const std::string me = run.size() > 1 ? "(i * si_ + j * sj_)" : fa2mo ? "(j * " + nsS + " + i)" : "(i * " + nsS + " + j)";
             for (int v = 0; v <= g.b; v++)
-              b += "        s[" + S(u + v) + "] = fma(f, W[" + MOf(slot) + " + " + me + " * " + S(mcap) + " + " + S(v) + "], s[" + S(u + v) + "]);\n";
+              b += "        s[" + S(u + v) + "] = fma(f, W[" + OM + " + " + me + " * " + S(mcap) + " + " + S(v) + "], s[" + S(u + v) + "]);\n";
           }
           b += "      }\n";
         }
         b += "    }\n";
       } else if (slot == 255) {
         for (int a = 0; a <= ds; a++)
-          b += "#pragma unroll\n    for (int j = 0; j < " + nsS + "; j++) s[" + S(a) + "] += W[" + PO(sf) + " + j * " + S(fcap) + " + " +
+          b += "#pragma unroll\n    for (int j = 0; j < " + nsS + "; j++) s[" + S(a) + "] += W[" + OF + " + j * " + S(fcap) + " + " +
                S(a) + "];\n";
       } else {
         const int mcap = capM[slot];
-        const std::string me = fa2mo ? "(j * " + nsS + " + i)" : "(i * " + nsS + " + j)";
-        b += "#pragma unroll\n    for (int j = 0; j < " + nsS + "; j++) {\n";
-        for (int u = 0; u <= g.a; u++) b += "      const double f" + S(u) + " = W[" + PO(sf) + " + j * " + S(fcap) + " + " + S(u) + "];\n";
-        for (int v = 0; v <= g.b; v++) b += "      const double g" + S(v) + " = W[" + MOf(slot) + " + " + me + " * " + S(mcap) + " + " + S(v) + "];\n";
+        const std::string me = run.size() > 1 ? "(i * si_ + j * sj_)" : fa2mo ? "(j * " + nsS + " + i)" : "(i * " + nsS + " + j)";
+        b += std::string(run.size() > 1 ? "#pragma unroll 2" : "#pragma unroll") + "\n    for (int j = 0; j < " + nsS + "; j++) {\n";
+        for (int u = 0; u <= g.a; u++) b += "      const double f" + S(u) + " = W[" + OF + " + j * " + S(fcap) + " + " + S(u) + "];\n";
+        for (int v = 0; v <= g.b; v++) b += "      const double g" + S(v) + " = W[" + OM + " + " + me + " * " + S(mcap) + " + " + S(v) + "];\n";
         for (int u = 0; u <= g.a; u++)
           for (int v = 0; v <= g.b; v++) b += "      s[" + S(u + v) + "] = fma(f" + S(u) + ", g" + S(v) + ", s[" + S(u + v) + "]);\n";
         b += "    }\n";
       }
       b += "    double t[" + S(g.c + 1) + "];\n";
-      for (int c = 0; c <= g.c; c++) b += "    t[" + S(c) + "] = W[" + PO(stt) + " + i * " + S(tcap) + " + " + S(c) + "];\n";
+      for (int c = 0; c <= g.c; c++) b += "    t[" + S(c) + "] = W[" + OT + " + i * " + S(tcap) + " + " + S(c) + "];\n";
       for (int a = 0; a <= g.c + ds; a++) {
         std::string acc;
         for (int c = std::max(0, a - ds); c <= std::min(a, g.c); c++)
           acc = acc.empty() ? "t[" + S(c) + "] * s[" + S(a - c) + "]" : "fma(t[" + S(c) + "], s[" + S(a - c) + "], " + acc + ")";
-        b += "    W[" + PO(stt) + " + i * " + S(tcap) + " + " + S(a) + "] = " + acc + ";\n";
+        b += "    W[" + OT + " + i * " + S(tcap) + " + " + S(a) + "] = " + acc + ";\n";
       }
-      code += lanes(NS, "i", b) + "  wave_sync();\n";
+      if (run.size() > 1)
+        code += "  {\n    const int q_ = lane >> 4, i = lane & 15;\n    if (q_ < " + S(run.size()) + " && i < " + nsS + ") {\n" + pre + b +
+                "    }\n  }\n  wave_sync();\n";
+      else code += lanes(NS, "i", b) + "  wave_sync();\n";
     } else {   // W(e) = P_fa[i] M(e) P_mo[j] -> LDS; lanes over k: S(k) = sum_e T(e, k) W(e), P_off[k] *= S(k) in place
       const int fa = from0, mo_ = from1, off_ = to0, csex = F.sex[off_];
       const int dw = g.a + g.b + g.c, ww = dw + 1;
@@ -792,6 +921,9 @@ extern "C" __global__ void __launch_bounds__(64 * WPB) WPEU es_hoist_wave(Args A
   }
   const double* t10 = A.T10;
   const double* t10dn = A.T10dn;
+  // PM_ES_PROF=1: clock cycles per wave in the pen fill, top rest, leaf prefix, 10-state rest and whole variants
+  unsigned long long pc[5] = {0, 0, 0, 0, 0};
+#define PCLK(c) if (PROF) { const unsigned long long t1_ = __builtin_readcyclecounter(); pc[c] += t1_ - tq; tq = t1_; }
   const int nItems = min(A.counts[A.list], A.it1);
   if (nItems <= A.it0) return;
   // a task: G consecutive items of the list -- with A.group, the de novo items of one site (list 0: cfgs 0-3, list 1:
@@ -801,6 +933,7 @@ extern "C" __global__ void __launch_bounds__(64 * WPB) WPEU es_hoist_wave(Args A
   for (long long u = (long long)blockIdx.x * WPB + wave; u < units; u += (long long)gridDim.x * WPB) {
     const int uq = (int)(u / A.nslots), k = (int)(u - (long long)uq * A.nslots);
     int leaf_site = -1, pen_site = -1;
+    unsigned long long tq = PROF ? __builtin_readcyclecounter() : 0;
     for (int t = 0; t < G; t++) {
     const int it = A.it0 + uq * G + t;
     if (it >= nItems) break;
@@ -823,16 +956,19 @@ extern "C" __global__ void __launch_bounds__(64 * WPB) WPEU es_hoist_wave(Args A
       pen_site = site;
       switch (sig) {
 PENS      }
+      PCLK(0);
     }
     if (G > 1 && dn) {
       if (site != leaf_site) {
         leaf_site = site;
         switch (sig) {
 PARTS1        }
+        PCLK(2);
       }
       if (top) {
         switch (sig) {
 PARTS3        }
+        PCLK(1);
         continue;
       }
       if (MULTI && t + 3 <= G && it + 2 < nItems) {   // the site's three 10-state items at once (lanes over item x state)
@@ -846,12 +982,14 @@ PARTS3        }
           const size_t ostr = (size_t)A.max_ext * A.dcap * A.T;
           switch (sig) {
 PARTS4          }
+          PCLK(3);
           t += 2;
           continue;
         }
       }
       switch (sig) {
 PARTS2      }
+      PCLK(3);
       continue;
     }
     leaf_site = -1;   // (the other variants' layouts overlay the leaf prefix's partials)
@@ -866,7 +1004,7 @@ PARTS2      }
   }
   for (size_t at; (at = k.find("WPB")) != std::string::npos;) k.replace(at, 3, std::to_string(wpb));
   k.replace(k.find("MULTI"), 5, pps == 4 ? "true" : "false");
-  k.replace(k.find("WPEU"), 4, g_tr_regs ? "__attribute__((amdgpu_waves_per_eu(4)))" : "");
+  k.replace(k.find("WPEU"), 4, "__attribute__((amdgpu_waves_per_eu(4)))");   // (<= 128 VGPRs: 4 waves per SIMD)
   const std::string call = "(pl, A.np, P11, P12, P22, p0, g11, g12, g22, lk, t10, t10dn, tb, tr0, tr1, W, lane, out, A.T, A.dcap, 0, PEN); break;\n";
   const std::string call3 = "(pl, A.np, P11, P12, P22, p0, G11, G12, G22, lk, t10, t10dn, tb, tr0, tr1, W, lane, out, A.T, A.dcap, ostr, PEN); break;\n";
   for (int p = 1; p <= 4; p++) {
@@ -878,7 +1016,8 @@ PARTS2      }
   }
   s += k;
   for (size_t i = 0; i < fns.size(); i++) s += "      case " + std::to_string(i) + ": " + fns[i] + call;
-  s += "    }\n    }\n  }\n}\n";
+  s += "    }\n    PCLK(4);\n    }\n  }\n  if (PROF && lane == 0)\n    for (int c = 0; c < 5; c++) atomicAdd(A.prof + c, pc[c]);\n}\n";
+  for (size_t at; (at = s.find("PROF")) != std::string::npos;) s.replace(at, 4, g_prof ? "true" : "false");
   return s;
 }
 
@@ -936,6 +1075,10 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
   const int pps = (em && em[0] == '1') ? 4 : 3;
   const char* etr = getenv("PM_ES_TR");
   g_tr_regs = etr && !strcmp(etr, "reg");
+  const char* epf = getenv("PM_ES_PROF");
+  g_prof = epf && epf[0] == '1';
+  const char* epk = getenv("PM_ES_PACK");
+  g_pack = !(epk && epk[0] == '0');
   int ws = 1;
   std::vector<std::pair<int, int>> order;   // (shape, index into fams)
   for (size_t i = 0; i < fams.size(); i++) {

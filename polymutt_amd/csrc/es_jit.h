@@ -38,6 +38,7 @@ struct Args {
   const double* T10;         // FamilyLikelihoodES::transmission [10][10][10] (es_hoist_wave)
   const double* T10dn;       // transmission_denovo
   const double* tba;         // transmission_BA tables [5][27]
+  unsigned long long* prof;  // [5] PM_ES_PROF clock cycles (es_hoist_wave)
   int list, it0, it1, nslots, np, T, max_ext, dcap, vcf, res_words, res_a1, res_a2, denovo,
       group;                 // es_hoist_wave: items per task (the de novo items of one site share the leaf steps), 0/1 none
 };
