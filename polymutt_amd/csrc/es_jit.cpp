@@ -447,7 +447,8 @@ extern "C" __global__ void __launch_bounds__(256) es_post_jit(PostArgs A) {
 // registers for the whole kernel (PM_ES_TR=reg: 149 VGPRs, 3 waves per SIMD; capped at 128 with 19 spilled)
 bool g_tr_regs = false;
 bool g_prof = false;
-bool g_pack = true;    // PM_ES_PACK=0: independent type-2 steps one phase each   // PM_ES_PROF=1: es_hoist_wave accumulates per-part clock cycles into Args::prof
+bool g_pack = true;
+int g_expt = 0;        // PM_ES_EXPT=1: timing experiments only (results wrong), see the uses    // PM_ES_PACK=0: independent type-2 steps one phase each   // PM_ES_PROF=1: es_hoist_wave accumulates per-part clock cycles into Args::prof
 
 struct WaveGen {
   std::string code;
@@ -684,8 +685,9 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
         // (k unrolled by 2 only: fully unrolled, the scheduler hoists every offspring coefficient's LDS read and
         // spills)
         c1 += "#pragma unroll 2\n    for (int k = 0; k < 10; k++) {\n";
-        c1 += g_tr_regs ? "      const double t0 = tr0[k], t1 = tr1[k];\n"
-                        : "      const double t0 = t10dn[lane * 10 + k], t1 = t10dn[e1c * 10 + k];\n";
+        c1 += g_expt == 1 ? "      const double t0 = 0.001 * k, t1 = 0.002 * k;\n"   // (timing experiment only: wrong values)
+              : g_tr_regs ? "      const double t0 = tr0[k], t1 = tr1[k];\n"
+                          : "      const double t0 = t10dn[lane * 10 + k], t1 = t10dn[e1c * 10 + k];\n";
         for (size_t q = 0; q < run.size(); q++) {
           const int2 Sq = F.steps[run[q]];
           const int offq = (Sq.x >> 8) & 255, ga = sd[run[q]].a;
@@ -894,7 +896,8 @@ std::string gen_pen_fill(int n, const std::string& name) {
 // fns: 3 variants per shape (bi-allelic, 10-state, top); parts: per shape the 10-state leaf prefix, the 10-state rest,
 // the top variant's rest and (pps == 4) the 10-state rest of three items at once
 std::string gen_wave_kernel(const std::vector<std::string>& fns, const std::vector<std::string>& parts, const std::vector<std::string>& pens,
-                            int pps, int ws, int pensz, int wpb) {
+                            const std::vector<int>& shape_ns, int pps, int ws, int pensz, int wpb) {
+  const int npf = pensz <= 4 * 64 ? (pensz + 63) / 64 : 0;   // prefetch registers per lane (0: families too large)
   std::string s = R"(
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -902,6 +905,9 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 )";
+  s += "__device__ __forceinline__ int shape_n(int sig) {\n  switch (sig) {\n";
+  for (size_t i = 0; i < shape_ns.size(); i++) s += "    case " + std::to_string(i) + ": return " + std::to_string(shape_ns[i]) + ";\n";
+  s += "  }\n  return 0;\n}\n";
   std::string k = R"(
 extern "C" __global__ void __launch_bounds__(64 * WPB) WPEU es_hoist_wave(Args A) {   // blockDim = 64 WPB
   __shared__ double lk[256], tb[6 * 27];
@@ -930,6 +936,28 @@ extern "C" __global__ void __launch_bounds__(64 * WPB) WPEU es_hoist_wave(Args A
   // cfgs 4-6), whose 10-state leaf steps are taken once per (site, family) -- on one family
   const int G = A.group > 1 ? A.group : 1;
   const long long units = ((long long)(nItems - A.it0) + G - 1) / G * A.nslots;
+  // the next task's penetrance bytes are loaded while this one is computed (NPF per lane: 10 n <= 64 NPF)
+  unsigned pb[NPF > 0 ? NPF : 1];
+  long long pf_u = -1;   // the task whose bytes pb holds
+  auto prefetch = [&](long long uu) {
+    pf_u = -1;
+    if (NPF == 0 || uu >= units) return;
+    const int uqn = (int)(uu / A.nslots), kn = (int)(uu - (long long)uqn * A.nslots);
+    const int itn = A.it0 + uqn * G;
+    if (itn >= nItems) return;
+    const int sn = __builtin_amdgcn_readfirstlane(A.items[itn]) >> 3;
+    const int p0n = __builtin_amdgcn_readfirstlane(A.slot_p0[kn]);
+    const int nn = shape_n(__builtin_amdgcn_readfirstlane(A.slot_sig[kn]));
+    if (10 * nn > 64 * NPF) return;
+    const uint8_t* pln = A.pl + (size_t)sn * A.np * 10 + p0n;
+#pragma unroll
+    for (int r = 0; r < (NPF > 0 ? NPF : 1); r++) {
+      const int e = lane + 64 * r, g = e / nn;
+      pb[r] = e < 10 * nn ? pln[(size_t)g * A.np + (e - g * nn)] : 0;
+    }
+    pf_u = uu;
+  };
+  prefetch((long long)blockIdx.x * WPB + wave);
   for (long long u = (long long)blockIdx.x * WPB + wave; u < units; u += (long long)gridDim.x * WPB) {
     const int uq = (int)(u / A.nslots), k = (int)(u - (long long)uq * A.nslots);
     int leaf_site = -1, pen_site = -1;
@@ -953,9 +981,18 @@ extern "C" __global__ void __launch_bounds__(64 * WPB) WPEU es_hoist_wave(Args A
     double* out = A.coef + ((size_t)(it - A.it0) * A.max_ext + q) * A.dcap * A.T + (e - q * A.T);
     const int dn = A.denovo && cfg != 7, top = dn && cfg == 0 && !A.vcf;   // variant: 0 bi-allelic, 1 10-state, 2 top
     if (site != pen_site) {
+      if (pf_u == u && t == 0) {   // the prefetched bytes (this task's first item)
+        const int nn = shape_n(sig);
+#pragma unroll
+        for (int r = 0; r < (NPF > 0 ? NPF : 1); r++)
+          if (lane + 64 * r < 10 * nn) PEN[lane + 64 * r] = lk[pb[r]];
+        wave_sync();
+        prefetch(u + (long long)gridDim.x * WPB);
+      } else {
+        switch (sig) {
+PENS        }
+      }
       pen_site = site;
-      switch (sig) {
-PENS      }
       PCLK(0);
     }
     if (G > 1 && dn) {
@@ -997,6 +1034,7 @@ PARTS2      }
 )";
   for (size_t at; (at = k.find("WSIZE")) != std::string::npos;) k.replace(at, 5, std::to_string(ws));
   k.replace(k.find("PENSZ"), 5, std::to_string(pensz));
+  for (size_t at; (at = k.find("NPF")) != std::string::npos;) k.replace(at, 3, std::to_string(npf));
   {
     std::string cases;
     for (size_t i = 0; i < pens.size(); i++) cases += "        case " + std::to_string(i) + ": " + pens[i] + "(pl, A.np, p0, lk, PEN, lane); break;\n";
@@ -1069,6 +1107,7 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
   for (auto& v : out->shape_ops) v.clear();
   std::vector<std::string> names, bodies, post_names, post_bodies, wave_names, wave_bodies, part_names, pen_names;
   int pensz = 1;
+  std::vector<int> shape_ns;   // persons per shape
   // --denovo, PM_ES_MULTI=1: a grouped task's three 10-state items in one pass of the wave (the default: one after the other;
   // the three copies of the workspace cut the waves per CU from 14 to 6, and the kernel takes 1.95 ms instead of 1.16)
   const char* em = getenv("PM_ES_MULTI");
@@ -1079,6 +1118,8 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
   g_prof = epf && epf[0] == '1';
   const char* epk = getenv("PM_ES_PACK");
   g_pack = !(epk && epk[0] == '0');
+  const char* eex = getenv("PM_ES_EXPT");
+  g_expt = eex ? atoi(eex) : 0;
   int ws = 1;
   std::vector<std::pair<int, int>> order;   // (shape, index into fams)
   for (size_t i = 0; i < fams.size(); i++) {
@@ -1096,6 +1137,7 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
         post_bodies.push_back(gen_post_family(fams[i], chrom, tba, post_names.back()));
       } else {   // variants 3 id + {0 bi-allelic, 1 10-state, 2 top}
         pen_names.push_back("wfam" + std::to_string(id) + "_pen");
+        shape_ns.push_back(fams[i].n);
         wave_bodies.push_back(gen_pen_fill(fams[i].n, pen_names.back()));
         pensz = std::max(pensz, 10 * fams[i].n);
         for (int v = 0; v < 3; v++) {
@@ -1139,7 +1181,7 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
     // (one wave per SIMD: the occupancy comes from blocks per CU, build() asks the runtime for them)
     out->wpb = std::max(1, std::min(4, (64 * 1024 - tables) / ((ws + pensz) * 8)));
     if ((64 * 1024 - tables) / ((ws + pensz) * 8) < 1) out->wpb = 0;   // a family too large for one slice: the engine's generic kernel
-    std::string wk = gen_wave_kernel(wave_names, part_names, pen_names, pps, ws, pensz, std::max(1, out->wpb));
+    std::string wk = gen_wave_kernel(wave_names, part_names, pen_names, shape_ns, pps, ws, pensz, std::max(1, out->wpb));
     const size_t at = wk.find("extern \"C\"");   // device helpers first, then the family functions, then the kernel
     src += wk.substr(0, at);
     for (auto& b : wave_bodies) src += b;
