@@ -520,7 +520,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
     for (int k = 0; k < nst; k++)
       if (ty(k) != 1) isto[to(k)] = 1;
     for (int k = 0; k < nst; k++) {
-      if (ty(k) == 2 && fo(fr(k)) && !touched[fr(k)] && !top) pristine[k] = 1;
+      if (ty(k) == 2 && fo(fr(k)) && !touched[fr(k)]) pristine[k] = 1;
       if (ty(k) != 1) touched[to(k)] = 1;
       // a leaf step reads a non-founder's penetrance partial that no step ever changes
       if (ty(k) == 1 && !fo(fr(k)) && !isto[fr(k)]) leaf[k] = 1;
@@ -544,6 +544,20 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
   // workspace layout: persons' partials, marriage partials, the type-3 products.  Parts put the leaf prefix's
   // regions first (a task's items share them) and give each of the M items of a part-2 function its own copy of the
   // rest, cb = c * NSZ doubles further on
+  // a pristine founder's non-zero states (q: 0 g11, 1 g12, 2 g22) and their coefficient u, in the dense loop's order
+  // of u at one j: prior x penetrance (SetFounderPriors), the top variant's f^D term only
+  auto pterms = [&](int f) {
+    const int sx = F.sex[f];
+    const int dfull = (Y && sx == FEMALE) ? 0 : (((X || Y) && sx == MALE) || MT) ? 1 : 2;
+    std::vector<std::pair<int, int>> t;
+    if (top) {
+      if (dfull > 0) t = {{0, 0}};
+      else t = {{2, 0}, {1, 0}, {0, 0}};
+    } else if (d0[f] == 2) t = {{2, 0}, {1, 1}, {0, 2}};
+    else if (d0[f] == 1) t = {{2, 0}, {0, 1}};
+    else t = {{2, 0}, {1, 0}, {0, 0}};
+    return t;
+  };
   const int M = part == 2 ? std::max(1, multi) : 1;
   std::map<int, int> leafs;   // the marriage slots the leaf steps write
   for (int k = 0; k < nst; k++)
@@ -619,6 +633,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
   int fin = -1;
   double nops = 0;
   std::vector<char> done(nst, 0);
+  std::vector<double> frac1(nst, 1.0);   // type-1 steps: the fraction of the 100 pairs computed (founder-sparse rows)
   for (const int2& St : F.steps) {
     const int kstep = (int)si;
     const StepDeg g = sd[si++];
@@ -628,10 +643,10 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
     {   // this step's FP64 operations (per item)
       const int type = St.x & 255, slot = (St.y >> 8) & 255, create = (St.y >> 16) & 1;
       const double ns = NS;
-      if (type == 1) nops += ns * ns * ((g.a + 1) * ns + (create ? 0 : (g.a + 1) * (g.b + 1)));
+      if (type == 1) nops += frac1[kstep] * ns * ns * ((g.a + 1) * ns + (create ? 0 : (g.a + 1) * (g.b + 1)));
       else if (type == 2) {
         const int ds = g.a + g.b;
-        if (pristine[kstep]) nops += ns * ((g.a == 1 ? 2 : 3) * (slot == 255 ? 1 : (g.b + 1)) + (g.c + 1) * (ds + 1));
+        if (pristine[kstep]) nops += ns * ((double)pterms((St.x >> 8) & 255).size() * (slot == 255 ? 1 : (g.b + 1)) + (g.c + 1) * (ds + 1));
         else nops += ns * ((slot == 255 ? (ds + 1) * ns : ns * (g.a + 1) * (g.b + 1)) + (g.c + 1) * (ds + 1));
       } else {
         const int dw = g.a + g.b + g.c;
@@ -676,34 +691,75 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
           run.push_back(k2);
         }
         for (int k2 : run) done[k2] = 1;
-        std::string c1 = "  {\n    const int e1 = lane + 64, e1c = e1 < 100 ? e1 : lane;\n";
-        for (size_t q = 0; q < run.size(); q++) {
-          const int ga = sd[run[q]].a;
-          c1 += "    double s0_" + S(q) + "[" + S(ga + 1) + "], s1_" + S(q) + "[" + S(ga + 1) + "];\n";
-          for (int a = 0; a <= ga; a++) c1 += "    s0_" + S(q) + "[" + S(a) + "] = 0.0;\n    s1_" + S(q) + "[" + S(a) + "] = 0.0;\n";
-        }
-        // (k unrolled by 2 only: fully unrolled, the scheduler hoists every offspring coefficient's LDS read and
-        // spills)
-        c1 += "#pragma unroll 2\n    for (int k = 0; k < 10; k++) {\n";
-        c1 += g_expt == 1 ? "      const double t0 = 0.001 * k, t1 = 0.002 * k;\n"   // (timing experiment only: wrong values)
-              : g_tr_regs ? "      const double t0 = tr0[k], t1 = tr1[k];\n"
-                          : "      const double t0 = t10dn[lane * 10 + k], t1 = t10dn[e1c * 10 + k];\n";
-        for (size_t q = 0; q < run.size(); q++) {
-          const int2 Sq = F.steps[run[q]];
-          const int offq = (Sq.x >> 8) & 255, ga = sd[run[q]].a;
-          for (int a = 0; a <= ga; a++)
-            c1 += "      {\n        const double p = W[" + PO(offq) + " + k * " + S(capP[offq]) + " + " + S(a) + "];\n        s0_" + S(q) + "[" + S(a) +
-                  "] = fma(t0, p, s0_" + S(q) + "[" + S(a) + "]);\n        s1_" + S(q) + "[" + S(a) + "] = fma(t1, p, s1_" + S(q) + "[" + S(a) + "]);\n      }\n";
-        }
-        c1 += "    }\n";
-        // per pair: the marriage partials in the run's order of first use, each chained through its steps
-        std::vector<int> slots;
+        std::vector<int> slots;   // the marriage partials the run writes, in order of first use
         for (int k2 : run) {
           const int sl2 = (F.steps[k2].y >> 8) & 255;
           if (std::find(slots.begin(), slots.end(), sl2) == slots.end()) slots.push_back(sl2);
         }
-        for (int pr = 0; pr < 2; pr++) {
-          const std::string sp = pr ? "s1_" : "s0_", e = pr ? "e1" : "lane";
+        // Founder-sparse rows: when the run writes one marriage partial and its only reader is a pristine type-2
+        // step (the founder spouse F peeled into the other), that step reads the rows of F's non-zero states only
+        // (2-3 of 10; 1 in the top variant): only those pairs are computed (lanes over F's states x the spouse's)
+        std::vector<std::pair<int, int>> sp_terms;
+        bool sp_father = false;
+        if (part != 1 && slots.size() == 1) {
+          int readers = 0, rk = -1;
+          bool writes_after = false;
+          for (int k2 = run.back() + 1; k2 < nst; k2++) {
+            if ((part == 2 && leaf[k2])) continue;
+            const int t2 = F.steps[k2].x & 255, s2 = (F.steps[k2].y >> 8) & 255;
+            if (s2 != slots[0]) continue;
+            if (t2 == 1) writes_after = true;
+            else { readers++; rk = k2; }
+          }
+          if (readers == 1 && !writes_after && (F.steps[rk].x & 255) == 2 && pristine[rk]) {
+            sp_terms = pterms((F.steps[rk].x >> 8) & 255);
+            sp_father = (F.steps[rk].y >> 17) & 1;
+          }
+        }
+        const bool sparse = !sp_terms.empty();
+        if (sparse) {   // (the run's first step was counted at 100 pairs above)
+          const double fr = 10.0 * sp_terms.size() / 100.0;
+          nops -= (1.0 - fr) * 100.0 * ((g.a + 1) * 10.0 + (create ? 0 : (g.a + 1) * (g.b + 1)));
+          for (int k2 : run) frac1[k2] = fr;
+        }
+        const int npair = sparse ? 1 : 2;
+        std::string c1 = "  {\n";
+        if (sparse) {
+          const std::string gq[3] = {"g11", "g12", "g22"};
+          std::string sF = gq[sp_terms.back().first];
+          for (int q = (int)sp_terms.size() - 2; q >= 0; q--) sF = "qi_ == " + S(q) + " ? " + gq[sp_terms[q].first] + " : " + sF;
+          c1 += "    const int qi_ = lane / 10, o_ = lane - qi_ * 10, sF_ = " + sF + ";\n    const int e = " +
+                (sp_father ? "sF_ * 10 + o_" : "o_ * 10 + sF_") + ";\n    if (lane < " + S(10 * sp_terms.size()) + ") {\n";
+        } else c1 += "    const int e1 = lane + 64, e1c = e1 < 100 ? e1 : lane;\n";
+        for (size_t q = 0; q < run.size(); q++) {
+          const int ga = sd[run[q]].a;
+          for (int pr = 0; pr < npair; pr++) {
+            c1 += "    double s" + S(pr) + "_" + S(q) + "[" + S(ga + 1) + "];\n";
+            for (int a = 0; a <= ga; a++) c1 += "    s" + S(pr) + "_" + S(q) + "[" + S(a) + "] = 0.0;\n";
+          }
+        }
+        // (k unrolled by 2 only: fully unrolled, the scheduler hoists every offspring coefficient's LDS read and
+        // spills)
+        c1 += "#pragma unroll 2\n    for (int k = 0; k < 10; k++) {\n";
+        if (sparse) c1 += "      const double t0 = t10dn[e * 10 + k];\n";
+        else
+          c1 += g_expt == 1 ? "      const double t0 = 0.001 * k, t1 = 0.002 * k;\n"   // (timing experiment only: wrong values)
+                : g_tr_regs ? "      const double t0 = tr0[k], t1 = tr1[k];\n"
+                            : "      const double t0 = t10dn[lane * 10 + k], t1 = t10dn[e1c * 10 + k];\n";
+        for (size_t q = 0; q < run.size(); q++) {
+          const int2 Sq = F.steps[run[q]];
+          const int offq = (Sq.x >> 8) & 255, ga = sd[run[q]].a;
+          for (int a = 0; a <= ga; a++) {
+            c1 += "      {\n        const double p = W[" + PO(offq) + " + k * " + S(capP[offq]) + " + " + S(a) + "];\n";
+            for (int pr = 0; pr < npair; pr++)
+              c1 += "        s" + S(pr) + "_" + S(q) + "[" + S(a) + "] = fma(t" + S(pr) + ", p, s" + S(pr) + "_" + S(q) + "[" + S(a) + "]);\n";
+            c1 += "      }\n";
+          }
+        }
+        c1 += "    }\n";
+        // per pair: each marriage partial chained through its steps in registers, one write
+        for (int pr = 0; pr < npair; pr++) {
+          const std::string sp = "s" + S(pr) + "_", e = sparse ? "e" : pr ? "e1" : "lane";
           c1 += pr ? "    if (e1 < 100) {\n" : "    {\n";
           int cid = 0;
           for (int sl2 : slots) {
@@ -738,6 +794,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
           }
           c1 += "    }\n";
         }
+        if (sparse) c1 += "    }\n";
         c1 += "  }\n  wave_sync();\n";
         code += c1;
       } else
@@ -797,23 +854,49 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
         // The sum visits j in the dense loop's order and skips the zero terms (fma(0, g, s) == s), so it is
         // bit-identical to the dense sum (q in the dense loop's coefficient order u = 0, 1, 2 at one j, should two of
         // the genotypes coincide)
-        const int d = d0[sf];
-        b += std::string(run.size() > 1 ? "#pragma unroll 2" : "#pragma unroll") + "\n    for (int j = 0; j < " + nsS + "; j++) {\n";
+        // No loop over j: the terms' states are wave-uniform, so their order by j (stable: ties keep the coefficient
+        // order) is one of at most 6, chosen once by a uniform switch; each case adds the terms in that order
         const std::string gq[3] = {"g11", "g12", "g22"};
-        for (int q = 2; q >= 0; q--) {
-          if (d == 1 && q == 1) continue;
-          const int u = d == 2 ? 2 - q : d == 1 ? (q == 0 ? 1 : 0) : 0;
-          b += "      if (j == " + gq[q] + ") {\n        const double f = W[" + OF + " + j * " + S(fcap) + " + " + S(u) + "];\n";
-          if (slot == 255) b += "        s[" + S(u) + "] += f;\n";
+        const std::vector<std::pair<int, int>> tm = pterms(sf);
+        auto term = [&](int q, int u) {
+          std::string t = "      {\n        const int j = " + gq[q] + ";\n        const double f = W[" + OF + " + j * " + S(fcap) + " + " + S(u) + "];\n";
+          if (slot == 255) t += "        s[" + S(u) + "] += f;\n";
           else {
             const int mcap = capM[slot];
             const std::string me = run.size() > 1 ? "(i * si_ + j * sj_)" : fa2mo ? "(j * " + nsS + " + i)" : "(i * " + nsS + " + j)";
             for (int v = 0; v <= g.b; v++)
-              b += "        s[" + S(u + v) + "] = fma(f, W[" + OM + " + " + me + " * " + S(mcap) + " + " + S(v) + "], s[" + S(u + v) + "]);\n";
+              t += "        s[" + S(u + v) + "] = fma(f, W[" + OM + " + " + me + " * " + S(mcap) + " + " + S(v) + "], s[" + S(u + v) + "]);\n";
           }
-          b += "      }\n";
+          return t + "      }\n";
+        };
+        const int nt = (int)tm.size();
+        if (nt == 1) b += term(tm[0].first, tm[0].second);
+        else {
+          // bit c of the case: term a (of pair c) is not after term b, in the terms' order a < b
+          std::vector<std::pair<int, int>> prs;
+          for (int a = 0; a < nt; a++)
+            for (int c = a + 1; c < nt; c++) prs.push_back({a, c});
+          std::string key;
+          for (size_t c = 0; c < prs.size(); c++)
+            key += std::string(c ? " | " : "") + "((" + gq[tm[prs[c].first].first] + " <= " + gq[tm[prs[c].second].first] + ") << " + S(c) + ")";
+          b += "    switch (" + key + ") {\n";
+          for (int cs = 0; cs < (1 << prs.size()); cs++) {
+            std::vector<int> ord(nt);
+            for (int a = 0; a < nt; a++) ord[a] = a;
+            auto before = [&](int x, int y) {   // x before y in this case
+              for (size_t c = 0; c < prs.size(); c++) {
+                if (prs[c].first == x && prs[c].second == y) return ((cs >> c) & 1) != 0;
+                if (prs[c].first == y && prs[c].second == x) return ((cs >> c) & 1) == 0;
+              }
+              return x < y;
+            };
+            std::stable_sort(ord.begin(), ord.end(), before);
+            b += "      case " + S(cs) + ":\n";
+            for (int a : ord) b += term(tm[a].first, tm[a].second);
+            b += "      break;\n";
+          }
+          b += "    }\n";
         }
-        b += "    }\n";
       } else if (slot == 255) {
         for (int a = 0; a <= ds; a++)
           b += "#pragma unroll\n    for (int j = 0; j < " + nsS + "; j++) s[" + S(a) + "] += W[" + OF + " + j * " + S(fcap) + " + " +
