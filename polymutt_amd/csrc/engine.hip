@@ -834,7 +834,9 @@ static const pmjit::Kernel* jit_kernel(pm_engine* E) {
     }
     std::string err;
     pmjit::Kernel& K = E->jit[plan][cls];
-    if (!fams.empty() && pmjit::build(E->device, cls, fams, kTBA, E->par.denovo != 0, &K, &err)) {
+    // (--denovo outside vcf_mode: every de novo item is hoisted in a grouped task, launch_brent)
+    const int dmode = !E->par.denovo ? 0 : (!E->vcf && !getenv("PM_ES_NOGROUP")) ? 2 : 1;
+    if (!fams.empty() && pmjit::build(E->device, cls, fams, kTBA, dmode, &K, &err)) {
       const size_t ns = K.slot_e.size();
       std::vector<int> tab(3 * ns);
       for (size_t i = 0; i < ns; i++) { tab[i] = K.slot_e[i]; tab[ns + i] = K.slot_sig[i]; tab[2 * ns + i] = K.slot_p0[i]; }

@@ -558,6 +558,52 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
     else t = {{2, 0}, {1, 0}, {0, 0}};
     return t;
   };
+  // runs of consecutive type-1 steps of this part (one phase each in the 10-state code), and their founder-sparse
+  // rows: when a run writes one marriage partial and its only later reader is a pristine type-2 step (the founder
+  // spouse F peeled into the other), that step reads the rows of F's non-zero states only (2-3 of 10; 1 in the top
+  // variant), so only those pairs are computed (lanes over F's states x the spouse's).  In part 2 a partial whose
+  // writers all sit in such a run is stored compactly, row q * 10 + spouse state for F's q-th term.
+  auto inpart = [&](int k2) { return !((part == 1 && !leaf[k2]) || (part == 2 && leaf[k2])); };
+  auto run_of = [&](int k0) {
+    std::vector<int> run;
+    for (int k2 = k0; k2 < nst; k2++) {
+      if (!inpart(k2)) continue;
+      if ((F.steps[k2].x & 255) != 1) break;
+      run.push_back(k2);
+    }
+    return run;
+  };
+  struct Sparse { std::vector<std::pair<int, int>> terms; bool father = false, compact = false; };
+  auto sparse_of = [&](const std::vector<int>& run) {
+    Sparse sp;
+    if (NS != 10 || part == 1 || run.empty()) return sp;
+    const int sl0 = (F.steps[run[0]].y >> 8) & 255;
+    for (int k2 : run)
+      if (((F.steps[k2].y >> 8) & 255) != sl0) return sp;
+    int readers = 0, rk = -1;
+    bool writes_after = false, writes_before = false;
+    for (int k2 = run.back() + 1; k2 < nst; k2++) {
+      if (!inpart(k2) || ((F.steps[k2].y >> 8) & 255) != sl0) continue;
+      if ((F.steps[k2].x & 255) == 1) writes_after = true;
+      else { readers++; rk = k2; }
+    }
+    for (int k2 = 0; k2 < run[0]; k2++)
+      if ((F.steps[k2].x & 255) == 1 && ((F.steps[k2].y >> 8) & 255) == sl0) writes_before = true;
+    if (readers == 1 && !writes_after && (F.steps[rk].x & 255) == 2 && pristine[rk]) {
+      sp.terms = pterms((F.steps[rk].x >> 8) & 255);
+      sp.father = (F.steps[rk].y >> 17) & 1;
+      sp.compact = part == 2 && !writes_before && multi <= 1;
+    }
+    return sp;
+  };
+  std::map<int, int> crows;   // compactly stored marriage partials: slot -> rows
+  if (NS == 10 && part == 2)
+    for (int k = 0; k < nst; k++) {
+      if (!inpart(k) || (F.steps[k].x & 255) != 1 || (k > 0 && inpart(k - 1) && (F.steps[k - 1].x & 255) == 1)) continue;
+      const std::vector<int> run = run_of(k);
+      const Sparse sp = sparse_of(run);
+      if (sp.compact) crows[(F.steps[k].y >> 8) & 255] = 10 * (int)sp.terms.size();
+    }
   const int M = part == 2 ? std::max(1, multi) : 1;
   std::map<int, int> leafs;   // the marriage slots the leaf steps write
   for (int k = 0; k < nst; k++)
@@ -569,11 +615,14 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
     for (int i = 0; i < n; i++)
       if (!part || leafp[i] == L) { po[i] = off; off += NS * capP[i]; }
     for (auto& m : capM)
-      if (!part || (int)leafs.count(m.first) == L) { mo[m.first] = off; off += NS * NS * m.second; }
+      if (!part || (int)leafs.count(m.first) == L) {
+        mo[m.first] = off;
+        off += (crows.count(m.first) ? crows[m.first] : NS * NS) * m.second;
+      }
     if (L == 1) LSZ = off;
   }
   const int TB = off, NSZ = off + tmp - LSZ;
-  *ws_doubles = LSZ + M * NSZ;
+  *ws_doubles = part == 1 ? LSZ : LSZ + M * NSZ;   // (the leaf prefix writes its own regions only)
   auto S = [](long v) { return std::to_string(v); };
   const std::string nsS = S(NS), nsq = S(NS * NS), R = S((NS * NS + 63) / 64);
   const bool mc = part == 2 && M > 1;   // offsets of the item's own regions carry cb (several items per call)
@@ -684,38 +733,16 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
         // the run (each offspring coefficient read from LDS once for the two pairs: wave-uniform broadcasts), then per
         // marriage partial the steps' products chained in registers and one write -- the same operations in the
         // same order as step by step
-        std::vector<int> run;
-        for (int k2 = kstep; k2 < nst; k2++) {
-          if ((part == 1 && !leaf[k2]) || (part == 2 && leaf[k2])) continue;
-          if ((F.steps[k2].x & 255) != 1) break;
-          run.push_back(k2);
-        }
+        const std::vector<int> run = run_of(kstep);
         for (int k2 : run) done[k2] = 1;
         std::vector<int> slots;   // the marriage partials the run writes, in order of first use
         for (int k2 : run) {
           const int sl2 = (F.steps[k2].y >> 8) & 255;
           if (std::find(slots.begin(), slots.end(), sl2) == slots.end()) slots.push_back(sl2);
         }
-        // Founder-sparse rows: when the run writes one marriage partial and its only reader is a pristine type-2
-        // step (the founder spouse F peeled into the other), that step reads the rows of F's non-zero states only
-        // (2-3 of 10; 1 in the top variant): only those pairs are computed (lanes over F's states x the spouse's)
-        std::vector<std::pair<int, int>> sp_terms;
-        bool sp_father = false;
-        if (part != 1 && slots.size() == 1) {
-          int readers = 0, rk = -1;
-          bool writes_after = false;
-          for (int k2 = run.back() + 1; k2 < nst; k2++) {
-            if ((part == 2 && leaf[k2])) continue;
-            const int t2 = F.steps[k2].x & 255, s2 = (F.steps[k2].y >> 8) & 255;
-            if (s2 != slots[0]) continue;
-            if (t2 == 1) writes_after = true;
-            else { readers++; rk = k2; }
-          }
-          if (readers == 1 && !writes_after && (F.steps[rk].x & 255) == 2 && pristine[rk]) {
-            sp_terms = pterms((F.steps[rk].x >> 8) & 255);
-            sp_father = (F.steps[rk].y >> 17) & 1;
-          }
-        }
+        const Sparse spi = sparse_of(run);
+        const std::vector<std::pair<int, int>>& sp_terms = spi.terms;
+        const bool sp_father = spi.father;
         const bool sparse = !sp_terms.empty();
         if (sparse) {   // (the run's first step was counted at 100 pairs above)
           const double fr = 10.0 * sp_terms.size() / 100.0;
@@ -759,7 +786,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
         c1 += "    }\n";
         // per pair: each marriage partial chained through its steps in registers, one write
         for (int pr = 0; pr < npair; pr++) {
-          const std::string sp = "s" + S(pr) + "_", e = sparse ? "e" : pr ? "e1" : "lane";
+          const std::string sp = "s" + S(pr) + "_", e = spi.compact ? "lane" : sparse ? "e" : pr ? "e1" : "lane";
           c1 += pr ? "    if (e1 < 100) {\n" : "    {\n";
           int cid = 0;
           for (int sl2 : slots) {
@@ -811,7 +838,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
           const int2 Q = F.steps[k2];
           const int f2 = (Q.x >> 8) & 255, t2 = (Q.x >> 24) & 255, s2 = (Q.y >> 8) & 255;
           return std::vector<int>{pristine[k2], sd[k2].a, sd[k2].b, sd[k2].c, s2 == 255, capP[f2], capP[t2], s2 == 255 ? 0 : capM[s2],
-                                  d0[f2]};
+                                  d0[f2], (int)crows.count(s2)};
         };
         const std::vector<int> sg0 = sig2(kstep);
         for (int k2 = kstep + 1; k2 < nst && run.size() < 4; k2++) {
@@ -858,19 +885,20 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
         // order) is one of at most 6, chosen once by a uniform switch; each case adds the terms in that order
         const std::string gq[3] = {"g11", "g12", "g22"};
         const std::vector<std::pair<int, int>> tm = pterms(sf);
-        auto term = [&](int q, int u) {
+        auto term = [&](int q, int u, int qpos) {
           std::string t = "      {\n        const int j = " + gq[q] + ";\n        const double f = W[" + OF + " + j * " + S(fcap) + " + " + S(u) + "];\n";
           if (slot == 255) t += "        s[" + S(u) + "] += f;\n";
           else {
             const int mcap = capM[slot];
-            const std::string me = run.size() > 1 ? "(i * si_ + j * sj_)" : fa2mo ? "(j * " + nsS + " + i)" : "(i * " + nsS + " + j)";
+            const std::string me = crows.count(slot) ? "(" + S(qpos * 10) + " + i)"   // (compact rows)
+                                 : run.size() > 1 ? "(i * si_ + j * sj_)" : fa2mo ? "(j * " + nsS + " + i)" : "(i * " + nsS + " + j)";
             for (int v = 0; v <= g.b; v++)
               t += "        s[" + S(u + v) + "] = fma(f, W[" + OM + " + " + me + " * " + S(mcap) + " + " + S(v) + "], s[" + S(u + v) + "]);\n";
           }
           return t + "      }\n";
         };
         const int nt = (int)tm.size();
-        if (nt == 1) b += term(tm[0].first, tm[0].second);
+        if (nt == 1) b += term(tm[0].first, tm[0].second, 0);
         else {
           // bit c of the case: term a (of pair c) is not after term b, in the terms' order a < b
           std::vector<std::pair<int, int>> prs;
@@ -892,7 +920,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
             };
             std::stable_sort(ord.begin(), ord.end(), before);
             b += "      case " + S(cs) + ":\n";
-            for (int a : ord) b += term(tm[a].first, tm[a].second);
+            for (int a : ord) b += term(tm[a].first, tm[a].second, a);
             b += "      break;\n";
           }
           b += "    }\n";
@@ -979,7 +1007,7 @@ std::string gen_pen_fill(int n, const std::string& name) {
 // fns: 3 variants per shape (bi-allelic, 10-state, top); parts: per shape the 10-state leaf prefix, the 10-state rest,
 // the top variant's rest and (pps == 4) the 10-state rest of three items at once
 std::string gen_wave_kernel(const std::vector<std::string>& fns, const std::vector<std::string>& parts, const std::vector<std::string>& pens,
-                            const std::vector<int>& shape_ns, int pps, int ws, int pensz, int wpb) {
+                            const std::vector<int>& shape_ns, int pps, int ws, int pensz, int wpb, bool parts_only) {
   const int npf = pensz <= 4 * 64 ? (pensz + 63) / 64 : 0;   // prefetch registers per lane (0: families too large)
   std::string s = R"(
 __device__ __forceinline__ void wave_sync() {
@@ -1078,7 +1106,7 @@ PENS        }
       pen_site = site;
       PCLK(0);
     }
-    if (G > 1 && dn) {
+    if ((G > 1 || PARTS_ONLY) && dn) {
       if (site != leaf_site) {
         leaf_site = site;
         switch (sig) {
@@ -1125,6 +1153,7 @@ PARTS2      }
   }
   for (size_t at; (at = k.find("WPB")) != std::string::npos;) k.replace(at, 3, std::to_string(wpb));
   k.replace(k.find("MULTI"), 5, pps == 4 ? "true" : "false");
+  k.replace(k.find("PARTS_ONLY"), 10, parts_only ? "true" : "false");
   k.replace(k.find("WPEU"), 4, "__attribute__((amdgpu_waves_per_eu(4)))");   // (<= 128 VGPRs: 4 waves per SIMD)
   const std::string call = "(pl, A.np, P11, P12, P22, p0, g11, g12, g22, lk, t10, t10dn, tb, tr0, tr1, W, lane, out, A.T, A.dcap, 0, PEN); break;\n";
   const std::string call3 = "(pl, A.np, P11, P12, P22, p0, G11, G12, G22, lk, t10, t10dn, tb, tr0, tr1, W, lane, out, A.T, A.dcap, ostr, PEN); break;\n";
@@ -1136,7 +1165,8 @@ PARTS2      }
     k.replace(k.find(key), key.size(), cases);
   }
   s += k;
-  for (size_t i = 0; i < fns.size(); i++) s += "      case " + std::to_string(i) + ": " + fns[i] + call;
+  for (size_t i = 0; i < fns.size(); i++)
+    if (!fns[i].empty()) s += "      case " + std::to_string(i) + ": " + fns[i] + call;
   s += "    }\n    PCLK(4);\n    }\n  }\n  if (PROF && lane == 0)\n    for (int c = 0; c < 5; c++) atomicAdd(A.prof + c, pc[c]);\n}\n";
   for (size_t at; (at = s.find("PROF")) != std::string::npos;) s.replace(at, 4, g_prof ? "true" : "false");
   return s;
@@ -1185,7 +1215,7 @@ int pack_steps(const pm_pedigree* ped, int f, int ns, std::vector<int2>& out) {
   return n * ns + (int)keys.size() * ns * ns;
 }
 
-std::string generate(int chrom, const std::vector<Family>& fams, const double (*tba)[27], Kernel* out, bool denovo) {
+std::string generate(int chrom, const std::vector<Family>& fams, const double (*tba)[27], Kernel* out, int denovo) {
   std::map<std::string, int> shape_of;
   for (auto& v : out->shape_ops) v.clear();
   std::vector<std::string> names, bodies, post_names, post_bodies, wave_names, wave_bodies, part_names, pen_names;
@@ -1225,6 +1255,10 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
         pensz = std::max(pensz, 10 * fams[i].n);
         for (int v = 0; v < 3; v++) {
           int w = 0;
+          if (denovo == 2 && v > 0) {   // (grouped tasks only: the de novo items go through the parts)
+            wave_names.push_back("");
+            continue;
+          }
           wave_names.push_back("wfam" + std::to_string(id) + "_" + std::to_string(v));
           wave_bodies.push_back(gen_wave_family(fams[i], chrom, v == 0 ? 3 : 10, v == 2, wave_names.back(), &w, &o3[v]));
           ws = std::max(ws, w);
@@ -1264,7 +1298,7 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
     // (one wave per SIMD: the occupancy comes from blocks per CU, build() asks the runtime for them)
     out->wpb = std::max(1, std::min(4, (64 * 1024 - tables) / ((ws + pensz) * 8)));
     if ((64 * 1024 - tables) / ((ws + pensz) * 8) < 1) out->wpb = 0;   // a family too large for one slice: the engine's generic kernel
-    std::string wk = gen_wave_kernel(wave_names, part_names, pen_names, shape_ns, pps, ws, pensz, std::max(1, out->wpb));
+    std::string wk = gen_wave_kernel(wave_names, part_names, pen_names, shape_ns, pps, ws, pensz, std::max(1, out->wpb), denovo == 2);
     const size_t at = wk.find("extern \"C\"");   // device helpers first, then the family functions, then the kernel
     src += wk.substr(0, at);
     for (auto& b : wave_bodies) src += b;
@@ -1303,7 +1337,7 @@ bool compile(const std::string& src, std::vector<char>* code, std::string* err, 
   return true;
 }
 
-bool build(int device, int chrom, const std::vector<Family>& fams, const double (*tba)[27], bool denovo, Kernel* out,
+bool build(int device, int chrom, const std::vector<Family>& fams, const double (*tba)[27], int denovo, Kernel* out,
            std::string* err) {
   const auto t0 = std::chrono::steady_clock::now();
   const std::string src = generate(chrom, fams, tba, out, denovo);

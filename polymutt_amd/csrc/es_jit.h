@@ -81,14 +81,15 @@ int pack_steps(const pm_pedigree* ped, int f, int ns, std::vector<int2>& out);
 
 // The generated source of the hoisting kernel of `fams` (fills out's slot tables; no device needed).
 // denovo: the wave-cooperative kernel es_hoist_wave (10-state, bi-allelic and top variants per shape) instead of the
-// per-thread es_hoist_jit and es_post_jit.
-std::string generate(int chrom, const std::vector<Family>& fams, const double (*tba)[27], Kernel* out, bool denovo = false);
+// per-thread es_hoist_jit and es_post_jit; 2: the same for engines whose de novo items always come in grouped tasks
+// (no whole 10-state / top variants: their larger workspace would set every wave's LDS slice).
+std::string generate(int chrom, const std::vector<Family>& fams, const double (*tba)[27], Kernel* out, int denovo = 0);
 // hipRTC compile of a generated source for gfx950 (no device needed).
 bool compile(const std::string& src, std::vector<char>* code, std::string* err, const std::string& arch = "gfx950");
 
 // Generates and compiles the hoisting and posterior kernels of `fams` for chromosome class `chrom` (PM_CHR_*); bi-allelic
 // (3-state) peels.  tba = transmission_BA tables [5][27] (:812-924).  Returns false with a message in err.
-bool build(int device, int chrom, const std::vector<Family>& fams, const double (*tba)[27], bool denovo, Kernel* out,
+bool build(int device, int chrom, const std::vector<Family>& fams, const double (*tba)[27], int denovo, Kernel* out,
            std::string* err);
 
 }  // namespace pmjit

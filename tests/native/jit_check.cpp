@@ -42,9 +42,9 @@ int main(int argc, char** argv) {
     fams.push_back(F);
   }
   if (fams.empty()) { fprintf(stderr, "no extended families\n"); return 1; }
-  for (int run = 0; run < 8; run++) {
+  for (int run = 0; run < 12; run++) {
     const int cls = run & 3;
-    const bool dn = run >= 4;   // the --denovo engines' wave-cooperative kernel
+    const int dn = run >= 8 ? 1 : run >= 4 ? 2 : 0;   // the --denovo engines' wave-cooperative kernel (2: grouped tasks only)
     pmjit::Kernel K;
     const std::string src = pmjit::generate(cls, fams, kTBA, &K, dn);
     if (!emit.empty() && cls == 0) {

@@ -347,7 +347,7 @@ def test_schedule_compiler_builds_every_class(tmp_path, shape):
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     lines = [l.split() for l in r.stdout.splitlines() if l.startswith("class")]
-    assert [int(l[1]) for l in lines] == [0, 1, 2, 3] * 2   # bi-allelic engines, then --denovo engines
+    assert [int(l[1]) for l in lines] == [0, 1, 2, 3] * 3   # bi-allelic engines, --denovo (grouped tasks, then all)
     assert all(int(l[3]) == 1 and int(l[5]) == 5 and int(l[9]) > 0 for l in lines), r.stdout   # one shape, 5 families
     src = (tmp_path / "k.hip").read_text()
     assert "es_hoist_jit" in src and "fam0(" in src and "asm" not in src
