@@ -777,7 +777,8 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
           const int2 Sq = F.steps[run[q]];
           const int offq = (Sq.x >> 8) & 255, ga = sd[run[q]].a;
           for (int a = 0; a <= ga; a++) {
-            c1 += "      {\n        const double p = W[" + PO(offq) + " + k * " + S(capP[offq]) + " + " + S(a) + "];\n";
+            c1 += g_expt == 2 ? "      {\n        const double p = 0.5 + 0.01 * k + " + S(a) + ";\n"   // (timing experiment only)
+                              : "      {\n        const double p = W[" + PO(offq) + " + k * " + S(capP[offq]) + " + " + S(a) + "];\n";
             for (int pr = 0; pr < npair; pr++)
               c1 += "        s" + S(pr) + "_" + S(q) + "[" + S(a) + "] = fma(t" + S(pr) + ", p, s" + S(pr) + "_" + S(q) + "[" + S(a) + "]);\n";
             c1 += "      }\n";
