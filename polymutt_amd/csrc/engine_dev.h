@@ -1319,6 +1319,25 @@ __device__ __forceinline__ void wave_prod(double& m, int& e) {
   e = __builtin_amdgcn_readlane(e, 63) + ev;  // step-wise normalised product, scalings by 2^k being exact)
 }
 
+// Sum of the 64 lanes' doubles in the same DPP order as wave_prod, broadcast from lane 63 (exact for integer values
+// whose partial sums stay below 2^53: k_prep's read statistics and PL sums)
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ void dpp_add_step(double& v) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  const int olo = __builtin_amdgcn_update_dpp(0, lo, CTRL, ROWMASK, 0xF, false);   // rows not written: +0.0
+  const int ohi = __builtin_amdgcn_update_dpp(0, hi, CTRL, ROWMASK, 0xF, false);
+  v = v + __hiloint2double(ohi, olo);
+}
+__device__ __forceinline__ double wave_sum_exact(double v) {
+  dpp_add_step<0xB1, 0xF>(v);
+  dpp_add_step<0x4E, 0xF>(v);
+  dpp_add_step<0x141, 0xF>(v);
+  dpp_add_step<0x140, 0xF>(v);
+  dpp_add_step<0x142, 0xA>(v);
+  dpp_add_step<0x143, 0xC>(v);
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), 63), __builtin_amdgcn_readlane(__double2loint(v), 63));
+}
+
 // log10(m * 2^e) for a normalised mantissa m in [0.5, 1) (or 0): m is moved to [sqrt(1/2), sqrt(2)) (exact),
 // then log(m) = 2 atanh(t), t = (m - 1) / (m + 1), |t| <= 0.172, as 2t + t^3 P(t^2) with the 10-term
 // atanh series (truncation < 3e-17 relative).  Absolute error <= ~7e-17 (OCML's double-double log10:
@@ -2042,10 +2061,10 @@ __global__ void __launch_bounds__(256) k_prep(DevArgs A) {
       double dm_m = 1.0;
       int dm_e = 0;
       const uint8_t* plane_h = pl + (size_t)h * np;
-      for (int base = 0; base < np; base += 64 * VEC) {
-        const int p0 = base + lane * VEC;
+      // one chunk of VEC persons per lane: the read statistics and the PL sum (SERIAL: the serial mono sum); hr keeps
+      // the hom-ref PL bytes for the de novo monomorphism product
+      auto chunk = [&](int p0, uint8_t* hr) {
         uint32_t x[VEC];
-        uint8_t hr[VEC];
         if (p0 < np) {   // np % VEC == 0: a lane's VEC persons are all present or all absent
           if (!A.vcf) load_dwords<VEC>(dm + p0, x);
           else {   // the VCF path has no read depth or mapping quality (PedVCF / FamilyLikelihoodSeq_VCF): dm is not read
@@ -2072,27 +2091,40 @@ __global__ void __launch_bounds__(256) k_prep(DevArgs A) {
             mono += __shfl(t, l, 64);
           }
         }
-        if (mdn && p0 < np) {
-          uint8_t fo[VEC];
-          load_bytes<VEC>((const uint8_t*)A.is_founder + p0, fo);
-          uint8_t kb[10][VEC];
+      };
+      if (!mdn) {
+        // unrolled: the loads of 4 chunks in flight together (one HBM round trip per chunk made k_prep latency-bound)
+#pragma unroll 4
+        for (int base = 0; base < np; base += 64 * VEC) {
+          uint8_t hr[VEC];
+          chunk(base + lane * VEC, hr);
+        }
+      } else
+        for (int base = 0; base < np; base += 64 * VEC) {
+          const int p0 = base + lane * VEC;
+          uint8_t hr[VEC];
+          chunk(p0, hr);
+          if (p0 < np) {
+            uint8_t fo[VEC];
+            load_bytes<VEC>((const uint8_t*)A.is_founder + p0, fo);
+            uint8_t kb[10][VEC];
 #pragma unroll
-          for (int g = 0; g < 10; g++) load_bytes<VEC>(pl + (size_t)g * np + p0, kb[g]);
+            for (int g = 0; g < 10; g++) load_bytes<VEC>(pl + (size_t)g * np + p0, kb[g]);
 #pragma unroll
-          for (int k = 0; k < VEC; k++) {
-            double fct;
-            if (fo[k]) fct = s_lk[hr[k]];
-            else {
-              fct = 0.0;
+            for (int k = 0; k < VEC; k++) {
+              double fct;
+              if (fo[k]) fct = s_lk[hr[k]];
+              else {
+                fct = 0.0;
 #pragma unroll
-              for (int g = 0; g < 10; g++) fct += s_M[h * 10 + g] * s_lk[kb[g][k]];
+                for (int g = 0; g < 10; g++) fct += s_M[h * 10 + g] * s_lk[kb[g][k]];
+              }
+              int xe;
+              dm_m = frexp(dm_m * fct, &xe);
+              dm_e += xe;
             }
-            int xe;
-            dm_m = frexp(dm_m * fct, &xe);
-            dm_e += xe;
           }
         }
-      }
       if (mdn) {
         wave_prod(dm_m, dm_e);
         if (lane == 0) {
@@ -2101,13 +2133,16 @@ __global__ void __launch_bounds__(256) k_prep(DevArgs A) {
           A.evals[site * 8] = 1;
         }
       }
+      // integer sums < 2^53 reduced as doubles on the DPP crossbar (exact in any order; no LDS round trips)
       if constexpr (!SERIAL) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) plsum += __shfl_xor(plsum, o, 64);
+        plsum = (long long)wave_sum_exact((double)plsum);
         mono = plsum ? -(double)plsum / 10 : 0.0;
       }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) { dsum += __shfl_xor(dsum, o, 64); mqsum += __shfl_xor(mqsum, o, 64); nsd += __shfl_xor(nsd, o, 64); }
+      if (!A.vcf) {   // (the VCF path's read statistics are all zero)
+        dsum = (long long)wave_sum_exact((double)dsum);
+        mqsum = (long long)wave_sum_exact((double)mqsum);
+        nsd = (long long)wave_sum_exact((double)nsd);
+      }
       if (lane == 0) {
         pm_site_result O;
         memset(&O, 0, sizeof(O));
