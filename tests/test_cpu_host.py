@@ -351,3 +351,12 @@ def test_schedule_compiler_builds_every_class(tmp_path, shape):
     assert all(int(l[3]) == 1 and int(l[5]) == 5 and int(l[9]) > 0 for l in lines), r.stdout   # one shape, 5 families
     src = (tmp_path / "k.hip").read_text()
     assert "es_hoist_jit" in src and "fam0(" in src and "asm" not in src
+    # --denovo kernels: the grouped-tasks-only kernel (lines 4-7) needs no larger a workspace slice than the one with
+    # the whole 10-state / top variants (lines 8-11); per (item, family) the leaf prefix + 10-state rest does the
+    # whole 10-state peel's operations or fewer (founder sparsity), and the top rest + leaf the top variant's
+    def field(l, name):
+        return int(l[l.index(name) + 1])
+    for g, f in zip(lines[4:8], lines[8:12]):
+        assert field(g, "ws") <= field(f, "ws"), (g, f)
+        ops = [float(x) for x in f[f.index("ops") + 1:]]   # bi-allelic, 10-state, top, leaf, rest, top rest
+        assert ops[3] + ops[4] <= ops[1] + 1e-9 and ops[3] + ops[5] <= ops[2] + 1e-9, f
