@@ -446,9 +446,10 @@ extern "C" __global__ void __launch_bounds__(256) es_post_jit(PostArgs A) {
 // The de novo transmission rows of a type-1 step's pairs: from the (cache-resident) global table, or held in 20
 // registers for the whole kernel (PM_ES_TR=reg: 149 VGPRs, 3 waves per SIMD; capped at 128 with 19 spilled)
 bool g_tr_regs = false;
-bool g_prof = false;
-bool g_pack = true;
-int g_expt = 0;        // PM_ES_EXPT=1: timing experiments only (results wrong), see the uses    // PM_ES_PACK=0: independent type-2 steps one phase each   // PM_ES_PROF=1: es_hoist_wave accumulates per-part clock cycles into Args::prof
+bool g_prof = false;   // PM_ES_PROF=1: es_hoist_wave accumulates per-part clock cycles into Args::prof
+bool g_pack = true;    // PM_ES_PACK=0: independent type-2 steps one phase each
+bool g_regp = true;    // PM_ES_REGP=0: type-1 phases read the offspring coefficients from LDS only
+int g_expt = 0;        // PM_ES_EXPT=1/2: timing experiments only (results wrong), see the uses
 
 struct WaveGen {
   std::string code;
@@ -683,6 +684,10 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
   double nops = 0;
   std::vector<char> done(nst, 0);
   std::vector<double> frac1(nst, 1.0);   // type-1 steps: the fraction of the 100 pairs computed (founder-sparse rows)
+  // persons whose partial the previous phase (a type-2 phase, lanes over states) left in registers: person -> (the
+  // registers' name, the first lane); a following type-1 phase takes its coefficients by v_readlane instead of
+  // wave-uniform LDS reads (the LDS pipe is what bounds this kernel)
+  std::map<int, std::pair<std::string, int>> regp;
   for (const int2& St : F.steps) {
     const int kstep = (int)si;
     const StepDeg g = sd[si++];
@@ -777,6 +782,11 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
           const int2 Sq = F.steps[run[q]];
           const int offq = (Sq.x >> 8) & 255, ga = sd[run[q]].a;
           for (int a = 0; a <= ga; a++) {
+            if (regp.count(offq)) {   // from the lanes of the type-2 phase that computed it
+              const std::string v = regp[offq].first + S(a), L = S(regp[offq].second) + " + k";
+              c1 += "      {\n        const double p = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(" + v + "), " + L +
+                    "), __builtin_amdgcn_readlane(__double2loint(" + v + "), " + L + "));\n";
+            } else
             c1 += g_expt == 2 ? "      {\n        const double p = 0.5 + 0.01 * k + " + S(a) + ";\n"   // (timing experiment only)
                               : "      {\n        const double p = W[" + PO(offq) + " + k * " + S(capP[offq]) + " + " + S(a) + "];\n";
             for (int pr = 0; pr < npair; pr++)
@@ -823,6 +833,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
           c1 += "    }\n";
         }
         if (sparse) c1 += "    }\n";
+        regp.clear();
         c1 += "  }\n  wave_sync();\n";
         code += c1;
       } else
@@ -942,17 +953,26 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
       }
       b += "    double t[" + S(g.c + 1) + "];\n";
       for (int c = 0; c <= g.c; c++) b += "    t[" + S(c) + "] = W[" + OT + " + i * " + S(tcap) + " + " + S(c) + "];\n";
+      const bool keep = NS == 10 && !mc && g_regp;   // (the outputs stay in registers for a following type-1 phase)
+      const std::string xr = "xr" + S(kstep) + "_";
+      if (keep)
+        for (int a = 0; a <= g.c + ds; a++) code += "  double " + xr + S(a) + " = 0.0;\n";
       for (int a = 0; a <= g.c + ds; a++) {
         std::string acc;
         for (int c = std::max(0, a - ds); c <= std::min(a, g.c); c++)
           acc = acc.empty() ? "t[" + S(c) + "] * s[" + S(a - c) + "]" : "fma(t[" + S(c) + "], s[" + S(a - c) + "], " + acc + ")";
-        b += "    W[" + OT + " + i * " + S(tcap) + " + " + S(a) + "] = " + acc + ";\n";
+        if (keep) b += "    " + xr + S(a) + " = " + acc + ";\n    W[" + OT + " + i * " + S(tcap) + " + " + S(a) + "] = " + xr + S(a) + ";\n";
+        else b += "    W[" + OT + " + i * " + S(tcap) + " + " + S(a) + "] = " + acc + ";\n";
       }
+      regp.clear();
+      if (keep)
+        for (size_t q = 0; q < run.size(); q++) regp[(F.steps[run[q]].x >> 24) & 255] = {xr, run.size() > 1 ? 16 * (int)q : 0};
       if (run.size() > 1)
         code += "  {\n    const int q_ = lane >> 4, i = lane & 15;\n    if (q_ < " + S(run.size()) + " && i < " + nsS + ") {\n" + pre + b +
                 "    }\n  }\n  wave_sync();\n";
       else code += lanes(NS, "i", b) + "  wave_sync();\n";
     } else {   // W(e) = P_fa[i] M(e) P_mo[j] -> LDS; lanes over k: S(k) = sum_e T(e, k) W(e), P_off[k] *= S(k) in place
+      regp.clear();
       const int fa = from0, mo_ = from1, off_ = to0, csex = F.sex[off_];
       const int dw = g.a + g.b + g.c, ww = dw + 1;
       std::string b = "      const int i = e / " + nsS + ", j = e - i * " + nsS + ";\n      double w[" + S(ww) + "];\n";
@@ -1232,6 +1252,8 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
   g_prof = epf && epf[0] == '1';
   const char* epk = getenv("PM_ES_PACK");
   g_pack = !(epk && epk[0] == '0');
+  const char* erp = getenv("PM_ES_REGP");
+  g_regp = !(erp && erp[0] == '0');
   const char* eex = getenv("PM_ES_EXPT");
   g_expt = eex ? atoi(eex) : 0;
   int ws = 1;
