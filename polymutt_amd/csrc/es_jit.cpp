@@ -643,9 +643,30 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
     return "#pragma unroll\n      for (int c = 0; c < " + S(M) + "; c++) {\n      const int cb = c * " + S(NSZ) + ";\n" + body + "      }\n";
   };
   std::string code = mc ? "" : "  const int g11 = gg11, g12 = gg12, g22 = gg22;\n  (void)g11; (void)g12; (void)g22;\n";
+  // Founders whose partial this part reads only through pristine type-2 steps (their states' prior x penetrance
+  // terms): the partial is never stored; lane x keeps the state's penetrance (fp<i>) and the terms take it by
+  // v_readlane at the term's (wave-uniform) state -- the same value the stored partial would have held
+  std::vector<char> regf(n, 0);
+  if (NS == 10 && part == 2 && multi <= 1 && g_regp) {
+    const int finp = (F.steps.back().x >> 24) & 255;
+    for (int i = 0; i < n; i++) regf[i] = F.founder[i] && i < F.nf && !leafp[i] && i != finp;
+    for (int k = 0; k < nst; k++) {
+      if (!inpart(k)) continue;
+      const int ty2 = F.steps[k].x & 255, f0 = (F.steps[k].x >> 8) & 255, f1 = (F.steps[k].x >> 16) & 255, t0 = (F.steps[k].x >> 24) & 255;
+      if (ty2 == 2) { regf[t0] = 0; if (!pristine[k]) regf[f0] = 0; }
+      else if (ty2 == 3) regf[f0] = regf[f1] = regf[t0] = 0;
+      else regf[f0] = 0;
+    }
+    for (int i = 0; i < n; i++)
+      if (regf[i]) code += "  double fp" + S(i) + " = 0.0;\n";
+  }
   // InitializePartials x SetFounderPriors, one person at a time (lanes over its states)
   for (int i = 0; i < n; i++) {
     if ((part == 1 && !leafp[i]) || (part == 2 && leafp[i])) continue;
+    if (regf[i]) {
+      code += lanes(NS, "x", "    fp" + S(i) + " = PEN[x * " + S(n) + " + " + S(i) + "];\n");
+      continue;
+    }
     const bool fo = F.founder[i] && i < F.nf;
     const int sx = F.sex[i];
     const bool yf = NS == 3 && Y && sx == FEMALE;
@@ -850,7 +871,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
           const int2 Q = F.steps[k2];
           const int f2 = (Q.x >> 8) & 255, t2 = (Q.x >> 24) & 255, s2 = (Q.y >> 8) & 255;
           return std::vector<int>{pristine[k2], sd[k2].a, sd[k2].b, sd[k2].c, s2 == 255, capP[f2], capP[t2], s2 == 255 ? 0 : capM[s2],
-                                  d0[f2], (int)crows.count(s2)};
+                                  d0[f2], (int)crows.count(s2), (int)regf[f2]};
         };
         const std::vector<int> sg0 = sig2(kstep);
         for (int k2 = kstep + 1; k2 < nst && run.size() < 4; k2++) {
@@ -898,7 +919,18 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
         const std::string gq[3] = {"g11", "g12", "g22"};
         const std::vector<std::pair<int, int>> tm = pterms(sf);
         auto term = [&](int q, int u, int qpos) {
-          std::string t = "      {\n        const int j = " + gq[q] + ";\n        const double f = W[" + OF + " + j * " + S(fcap) + " + " + S(u) + "];\n";
+          std::string t = "      {\n        const int j = " + gq[q] + ";\n";
+          if (regf[sf]) {   // the founder's penetrance at state j from lane j (x 2 for the heterozygote's coefficient)
+            auto pj = [&](int fperson) {
+              const std::string v = "fp" + S(fperson);
+              return "__hiloint2double(__builtin_amdgcn_readlane(__double2hiint(" + v + "), j), __builtin_amdgcn_readlane(__double2loint(" +
+                     v + "), j))";
+            };
+            std::string pe = pj((F.steps[run.back()].x >> 8) & 255);
+            for (int r2 = (int)run.size() - 2; r2 >= 0; r2--) pe = "q_ == " + S(r2) + " ? " + pj((F.steps[run[r2]].x >> 8) & 255) + " : " + pe;
+            t += "        const double pj_ = " + pe + ";\n";
+            t += (!top && d0[sf] == 2 && q == 1) ? "        const double f = 2 * pj_;\n" : "        const double f = pj_;\n";
+          } else t += "        const double f = W[" + OF + " + j * " + S(fcap) + " + " + S(u) + "];\n";
           if (slot == 255) t += "        s[" + S(u) + "] += f;\n";
           else {
             const int mcap = capM[slot];
