@@ -646,7 +646,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
   // Founders whose partial this part reads only through pristine type-2 steps (their states' prior x penetrance
   // terms): the partial is never stored; lane x keeps the state's penetrance (fp<i>) and the terms take it by
   // v_readlane at the term's (wave-uniform) state -- the same value the stored partial would have held
-  std::vector<char> regf(n, 0);
+  std::vector<char> regf(n, 0), regn(n, 0);
   if (NS == 10 && part == 2 && multi <= 1 && g_regp) {
     const int finp = (F.steps.back().x >> 24) & 255;
     for (int i = 0; i < n; i++) regf[i] = F.founder[i] && i < F.nf && !leafp[i] && i != finp;
@@ -659,6 +659,19 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
     }
     for (int i = 0; i < n; i++)
       if (regf[i]) code += "  double fp" + S(i) + " = 0.0;\n";
+    // non-founders whose partial is the penetrance until one type-2 step peels a spouse into it, and is then read
+    // only as a type-1 offspring (by v_readlane from that step's registers): never stored either
+    std::vector<int> t2to(n, 0);
+    for (int i = 0; i < n; i++) regn[i] = !(F.founder[i] && i < F.nf) && !leafp[i] && i != finp;
+    for (int k = 0; k < nst; k++) {
+      if (!inpart(k)) continue;
+      const int ty2 = F.steps[k].x & 255, f0 = (F.steps[k].x >> 8) & 255, f1 = (F.steps[k].x >> 16) & 255, t0 = (F.steps[k].x >> 24) & 255;
+      if (ty2 == 2) { t2to[t0]++; regn[f0] = 0; }
+      else if (ty2 == 3) regn[f0] = regn[f1] = regn[t0] = 0;
+      else if (!t2to[f0]) regn[f0] = 0;   // (a type-1 read before the type-2 step)
+    }
+    for (int i = 0; i < n; i++)
+      if (t2to[i] != 1) regn[i] = 0;
   }
   // InitializePartials x SetFounderPriors, one person at a time (lanes over its states)
   for (int i = 0; i < n; i++) {
@@ -667,6 +680,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
       code += lanes(NS, "x", "    fp" + S(i) + " = PEN[x * " + S(n) + " + " + S(i) + "];\n");
       continue;
     }
+    if (regn[i]) continue;   // (its type-2 step reads the penetrance itself)
     const bool fo = F.founder[i] && i < F.nf;
     const int sx = F.sex[i];
     const bool yf = NS == 3 && Y && sx == FEMALE;
@@ -854,7 +868,6 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
           c1 += "    }\n";
         }
         if (sparse) c1 += "    }\n";
-        regp.clear();
         c1 += "  }\n  wave_sync();\n";
         code += c1;
       } else
@@ -871,7 +884,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
           const int2 Q = F.steps[k2];
           const int f2 = (Q.x >> 8) & 255, t2 = (Q.x >> 24) & 255, s2 = (Q.y >> 8) & 255;
           return std::vector<int>{pristine[k2], sd[k2].a, sd[k2].b, sd[k2].c, s2 == 255, capP[f2], capP[t2], s2 == 255 ? 0 : capM[s2],
-                                  d0[f2], (int)crows.count(s2), (int)regf[f2]};
+                                  d0[f2], (int)crows.count(s2), (int)regf[f2], (int)regn[t2]};
         };
         const std::vector<int> sg0 = sig2(kstep);
         for (int k2 = kstep + 1; k2 < nst && run.size() < 4; k2++) {
@@ -983,9 +996,16 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
           for (int v = 0; v <= g.b; v++) b += "      s[" + S(u + v) + "] = fma(f" + S(u) + ", g" + S(v) + ", s[" + S(u + v) + "]);\n";
         b += "    }\n";
       }
-      b += "    double t[" + S(g.c + 1) + "];\n";
-      for (int c = 0; c <= g.c; c++) b += "    t[" + S(c) + "] = W[" + OT + " + i * " + S(tcap) + " + " + S(c) + "];\n";
       const bool keep = NS == 10 && !mc && g_regp;   // (the outputs stay in registers for a following type-1 phase)
+      const bool rn = keep && regn[stt];   // (the to-person is register-only: its partial was its penetrance)
+      b += "    double t[" + S(g.c + 1) + "];\n";
+      if (rn) {
+        std::string tp = S((F.steps[run.back()].x >> 24) & 255);   // (packed: the lane group's to-person)
+        for (int r2 = (int)run.size() - 2; r2 >= 0; r2--) tp = "q_ == " + S(r2) + " ? " + S((F.steps[run[r2]].x >> 24) & 255) + " : " + tp;
+        b += "    t[0] = PEN[i * " + S(n) + " + (" + tp + ")];\n";
+        for (int c = 1; c <= g.c; c++) b += "    t[" + S(c) + "] = 0.0;\n";
+      } else
+        for (int c = 0; c <= g.c; c++) b += "    t[" + S(c) + "] = W[" + OT + " + i * " + S(tcap) + " + " + S(c) + "];\n";
       const std::string xr = "xr" + S(kstep) + "_";
       if (keep)
         for (int a = 0; a <= g.c + ds; a++) code += "  double " + xr + S(a) + " = 0.0;\n";
@@ -993,10 +1013,11 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
         std::string acc;
         for (int c = std::max(0, a - ds); c <= std::min(a, g.c); c++)
           acc = acc.empty() ? "t[" + S(c) + "] * s[" + S(a - c) + "]" : "fma(t[" + S(c) + "], s[" + S(a - c) + "], " + acc + ")";
-        if (keep) b += "    " + xr + S(a) + " = " + acc + ";\n    W[" + OT + " + i * " + S(tcap) + " + " + S(a) + "] = " + xr + S(a) + ";\n";
+        if (rn) b += "    " + xr + S(a) + " = " + acc + ";\n";
+        else if (keep) b += "    " + xr + S(a) + " = " + acc + ";\n    W[" + OT + " + i * " + S(tcap) + " + " + S(a) + "] = " + xr + S(a) + ";\n";
         else b += "    W[" + OT + " + i * " + S(tcap) + " + " + S(a) + "] = " + acc + ";\n";
       }
-      regp.clear();
+      for (size_t q = 0; q < run.size(); q++) regp.erase((F.steps[run[q]].x >> 24) & 255);
       if (keep)
         for (size_t q = 0; q < run.size(); q++) regp[(F.steps[run[q]].x >> 24) & 255] = {xr, run.size() > 1 ? 16 * (int)q : 0};
       if (run.size() > 1)
@@ -1004,7 +1025,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
                 "    }\n  }\n  wave_sync();\n";
       else code += lanes(NS, "i", b) + "  wave_sync();\n";
     } else {   // W(e) = P_fa[i] M(e) P_mo[j] -> LDS; lanes over k: S(k) = sum_e T(e, k) W(e), P_off[k] *= S(k) in place
-      regp.clear();
+      regp.erase(to0);
       const int fa = from0, mo_ = from1, off_ = to0, csex = F.sex[off_];
       const int dw = g.a + g.b + g.c, ww = dw + 1;
       std::string b = "      const int i = e / " + nsS + ", j = e - i * " + nsS + ";\n      double w[" + S(ww) + "];\n";
