@@ -646,7 +646,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
   // Founders whose partial this part reads only through pristine type-2 steps (their states' prior x penetrance
   // terms): the partial is never stored; lane x keeps the state's penetrance (fp<i>) and the terms take it by
   // v_readlane at the term's (wave-uniform) state -- the same value the stored partial would have held
-  std::vector<char> regf(n, 0), regn(n, 0);
+  std::vector<char> regf(n, 0), regn(n, 0), iinit(n, 0);
   if (NS == 10 && part == 2 && multi <= 1 && g_regp) {
     const int finp = (F.steps.back().x >> 24) & 255;
     for (int i = 0; i < n; i++) regf[i] = F.founder[i] && i < F.nf && !leafp[i] && i != finp;
@@ -672,6 +672,19 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
     }
     for (int i = 0; i < n; i++)
       if (t2to[i] != 1) regn[i] = 0;
+    // persons whose first use is as the to-person of a type-2 step: their initial partial (penetrance, or prior x
+    // penetrance) is formed inside that step's lanes instead of being stored and read back
+    std::vector<char> seen(n, 0);
+    for (int k = 0; k < nst; k++) {
+      if (!inpart(k)) continue;
+      const int ty2 = F.steps[k].x & 255, f0 = (F.steps[k].x >> 8) & 255, f1 = (F.steps[k].x >> 16) & 255, t0 = (F.steps[k].x >> 24) & 255;
+      if (ty2 == 2 && !seen[t0] && !regf[t0]) iinit[t0] = 1;
+      seen[f0] = 1;
+      if (ty2 != 1) seen[t0] = 1;
+      if (ty2 == 3) seen[f1] = 1;
+    }
+    for (int i = 0; i < n; i++)
+      if (leafp[i]) iinit[i] = 0;
   }
   // InitializePartials x SetFounderPriors, one person at a time (lanes over its states)
   for (int i = 0; i < n; i++) {
@@ -680,7 +693,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
       code += lanes(NS, "x", "    fp" + S(i) + " = PEN[x * " + S(n) + " + " + S(i) + "];\n");
       continue;
     }
-    if (regn[i]) continue;   // (its type-2 step reads the penetrance itself)
+    if (regn[i] || iinit[i]) continue;   // (its type-2 step forms the initial partial itself)
     const bool fo = F.founder[i] && i < F.nf;
     const int sx = F.sex[i];
     const bool yf = NS == 3 && Y && sx == FEMALE;
@@ -884,7 +897,9 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
           const int2 Q = F.steps[k2];
           const int f2 = (Q.x >> 8) & 255, t2 = (Q.x >> 24) & 255, s2 = (Q.y >> 8) & 255;
           return std::vector<int>{pristine[k2], sd[k2].a, sd[k2].b, sd[k2].c, s2 == 255, capP[f2], capP[t2], s2 == 255 ? 0 : capM[s2],
-                                  d0[f2], (int)crows.count(s2), (int)regf[f2], (int)regn[t2]};
+                                  d0[f2], (int)crows.count(s2), (int)regf[f2], (int)regn[t2], (int)iinit[t2], F.founder[t2] && t2 < F.nf,
+                                  (F.founder[t2] && t2 < F.nf) ? ((Y && F.sex[t2] == FEMALE) ? 0 : (((X || Y) && F.sex[t2] == MALE) || MT) ? 1 : 2)
+                                                               : -1};
         };
         const std::vector<int> sg0 = sig2(kstep);
         for (int k2 = kstep + 1; k2 < nst && run.size() < 4; k2++) {
@@ -999,11 +1014,24 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
       const bool keep = NS == 10 && !mc && g_regp;   // (the outputs stay in registers for a following type-1 phase)
       const bool rn = keep && regn[stt];   // (the to-person is register-only: its partial was its penetrance)
       b += "    double t[" + S(g.c + 1) + "];\n";
-      if (rn) {
+      if (keep && iinit[stt]) {   // the initial partial at state i (InitializePartials x SetFounderPriors, as the init phase)
         std::string tp = S((F.steps[run.back()].x >> 24) & 255);   // (packed: the lane group's to-person)
         for (int r2 = (int)run.size() - 2; r2 >= 0; r2--) tp = "q_ == " + S(r2) + " ? " + S((F.steps[run[r2]].x >> 24) & 255) + " : " + tp;
-        b += "    t[0] = PEN[i * " + S(n) + " + (" + tp + ")];\n";
-        for (int c = 1; c <= g.c; c++) b += "    t[" + S(c) + "] = 0.0;\n";
+        const bool fo2 = F.founder[stt] && stt < F.nf;
+        const int sx2 = F.sex[stt];
+        const int dfull2 = !fo2 ? 0 : (Y && sx2 == FEMALE) ? 0 : (((X || Y) && sx2 == MALE) || MT) ? 1 : 2;
+        const int d2 = d0[stt];
+        b += "    const double pen_ = PEN[i * " + S(n) + " + (" + tp + ")];\n";
+        b += "    const int qi_ = i == g11 ? 0 : i == g12 ? 1 : i == g22 ? 2 : 3;\n    (void)qi_;\n";
+        for (int c = 0; c <= g.c; c++) {
+          std::string v = "0.0";
+          if (!fo2) v = c == 0 ? "pen_" : "0.0";
+          else if (top && dfull2 > 0) v = c == 0 ? "(qi_ == 0 ? pen_ : 0.0)" : "0.0";
+          else if (d2 == 2) v = c == 0 ? "(qi_ == 2 ? pen_ : 0.0)" : c == 1 ? "(qi_ == 1 ? 2 * pen_ : 0.0)" : c == 2 ? "(qi_ == 0 ? pen_ : 0.0)" : "0.0";
+          else if (d2 == 1) v = c == 0 ? "(qi_ == 2 ? pen_ : 0.0)" : c == 1 ? "(qi_ == 0 ? pen_ : 0.0)" : "0.0";
+          else v = c == 0 ? "(qi_ != 3 ? pen_ : 0.0)" : "0.0";
+          b += "    t[" + S(c) + "] = " + v + ";\n";
+        }
       } else
         for (int c = 0; c <= g.c; c++) b += "    t[" + S(c) + "] = W[" + OT + " + i * " + S(tcap) + " + " + S(c) + "];\n";
       const std::string xr = "xr" + S(kstep) + "_";
