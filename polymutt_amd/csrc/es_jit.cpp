@@ -448,7 +448,7 @@ extern "C" __global__ void __launch_bounds__(256) es_post_jit(PostArgs A) {
 bool g_tr_regs = false;
 bool g_prof = false;   // PM_ES_PROF=1: es_hoist_wave accumulates per-part clock cycles into Args::prof
 bool g_pack = true;    // PM_ES_PACK=0: independent type-2 steps one phase each
-bool g_regp = true;    // PM_ES_REGP=0: type-1 phases read the offspring coefficients from LDS only
+int g_regp = 1;        // PM_ES_REGP=0: type-1 phases read the offspring coefficients from LDS only; 2: every other one
 int g_expt = 0;        // PM_ES_EXPT=1/2: timing experiments only (results wrong), see the uses
 
 struct WaveGen {
@@ -671,7 +671,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
       else if (!t2to[f0]) regn[f0] = 0;   // (a type-1 read before the type-2 step)
     }
     for (int i = 0; i < n; i++)
-      if (t2to[i] != 1) regn[i] = 0;
+      if (t2to[i] != 1 || g_regp == 2) regn[i] = 0;
     // persons whose first use is as the to-person of a type-2 step: their initial partial (penetrance, or prior x
     // penetrance) is formed inside that step's lanes instead of being stored and read back
     std::vector<char> seen(n, 0);
@@ -830,7 +830,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
           const int2 Sq = F.steps[run[q]];
           const int offq = (Sq.x >> 8) & 255, ga = sd[run[q]].a;
           for (int a = 0; a <= ga; a++) {
-            if (regp.count(offq)) {   // from the lanes of the type-2 phase that computed it
+            if (regp.count(offq) && (g_regp != 2 || q % 2 == 1)) {   // from the lanes of the type-2 phase that computed it
               const std::string v = regp[offq].first + S(a), L = S(regp[offq].second) + " + k";
               c1 += "      {\n        const double p = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(" + v + "), " + L +
                     "), __builtin_amdgcn_readlane(__double2loint(" + v + "), " + L + "));\n";
@@ -1334,7 +1334,7 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
   const char* epk = getenv("PM_ES_PACK");
   g_pack = !(epk && epk[0] == '0');
   const char* erp = getenv("PM_ES_REGP");
-  g_regp = !(erp && erp[0] == '0');
+  g_regp = erp ? atoi(erp) : 1;
   const char* eex = getenv("PM_ES_EXPT");
   g_expt = eex ? atoi(eex) : 0;
   int ws = 1;
