@@ -448,7 +448,11 @@ extern "C" __global__ void __launch_bounds__(256) es_post_jit(PostArgs A) {
 bool g_tr_regs = false;
 bool g_prof = false;   // PM_ES_PROF=1: es_hoist_wave accumulates per-part clock cycles into Args::prof
 bool g_pack = true;    // PM_ES_PACK=0: independent type-2 steps one phase each
-int g_regp = 1;        // PM_ES_REGP=0: type-1 phases read the offspring coefficients from LDS only; 2: every other one
+// PM_ES_REGP: how a type-1 phase reads the offspring coefficients a preceding type-2 phase computed -- 0 from LDS,
+// 1 all by v_readlane (the non-founder is then never stored), 2 (default) every other offspring of a run by
+// v_readlane and the rest from LDS: the readlanes are VALU work and the LDS reads LDS work, and the two pipes are
+// best balanced half and half (ext10: 0.667 / 0.617 / 0.555 ms per hoisting launch)
+int g_regp = 2;
 int g_expt = 0;        // PM_ES_EXPT=1/2: timing experiments only (results wrong), see the uses
 
 struct WaveGen {
@@ -1334,7 +1338,7 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
   const char* epk = getenv("PM_ES_PACK");
   g_pack = !(epk && epk[0] == '0');
   const char* erp = getenv("PM_ES_REGP");
-  g_regp = erp ? atoi(erp) : 1;
+  g_regp = erp ? atoi(erp) : 2;
   const char* eex = getenv("PM_ES_EXPT");
   g_expt = eex ? atoi(eex) : 0;
   int ws = 1;
