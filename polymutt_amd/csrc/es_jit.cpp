@@ -453,6 +453,7 @@ bool g_pack = true;    // PM_ES_PACK=0: independent type-2 steps one phase each
 // v_readlane and the rest from LDS: the readlanes are VALU work and the LDS reads LDS work, and the two pipes are
 // best balanced half and half (ext10: 0.667 / 0.617 / 0.555 ms per hoisting launch)
 int g_regp = 2;
+bool g_regf = true;    // PM_ES_REGF=0: pristine founders stored and read from LDS (with PM_ES_REGP != 0)
 int g_expt = 0;        // PM_ES_EXPT=1/2: timing experiments only (results wrong), see the uses
 
 struct WaveGen {
@@ -653,7 +654,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
   std::vector<char> regf(n, 0), regn(n, 0), iinit(n, 0);
   if (NS == 10 && part == 2 && multi <= 1 && g_regp) {
     const int finp = (F.steps.back().x >> 24) & 255;
-    for (int i = 0; i < n; i++) regf[i] = F.founder[i] && i < F.nf && !leafp[i] && i != finp;
+    for (int i = 0; i < n; i++) regf[i] = g_regf && F.founder[i] && i < F.nf && !leafp[i] && i != finp;
     for (int k = 0; k < nst; k++) {
       if (!inpart(k)) continue;
       const int ty2 = F.steps[k].x & 255, f0 = (F.steps[k].x >> 8) & 255, f1 = (F.steps[k].x >> 16) & 255, t0 = (F.steps[k].x >> 24) & 255;
@@ -1339,6 +1340,8 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
   g_pack = !(epk && epk[0] == '0');
   const char* erp = getenv("PM_ES_REGP");
   g_regp = erp ? atoi(erp) : 2;
+  const char* erf = getenv("PM_ES_REGF");
+  g_regf = !(erf && erf[0] == '0');
   const char* eex = getenv("PM_ES_EXPT");
   g_expt = eex ? atoi(eex) : 0;
   int ws = 1;
