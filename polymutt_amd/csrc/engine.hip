@@ -86,6 +86,8 @@ struct pm_engine {
   int *d_ext_count1 = nullptr, *d_ext_fam1 = nullptr;
   // --quick_call: the MakeUnrelated() plan (every family an all-founder product) with its own geometry
   int Tq = 0, Sq = 0, grid_q = 0;
+  int quad_bpc16 = 0, quad_bpc8 = 0;   // QUAD k_brent blocks resident per CU (occupancy query, first launch)
+  bool units_empty = false, units1_empty = false;   // a lane plan with no nuclear or founder unit (every family peeled)
   int4* d_units_q = nullptr;
   int* d_items[N_LISTS] = {nullptr, nullptr, nullptr};
   int* d_counts = nullptr;
@@ -422,6 +424,7 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
   HIP_TRY(hipMemcpy(E->d_mo, mo.data(), sizeof(int) * ped->n_person, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(E->d_sex, ped->sex, ped->n_person, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(E->d_units, units.data(), sizeof(int4) * units.size(), hipMemcpyHostToDevice));
+  E->units_empty = std::all_of(units.begin(), units.end(), [](const int4& u) { return u.x == U_NONE; });
   {   // k_posterior's family order: by kind, then size (mixed trio / quad pedigrees: no divergent family-size paths)
     std::vector<int> perm(ped->n_fam);
     for (int f = 0; f < ped->n_fam; f++) perm[f] = f;
@@ -585,6 +588,7 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
         DALLOC(E->d_ext_count1, E->T1);
         DALLOC(E->d_ext_fam1, e1.size());
         HIP_TRY(hipMemcpy(E->d_units1, u1.data(), sizeof(int4) * u1.size(), hipMemcpyHostToDevice));
+        E->units1_empty = std::all_of(u1.begin(), u1.end(), [](const int4& u) { return u.x == U_NONE; });
         HIP_TRY(hipMemcpy(E->d_ext_count1, c1.data(), sizeof(int) * E->T1, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(E->d_ext_fam1, e1.data(), sizeof(int) * e1.size(), hipMemcpyHostToDevice));
         E->grid1 = E->n_cu * std::max(1, 1024 / E->T1);
@@ -882,14 +886,30 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
   const bool quad = !gen && !unrelated && n_ext == 0 && A.denovo && E->par.numerics == PM_NUM_POLY && E->quad && T == 64 &&
                     (S == 8 || S == 16);
   if (quad) shmem = QWAVE;
+  BrentFn qfn = nullptr;
+  if (quad) {   // persistent grid = the blocks that are resident at once (PM_QD_WAVES per SIMD): no partial second round
+    qfn = S == 16 ? k_brent<64, 16, PM_NUM_POLY, false, false, true, false, false, true>
+                  : k_brent<64, 8, PM_NUM_POLY, false, false, true, false, false, true>;
+    int& bpc = S == 16 ? E->quad_bpc16 : E->quad_bpc8;
+    if (bpc == 0) {
+      int n = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)qfn, 64, shmem) != hipSuccess || n <= 0) {
+        (void)hipGetLastError();
+        n = 1024 / 64;
+      }
+      bpc = n;
+      if (getenv("PM_QD_BPC")) bpc = std::max(1, atoi(getenv("PM_QD_BPC")));
+    }
+    grid = E->n_cu * bpc;
+    grid -= grid % 8;   // (the XCD-aware item order)
+  }
   if (!quad && !gen && !unrelated && n_ext == 0 && A.denovo && E->par.numerics == PM_NUM_POLY && E->max_nuc <= 4 && S % DN_PF_C == 0 &&
       E->n_person % 16 == 0 && E->n_person >= 16 && !getenv("PM_NO_PREFETCH")) {
     A.dn_pf = 1;
     shmem = (size_t)(T / 64) * 2 * DN_PF_BUF;
   }
   const bool ep = !unrelated && n_ext > 0 && E->es_poly && E->par.numerics == PM_NUM_POLY;
-  BrentFn fn = quad ? (S == 16 ? k_brent<64, 16, PM_NUM_POLY, false, false, true, false, false, true>
-                              : k_brent<64, 8, PM_NUM_POLY, false, false, true, false, false, true>)
+  BrentFn fn = quad ? qfn
                    : brent_kernel(T, S, E->par.numerics, gen, !unrelated && n_ext > 0, A.denovo != 0, A.pf_npad > 0 || A.dn_pf, ep);
   if (!fn) { pm_set_last_error("launch_brent: no kernel variant for the lane plan"); return PM_EINVAL; }
   // multi-wave de novo plans (T = 512 / 1024: more than 1024 families) stage 2 buffers per wave: above the
@@ -907,6 +927,7 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
   A.ws_lds = 0;
   if (ep) {   // polynomial-form peels: coefficients from k_es_hoist, no workspace in k_brent
     A.es_poly = 1;
+    A.ep_only = (E->use_plan1 ? E->units1_empty : E->units_empty) && !getenv("PM_NO_EP_ONLY");
   } else if (!unrelated && n_ext > 0 && !E->par.denovo) {   // BA peels (the 10-state one is too big)
     const size_t need = (size_t)E->ws_per_lane * T * sizeof(double);
     if (need > 0 && need <= 150 * 1024) {

@@ -39,6 +39,15 @@
 #ifndef PM_HOIST_CHUNK
 #define PM_HOIST_CHUNK 4
 #endif
+#ifndef PM_QD_NC4
+#define PM_QD_NC4 0   // QUAD plans: 4 normalised coefficients per family (hoist_quad_t; measured slower at 2 waves)
+#endif
+#ifndef PM_QD_WAVES
+#define PM_QD_WAVES 2   // QUAD plans: waves per SIMD the k_brent instantiation is compiled for (launch bounds, grid)
+#endif
+#ifndef PM_QD_KIDSEQ
+#define PM_QD_KIDSEQ 0   // QUAD de novo hoisting: the two kids' lookups one kid at a time
+#endif
 #ifndef PM_QD_MONO
 #define PM_QD_MONO 1
 #endif
@@ -124,6 +133,7 @@ struct DevArgs {
   int pf_dw;               // ... in 4-byte pieces (n_person % 16 != 0, n_person % 4 == 0)
   int dn_pf;               // lean --denovo kernel: PL windows staged through LDS by LDS-DMA (hoist_poly4_dn_pf)
   int quad_full;           // QUAD plan (hoist_quad): slot rows below this have no empty lane
+  int ep_only;             // EP launches: the lane plan has no nuclear or founder units (every family is peeled)
   // tables
   const double* lktab;     // [256]
   const double* M;         // [100] genotype mutation matrix
@@ -1145,9 +1155,15 @@ __device__ __forceinline__ void quad_poly4(const double (*D)[3], const double* l
 // QUAD hoisting of one item: slots 0 .. QD_AHEAD - 1 are already in the ring (quad_prefetch).  vmcnt counts in
 // issue order (loads, stores and LDS-DMA together), so waiting until only the next slot's three DMA instructions
 // may be outstanding means this slot's have landed.
-template <int S, bool DNV>
+// NC = 4 (PM_QD_NC4): each family's quartic is stored normalised by its constant term a4 (> 0: every PL likelihood
+// and mutation-matrix dot product is positive), b_k = a_k / a4 for k = 0..3, and the lane's product of the a4 is
+// kept as one (mantissa, exponent) pair (m0, e0) that seeds the evaluation's product: 4 x S registers of
+// coefficients instead of 5 x S, so the 16-slot kernel runs 3 waves per SIMD.  h(r) = a4 (b0 r^4 + .. + b3 r + 1):
+// still non-negative throughout, the normalisation adds one rounding per coefficient.
+template <int S, bool DNV, int NC>
 __device__ __forceinline__ void hoist_quad_t(const DevArgs& A, const ItemCtx& I, const uint8_t* pl, const double* lk,
-                                             const double* M, double (*a)[5], uint8_t* ring, const uint32_t* voff) {
+                                             const double* M, double (*a)[NC], uint8_t* ring, const uint32_t* voff, double& m0, int& e0) {
+  if constexpr (NC == 4) { m0 = 1.0; e0 = 0; }
   const int lane = threadIdx.x & 63;
   const uint32_t* rw = (const uint32_t*)ring + lane;   // the lane's dword of plane g, slot buffer b: rw[(b * QSLOT + g * 256) / 4]
   const int o11 = I.g11 * 64, o12 = I.g12 * 64, o22 = I.g22 * 64;
@@ -1170,9 +1186,10 @@ __device__ __forceinline__ void hoist_quad_t(const DevArgs& A, const ItemCtx& I,
       for (int g = 0; g < 10; g++) wg[g] = b[g * 64];
 #pragma unroll
       for (int k = 0; k < 3; k++) { lF[k] = lk[w[k] & 0xFF]; lM[k] = lk[(w[k] >> 8) & 0xFF]; }
-      double pg[2][10];   // both kids' 20 table lookups in flight together
+      double pg[2][10];   // both kids' 20 table lookups in flight together (PM_QD_KIDSEQ: one kid at a time)
+      if constexpr (!PM_QD_KIDSEQ)
 #pragma unroll
-      for (int g = 0; g < 10; g++) { pg[0][g] = lk[(wg[g] >> 16) & 0xFF]; pg[1][g] = lk[wg[g] >> 24]; }
+        for (int g = 0; g < 10; g++) { pg[0][g] = lk[(wg[g] >> 16) & 0xFF]; pg[1][g] = lk[wg[g] >> 24]; }
       // the item's three mutation-matrix rows from the kernel arguments (scalar loads issued beside the lookups):
       // scalar FMA operands, no LDS read per slot
       double mr[3][10];
@@ -1180,16 +1197,32 @@ __device__ __forceinline__ void hoist_quad_t(const DevArgs& A, const ItemCtx& I,
       for (int g = 0; g < 10; g++) { mr[0][g] = A.Mk[I.g11 * 10 + g]; mr[1][g] = A.Mk[I.g12 * 10 + g]; mr[2][g] = A.Mk[I.g22 * 10 + g]; }
       __builtin_amdgcn_sched_barrier(0);
       if (s + QD_AHEAD < S) quad_dma(pl, s + QD_AHEAD, npo, voff, ring + ((s + QD_AHEAD) % QB) * QSLOT);
+      if constexpr (PM_QD_KIDSEQ) {
 #pragma unroll
-      for (int q = 0; q < 2; q++) D[q][0] = D[q][1] = D[q][2] = 0.0;
+        for (int q = 0; q < 2; q++) {   // one kid at a time: 10 lookups in flight (register pressure at 3 waves / SIMD)
 #pragma unroll
-      for (int g = 0; g < 10; g++) {   // CalcDenovoMutLk (:1553-1562), each matrix entry read once for both kids
-        const double m11 = mr[0][g], m12 = mr[1][g], m22 = mr[2][g];
+          for (int g = 0; g < 10; g++) pg[q][g] = lk[(wg[g] >> (16 + 8 * q)) & 0xFF];
+          D[q][0] = D[q][1] = D[q][2] = 0.0;
 #pragma unroll
-        for (int q = 0; q < 2; q++) {
-          D[q][0] = fma(m11, pg[q][g], D[q][0]);
-          D[q][1] = fma(m12, pg[q][g], D[q][1]);
-          D[q][2] = fma(m22, pg[q][g], D[q][2]);
+          for (int g = 0; g < 10; g++) {   // CalcDenovoMutLk (:1553-1562)
+            D[q][0] = fma(mr[0][g], pg[q][g], D[q][0]);
+            D[q][1] = fma(mr[1][g], pg[q][g], D[q][1]);
+            D[q][2] = fma(mr[2][g], pg[q][g], D[q][2]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 2; q++) D[q][0] = D[q][1] = D[q][2] = 0.0;
+#pragma unroll
+        for (int g = 0; g < 10; g++) {   // CalcDenovoMutLk (:1553-1562), each matrix entry read once for both kids
+          const double m11 = mr[0][g], m12 = mr[1][g], m22 = mr[2][g];
+#pragma unroll
+          for (int q = 0; q < 2; q++) {
+            D[q][0] = fma(m11, pg[q][g], D[q][0]);
+            D[q][1] = fma(m12, pg[q][g], D[q][1]);
+            D[q][2] = fma(m22, pg[q][g], D[q][2]);
+          }
         }
       }
     } else {   // cfg-7 items: likelihoodONEKid's autosomal terms on the item's three planes
@@ -1202,34 +1235,53 @@ __device__ __forceinline__ void hoist_quad_t(const DevArgs& A, const ItemCtx& I,
       __builtin_amdgcn_sched_barrier(0);
       if (s + QD_AHEAD < S) quad_dma(pl, s + QD_AHEAD, npo, voff, ring + ((s + QD_AHEAD) % QB) * QSLOT);
     }
-    quad_poly4(D, lF, lM, a[s]);
+    double q5x[5];
+    double* q5 = NC == 5 ? a[s] : q5x;   // (NC = 5: the quartic straight into the slot's registers)
+    quad_poly4(D, lF, lM, q5);
     if (s >= qfull) {   // the partial last slot row: empty lanes hold the phantom family (f + g)^4
       const bool empty = 64 * s + lane >= nfam;
-      a[s][0] = empty ? 1.0 : a[s][0]; a[s][1] = empty ? 4.0 : a[s][1]; a[s][2] = empty ? 6.0 : a[s][2];
-      a[s][3] = empty ? 4.0 : a[s][3]; a[s][4] = empty ? 1.0 : a[s][4];
+      q5[0] = empty ? 1.0 : q5[0]; q5[1] = empty ? 4.0 : q5[1]; q5[2] = empty ? 6.0 : q5[2];
+      q5[3] = empty ? 4.0 : q5[3]; q5[4] = empty ? 1.0 : q5[4];
+    }
+    if constexpr (NC == 4) {
+      // 1 / a4 from the hardware reciprocal and two Newton steps (within an ulp), then the four quotients
+      double y = __builtin_amdgcn_rcp(q5[4]);
+      double ee = fma(-q5[4], y, 1.0);
+      y = fma(y, ee, y);
+      ee = fma(-q5[4], y, 1.0);
+      y = fma(y, ee, y);
+#pragma unroll
+      for (int k = 0; k < 4; k++) a[s][k] = q5[k] * y;
+      int x;
+      m0 = frexp(m0 * q5[4], &x);   // a4 >= ~1e-120: one factor per renormalisation
+      e0 += x;
+      // pinned here: otherwise IR-level sinking moves every slot's arithmetic past the hoisting loop, where all the
+      // slots' table lookups are then live at once (2 KB of spills)
+      asm volatile("" : "+v"(a[s][0]), "+v"(a[s][1]), "+v"(a[s][2]), "+v"(a[s][3]), "+v"(m0), "+v"(e0));
     }
     __builtin_amdgcn_sched_barrier(0);
   }
 }
 
 // de novo items and cfg-7 items (uniform per item) take separate straight-line slot loops
-template <int S>
+template <int S, int NC>
 __device__ __forceinline__ void hoist_quad(const DevArgs& A, const ItemCtx& I, const uint8_t* pl, const double* lk,
-                                           const double* M, double (*a)[5], uint8_t* ring, const uint32_t* voff) {
-  if (I.denovo) hoist_quad_t<S, true>(A, I, pl, lk, M, a, ring, voff);
-  else hoist_quad_t<S, false>(A, I, pl, lk, M, a, ring, voff);
+                                           const double* M, double (*a)[NC], uint8_t* ring, const uint32_t* voff, double& m0, int& e0) {
+  if (I.denovo) hoist_quad_t<S, true, NC>(A, I, pl, lk, M, a, ring, voff, m0, e0);
+  else hoist_quad_t<S, false, NC>(A, I, pl, lk, M, a, ring, voff, m0, e0);
 }
 
 // f = 1 (the generic-path de novo monomorphism item): L_fam(1) = a0, the f^4 coefficient; an empty slot's
 // phantom family (f + g)^4 has a0 = 1, so no slot needs masking.  Four interleaved (mantissa, exponent)
 // accumulators, renormalised after every factor.
-template <int S>
-__device__ __forceinline__ void lane_poly_top(const double (*a)[5], double& m, int& e) {
+template <int S, int NC = 5>
+__device__ __forceinline__ void lane_poly_top(const double (*a)[NC], double& m, int& e, double m0 = 1.0, int e0 = 0) {
   constexpr int NA = S < 4 ? S : 4;
   double am[NA];
   int ae[NA];
 #pragma unroll
   for (int j = 0; j < NA; j++) { am[j] = 1.0; ae[j] = 0; }
+  am[0] = m0; ae[0] = e0;   // (NC = 4: the lane's product of the a4, so that a0 = b0 a4)
 #pragma unroll
   for (int s = 0; s < S; s++) {
     int x;
@@ -1251,16 +1303,20 @@ __device__ __forceinline__ void lane_poly_top(const double (*a)[5], double& m, i
 // Hot form: L_fam(f) = g^4 h(r), h(r) = a0 r^4 + a1 r^3 + a2 r^2 + a3 r + a4 with r = f / g, g = 1 - f
 // (non-negative coefficients: no cancellation, relative error <= ~8 ulp for any r).  g4 = g^4 is folded
 // into every slot, so the objective needs no log10(g); empty slots hold the phantom family (f + g)^4.
-template <int S>
-__device__ __forceinline__ void lane_poly_r(double r, double g4, const double (*a)[5], double& m, int& e) {
+// NC = 4: normalised coefficients (b0..b3, constant term 1) and the lane's product of the a4 as the seed (m0, e0):
+// h = b0 r^4 + .. + b3 r + 1 >= 1, so two factors of g4 h stay within range as before.
+template <int S, int NC = 5>
+__device__ __forceinline__ void lane_poly_r(double r, double g4, const double (*a)[NC], double& m, int& e, double m0 = 1.0, int e0 = 0) {
   constexpr int NA = S < 4 ? S : 4;
   double am[NA];
   int ae[NA];
 #pragma unroll
   for (int j = 0; j < NA; j++) { am[j] = 1.0; ae[j] = 0; }
+  am[0] = m0; ae[0] = e0;
 #pragma unroll
   for (int s = 0; s < S; s++) {
-    const double h = fma(r, fma(r, fma(r, fma(r, a[s][0], a[s][1]), a[s][2]), a[s][3]), a[s][4]) * g4;
+    const double h = (NC == 4 ? fma(r, fma(r, fma(r, fma(r, a[s][0], a[s][1]), a[s][2]), a[s][3]), 1.0)
+                              : fma(r, fma(r, fma(r, fma(r, a[s][0], a[s][1]), a[s][2]), a[s][3]), a[s][NC - 1])) * g4;
     am[s % NA] = am[s % NA] * h;
     // renormalise after every second factor of an accumulator (and after the last): a nuclear family's
     // likelihood is >= ~1e-118 (PL <= 255 per person, HWE prior >= 1e-16), so two factors on a mantissa in
@@ -1658,18 +1714,18 @@ constexpr int brent_waves() { return (NUM == PM_NUM_POLY && !GEN && (T == 64 || 
 // reference-order peel (d_es_lk) is compiled out, and the block asks for 2 waves per SIMD.
 // QD: lean --denovo kernel on a QUAD plan (hoist_quad: coalesced dword loads, prefetched across items).
 template <int T, int S, int NUM, bool GEN, bool ES, bool DN = false, bool PF = false, bool EP = false, bool QD = false>
-__global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k_brent(DevArgs A, int list) {
+__global__ void __launch_bounds__(T, (EP ? 2 : QD ? PM_QD_WAVES : brent_waves<T, S, NUM, GEN>())) k_brent(DevArgs A, int list) {
   constexpr bool PROD = NUM != PM_NUM_EXACT;
   constexpr bool POLYK = NUM == PM_NUM_POLY && !GEN;
   __shared__ double s_lk[256];
   __shared__ double s_M[(GEN || DN) ? 100 : 1];
   __shared__ double s_red[T > 64 ? 96 : 1];
   __shared__ int s_rede[T > 64 ? 32 : 1];
-  __shared__ __attribute__((aligned(16))) int s_u[POLYK ? S * T : 4];   // packed lane plan (unit_pack, lane-major)
+  __shared__ __attribute__((aligned(16))) int s_u[POLYK && !QD ? S * T : 4];   // packed lane plan (unit_pack, lane-major)
   for (int i = threadIdx.x; i < 256; i += T) s_lk[i] = A.lktab[i];
   if constexpr (GEN || DN)
     for (int i = threadIdx.x; i < 100; i += T) s_M[i] = A.M[i];
-  if constexpr (POLYK)
+  if constexpr (POLYK && !QD)   // (QUAD plans address families by slot and lane: no lane plan)
 #pragma unroll
     for (int s = 0; s < S; s++) s_u[threadIdx.x * S + s] = unit_pack(A.units[s * T + threadIdx.x]);
   __syncthreads();
@@ -1745,8 +1801,10 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
     const uint8_t* pl = A.pl + (size_t)site * A.n_person * 10;
     // POLY (lean product kernel, always the autosomal HWE prior with > 1 family): 5 coefficients per family
     constexpr bool POLY = NUM == PM_NUM_POLY && !GEN;
-    constexpr int NC = POLY ? 5 : 9;
+    constexpr int NC = POLY ? ((QD && PM_QD_NC4) ? 4 : 5) : 9;
     double cond[S][NC];
+    double lm0 = 1.0;   // NC = 4: the lane's product of the families' a4 (hoist_quad_t)
+    int le0 = 0;
     int fl[S];
     bool hoisted = false;
     if constexpr (POLY) {
@@ -1763,7 +1821,7 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
         }
       }
       if constexpr (QD) {
-        hoist_quad<S>(A, I, pl, s_lk, s_M, cond, qring, qvoff);
+        hoist_quad<S, NC>(A, I, pl, s_lk, s_M, cond, qring, qvoff, lm0, le0);
         hoisted = true;
         const int itn = it + gridDim.x;   // the next item's first slots land during this item's Brent
         // (landed: the hoisting ended with vmcnt(0)); uniform, so the next site's addresses are scalar
@@ -1777,7 +1835,7 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
         const bool mdn = PM_QD_MONO && A.mono_dn == 2 && cfg == 1;
         if (mdn) {
           double m; int e;
-          lane_poly_top<S>((const double(*)[5])cond, m, e);
+          lane_poly_top<S, NC>((const double(*)[NC])cond, m, e, lm0, le0);
           mono_dn = block_logprod<T>(m, e, s_red, s_rede, par);
         }
         if (threadIdx.x == 0) {
@@ -1798,7 +1856,7 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
           q_item = nitem;
         }
       }
-      if (!PFK && !QD && !hoisted && A.max_nuc <= 4) {
+      if constexpr (!QD) if (!PFK && !hoisted && A.max_nuc <= 4) {
         if constexpr (DN) {   // de novo and cfg-7 items
           if constexpr (DNPF_ONLY) hoist_poly4_dn_pf<S, T>(A, s_u, I, pl, s_lk, s_M, cond, s_pf + (threadIdx.x >> 6) * 2 * DN_PF_BUF);
           else if constexpr (S % DN_PF_C == 0) {
@@ -1813,7 +1871,8 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
 #pragma unroll
     for (int s = 0; s < S; s++) {
       fl[s] = 0;
-      if (PFK || DNPF_ONLY || QD || hoisted) continue;
+      if constexpr (QD) continue;
+      if (PFK || DNPF_ONLY || hoisted) continue;
       if constexpr (POLY) {
         const int4 u = A.units[s * T + threadIdx.x];   // L1/L2-resident; not kept in registers
         double c9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -1833,18 +1892,26 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
     constexpr int EPE = (EP && T == 64) ? PM_EPE : 0;
     double ce[EPE ? EPE : 1][EPE ? PDM + 1 : 1];
     int ed[EPE ? EPE : 1];
+    // EPR: the register families' degrees summed (the lane's power of g) and whether any family of the wave is
+    // evaluated from the coefficient buffer instead (more than PM_EPE on a lane, or D > PDM)
+    int edl = 0;
+    bool epmem = true;
     // EP: the lane's extended families' coefficients, peeled for this item by k_es_hoist
     const double* coef = (ES && EP) ? A.es_coef + (size_t)(it - A.es_it0) * A.max_ext * A.poly_dcap * T + threadIdx.x : nullptr;
     if constexpr (ES && EP) {
       const int cnt = A.ext_count ? A.ext_count[threadIdx.x] : 0;
+      bool mem = cnt > EPE;
 #pragma unroll
       for (int q = 0; q < EPE; q++) {
         const double* co = coef + (size_t)q * A.poly_dcap * T;
         ed[q] = q < cnt ? (int)co[(size_t)(A.poly_dcap - 1) * T] : -1;
-        if (ed[q] > PDM) ed[q] = -1;
+        if (ed[q] > PDM) { ed[q] = -1; mem = true; }
 #pragma unroll
         for (int a = 0; a <= PDM; a++) ce[q][a] = a <= ed[q] ? co[(size_t)a * T] : 0.0;
+        if (ed[q] < 0) ce[q][0] = 1.0;   // (an absent family: the unit polynomial, D = 0 -- the t-form loop is branch-free)
+        edl += ed[q] < 0 ? 0 : ed[q];
       }
+      if constexpr (EPE > 0) epmem = __ballot(mem) != 0;
     }
     if (A.phase) { const unsigned long long t = wall_clock64(); ph_h += t - ph_t; ph_t = t; }
     const bool single = !A.vcf && ((cfg == 0) || (A.single_nuclear && !A.unrelated));
@@ -1870,26 +1937,53 @@ __global__ void __launch_bounds__(T, (EP ? 2 : brent_waves<T, S, NUM, GEN>())) k
         double m; int e;
         if (__builtin_amdgcn_readfirstlane((int)(g > 0.0))) {
           // (r from the hardware reciprocal + a Newton step instead of the division: measured no faster)
-          lane_poly_r<S>(pos_div(x, g), (g * g) * (g * g), (const double(*)[5])cond, m, e);
+          lane_poly_r<S, NC>(pos_div(x, g), (g * g) * (g * g), (const double(*)[NC])cond, m, e, lm0, le0);
           tot = block_logprod<T>(m, e, s_red, s_rede, par);
         } else {
-          lane_poly_top<S>((const double(*)[5])cond, m, e);   // x = 1: L = a0 per family, log10(x^4) = 0
+          lane_poly_top<S, NC>((const double(*)[NC])cond, m, e, lm0, le0);   // x = 1: L = a0 per family, log10(x^4) = 0
           tot = block_logprod<T>(m, e, s_red, s_rede, par);
         }
       } else if (PROD) {
-        double m; int e;
-        lane_prod<S, GEN>(x, unit, (const double(*)[9])cond, fl, pmode, m, e);
+        double m = 1.0; int e = 0;
+        if (!(ES && EP && A.ep_only)) lane_prod<S, GEN>(x, unit, (const double(*)[9])cond, fl, pmode, m, e);
         if constexpr (ES && EP && EPE > 0) {   // register-resident coefficients first (independent Horner chains)
+          const double g = 1 - x;
+          if (__builtin_amdgcn_readfirstlane((int)(g > 0.0))) {
+            // EPR: every family in the one direction L = g^D sum_a c_a t^a, t = f / g (t in [1e-4, 1e4] on Brent's
+            // bracket; non-negative terms, no cancellation), by FMA Horner over the PDM + 1 registers (zeros above D
+            // leave the sum's bits unchanged); g^D of all the lane's families as one power g^edl (edl <= 32).  The
+            // t (one division) and the powers of g are shared by the lane's families.
+            const double t = pos_div(x, g);
+            double gp = g, pw = 1.0;
 #pragma unroll
-          for (int q = 0; q < EPE; q++)
-            if (ed[q] >= 0) {
-              int e1, e2;
-              const double mv = frexp(es_poly_eval_r(ce[q], ed[q], x), &e1);
-              m = frexp(m * mv, &e2);
-              e += e1 + e2;
+            for (int b = 0; b < 6; b++) {
+              pw = ((edl >> b) & 1) ? pw * gp : pw;
+              gp = gp * gp;
             }
+#pragma unroll
+            for (int q = 0; q < EPE; q++) {
+              double acc = ce[q][PDM];
+#pragma unroll
+              for (int a = PDM - 1; a >= 0; a--) acc = fma(acc, t, ce[q][a]);
+              int e1;
+              m = frexp(m * acc, &e1);   // (one factor per renormalisation: a peeled family's L can be ~1e-290)
+              e += e1;
+            }
+            int e2;
+            m = frexp(m * pw, &e2);
+            e += e2;
+          } else {   // f = 1 (the de novo monomorphism item): the f^D coefficient of each family
+#pragma unroll
+            for (int q = 0; q < EPE; q++)
+              if (ed[q] >= 0) {
+                int e1, e2;
+                const double mv = frexp(es_poly_eval_r(ce[q], ed[q], x), &e1);
+                m = frexp(m * mv, &e2);
+                e += e1 + e2;
+              }
+          }
         }
-        if (ES && A.ext_count)   // extended families of this lane: Elston-Stewart peeling per evaluation
+        if (ES && A.ext_count && (EPE == 0 || epmem))   // extended families of this lane: Elston-Stewart peeling per evaluation
           for (int q = 0; q < A.ext_count[threadIdx.x]; q++) {
             const int f = A.ext_fam[q * T + threadIdx.x];
             double v;

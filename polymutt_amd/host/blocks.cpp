@@ -237,8 +237,22 @@ void BlockSiteSource::fill(const int* rowOf, uint8_t* pl, uint32_t* dm) {
     add((char*)(dm + (size_t)r * np_), dmOff_ + (uint64_t)s * rdm, (size_t)m * rdm);
     i = j;
   }
-  if (pool_ && pieces.size() > 1) pool_->run((int)pieces.size(), [&](int k) { readAt(pieces[k].dst, pieces[k].off, pieces[k].len); });
-  else for (auto& p : pieces) readAt(p.dst, p.off, p.len);
+  if (pool_ && pieces.size() > 1) {
+    // a failed or short read on a worker is recorded and rethrown here, on the calling thread (TaskPool::run does not
+    // carry exceptions: one escaping a worker would end the process without the "truncated" message)
+    std::vector<std::string> err(pieces.size());
+    pool_->run((int)pieces.size(), [&](int k) {
+      try {
+        readAt(pieces[k].dst, pieces[k].off, pieces[k].len);
+      } catch (const std::exception& e) {
+        err[k] = e.what();
+      }
+    });
+    for (auto& e : err)
+      if (!e.empty()) throw FatalError(e);
+  } else {
+    for (auto& p : pieces) readAt(p.dst, p.off, p.len);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -105,8 +105,9 @@ int pmh_run_polymutt(int argc, char** argv, int32_t rank, int32_t world, int32_t
     };
   }
   return pmhost::polymutt_main(argc, argv, &comm, [&](const pm_pedigree& v, const pm_params& par, const pmhost::Options& opt) {
-    // (several engines only where batches are pipelined: one process, no --pos; a shard or --pos run uses one)
-    const int engines = (world > 1 || opt.force_call || getenv("PM_SERIAL")) ? 1 : opt.engines;
+    // (several engines only where batches are pipelined: one process, GLF or block input, no --pos; a shard, --pos or
+    // --in_vcf run uses one -- run_polymutt_vcf evaluates on the first engine only)
+    const int engines = (world > 1 || opt.force_call || !opt.vcfInFile.empty() || getenv("PM_SERIAL")) ? 1 : opt.engines;
     return std::unique_ptr<pmhost::SiteEvaluator>(
         new pmhost::EngineEvaluator(v, par, device >= 0 ? device : opt.device, opt.batch, engines));
   });

@@ -761,6 +761,9 @@ int polymutt_main(int argc, char** argv, const ShardComm* comm, const EvaluatorF
   } catch (const FatalError& e) {
     printf("\nFATAL ERROR - \n%s\n\n", e.what());
     return 1;
+  } catch (const BrentError& e) {
+    printf("\nFATAL NUMERIC ERROR - %s\n\n", e.what());
+    return 1;
   }
 }
 

@@ -9,7 +9,8 @@
 // famlk[0]'s stale posterior state (pm_engine_set_posterior_carry) depends on whether any earlier site reached
 // CalcPostProb; it changes only chrX/Y genotype posteriors (likelihoodONEKid's member sex).  So on
 // autosomal sections batches run concurrently, and on chrX/Y/MT sections one at a time, each engine being told the
-// state from the results collected so far before its batch is submitted.
+// state from the results collected so far before its batch is submitted.  The exception is --denovo: its
+// posteriors do not read the carry (d_member_sex_before), so chrX/Y/MT batches stay concurrent there (in_flight()).
 #pragma once
 #include <chrono>
 #include <cstdio>
@@ -53,7 +54,7 @@ class EngineEvaluator : public SiteEvaluator {
            int* n_rows) override {
     check(pm_engine_set_posterior_carry(eng_[0], seen_ ? 1 : 0));
     int rc = pm_engine_run(eng_[0], n, pl, dm, ref, 0, res, calls, n_rows);
-    if (rc == PM_EBRENT) { printf("\nFATAL NUMERIC ERROR - ScalarMinimizer::Brent got stuck\n\n"); exit(1); }
+    if (rc == PM_EBRENT) throw BrentError();
     check(rc);
     note(res, n);
   }
@@ -84,7 +85,7 @@ class EngineEvaluator : public SiteEvaluator {
     q_.pop_front();
     int rows = 0;
     int rc = pm_engine_collect(j.e, j.res, j.calls, &rows);
-    if (rc == PM_EBRENT) { printf("\nFATAL NUMERIC ERROR - ScalarMinimizer::Brent got stuck\n\n"); exit(1); }
+    if (rc == PM_EBRENT) throw BrentError();   // (the driver drains the writer first: no exit() with threads live)
     check(rc);
     note(j.res, j.n);
     return rows;

@@ -16,6 +16,9 @@ namespace pmhost {
 
 // Thrown for conditions where the reference calls error() (prints "FATAL ERROR" and exits 1).
 struct FatalError : std::runtime_error { explicit FatalError(const std::string& m) : std::runtime_error(m) {} };
+// Thrown where the reference calls numerror("ScalarMinimizer::Brent got stuck") (MathGold.cpp): the driver writes every
+// record before the failing batch, then prints the reference's "FATAL NUMERIC ERROR" text and returns 1.
+struct BrentError : std::runtime_error { BrentError() : std::runtime_error("ScalarMinimizer::Brent got stuck") {} };
 
 struct Person {
   std::string famid, pid, fatid, motid;

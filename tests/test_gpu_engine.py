@@ -399,6 +399,27 @@ def test_cli_pipelined_engines_reproduce_golden(built, tmp_path, engines, batch)
         assert got == _golden_body(golden), golden
 
 
+@pytest.mark.parametrize("case", ["quad_chrX", "late_chrX"])
+@pytest.mark.parametrize("denovo", [False, True])
+def test_cli_engines_chrX_posterior_carry(built, tmp_path, case, denovo):
+    """chrX sections over many small batches with several engines: famlk[0]'s stale posterior state passes from one
+    engine's batch to the next (EngineEvaluator::note / set_posterior_carry; plain runs take chrX batches one at a
+    time), and under --denovo -- where the posterior ignores the carry (d_member_sex_before) and batches stay
+    concurrent (in_flight) -- the records equal one engine's, byte for byte."""
+    from test_cpu_host import _sharded_case, vcf_body
+    cwd, args = _sharded_case(tmp_path, case)
+    if denovo:
+        args = args + ["--denovo"]
+    bodies = []
+    for engines in (1, 3):
+        out = str(tmp_path / f"e{engines}.vcf")
+        r = subprocess.run([pm.BIN_PATH] + args + ["--out_vcf", out, "--engines", str(engines), "--batch", "64"], cwd=cwd,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        bodies.append(vcf_body(out))
+    assert bodies[0] == bodies[1] and len(bodies[0]) > 1
+
+
 def test_engine_submit_collect_matches_run(built):
     """pm_engine_submit / pm_engine_collect with two engines' batches in flight at once give the same bytes as
     pm_engine_run, batch by batch (the CLI's pipelined engine stage)."""
