@@ -369,7 +369,9 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
     const int2* pref = gen ? generic : dn_lean ? (dn_pf ? lean_dn_pf : lean_dn) : lean;
     // extended families are the expensive terms: spread them one per lane up to 256 lanes
     // (polynomial form: up to PM_EPE families per lane, their coefficients in registers, one wave per item)
-    const int per_lane = (par->numerics == PM_NUM_POLY && !par->denovo) ? PM_EPE : 1;   // (10-state hoisting: one per lane)
+    // (--denovo too: the 10-state peels are hoisted by the schedule compiler's es_hoist_wave, and k_brent only
+    // evaluates their coefficients; the reference-order 10-state peel of PRODUCT / EXACT numerics keeps one per lane)
+    const int per_lane = (par->numerics == PM_NUM_POLY && !getenv("PM_EP_DN_ONE")) ? PM_EPE : 1;
     int tmin = 1;
     while (tmin < std::min((E->n_ext + per_lane - 1) / per_lane, 256)) tmin *= 2;
     const int npref = gen ? 9 : 8;
