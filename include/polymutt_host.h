@@ -37,8 +37,10 @@ void pmh_glf_close(pmh_glf_reader *r);
  * world > 1: this process is shard `rank` of a multi-GPU run (one process per GPU, launched by
  * polymutt_amd/launch.py): it analyses a contiguous position range of every section and calls
  * allgather(ctx, send, n, recv) -- recv receives world x n int64, rank-major -- once per section and
- * once at the end; rank 0 prints the summed summaries and writes the merged VCF.  device >= 0 overrides
- * --gpu.  allgather returns 0 on success. */
+ * once at the end; rank 0 prints the summed summaries and writes the merged VCF.  world == 1 with a non-null
+ * allgather runs the same sharded protocol over one rank (the exchange on the device's collective, e.g. RCCL at
+ * world 1); world == 1 with a null allgather is the plain one-process CLI.  device >= 0 overrides --gpu.  allgather
+ * returns 0 on success. */
 typedef int (*pmh_allgather_fn)(void *ctx, const int64_t *send, int32_t n, int64_t *recv);
 int pmh_run_polymutt(int argc, char **argv, int32_t rank, int32_t world, int32_t device, pmh_allgather_fn allgather,
                      void *ctx);

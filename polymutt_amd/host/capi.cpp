@@ -98,7 +98,7 @@ int pmh_run_polymutt(int argc, char** argv, int32_t rank, int32_t world, int32_t
   pmhost::ShardComm comm;
   comm.rank = rank;
   comm.world = world;
-  if (world > 1) {
+  if (world > 1 || (world == 1 && allgather)) {   // (world 1 + allgather: the sharded protocol over one rank)
     if (!allgather || rank < 0 || rank >= world) { fprintf(stderr, "pmh_run_polymutt: invalid shard arguments\n"); return 1; }
     comm.allgather = [=](const int64_t* send, int n, int64_t* recv) {
       if (allgather(ctx, send, n, recv) != 0) throw pmhost::FatalError("shard exchange (allgather) failed\n");
@@ -107,7 +107,7 @@ int pmh_run_polymutt(int argc, char** argv, int32_t rank, int32_t world, int32_t
   return pmhost::polymutt_main(argc, argv, &comm, [&](const pm_pedigree& v, const pm_params& par, const pmhost::Options& opt) {
     // (several engines only where batches are pipelined: one process, GLF or block input, no --pos; a shard, --pos or
     // --in_vcf run uses one -- run_polymutt_vcf evaluates on the first engine only)
-    const int engines = (world > 1 || opt.force_call || !opt.vcfInFile.empty() || getenv("PM_SERIAL")) ? 1 : opt.engines;
+    const int engines = (world > 1 || allgather || opt.force_call || !opt.vcfInFile.empty() || getenv("PM_SERIAL")) ? 1 : opt.engines;
     return std::unique_ptr<pmhost::SiteEvaluator>(
         new pmhost::EngineEvaluator(v, par, device >= 0 ? device : opt.device, opt.batch, engines));
   });

@@ -442,7 +442,7 @@ int run_polymutt_sharded(const Options& opt, const Pedigree& ped, SiteEvaluator&
 }
 
 int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, const ShardComm* comm) {
-  const bool sharded = comm && comm->world > 1;
+  const bool sharded = comm && (comm->world > 1 || comm->allgather);   // (world 1 with an exchange: the shard protocol)
   if (!sharded || comm->rank == 0) print_status(opt);
   if (opt.vcfInFile == opt.vcfOutFile) throw FatalError("Input and output VCF files are the same!\n");
   if (opt.pedFile.empty()) throw FatalError("pedFile not provided for input!\n");

@@ -179,7 +179,7 @@ int64_t d2bits(double d) { int64_t v; memcpy(&v, &d, 8); return v; }
 int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, const ShardComm* comm) {
   if (opt.vcfInFile == opt.vcfOutFile) throw FatalError("Input and output VCF files are the same!\n");
   if (opt.vcfOutFile.empty()) throw FatalError("vcfOutFile not provided for output!\n");
-  const bool sharded = comm && comm->world > 1;
+  const bool sharded = comm && (comm->world > 1 || comm->allgather);
   const int R = sharded ? comm->rank : 0, N = sharded ? comm->world : 1;
   LineReader in;
   if (!in.open(opt.vcfInFile)) throw FatalError("Cannot open VCF file " + opt.vcfInFile + "\n");

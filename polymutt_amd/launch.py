@@ -13,6 +13,10 @@ header; the result is byte-identical to a one-process run (tests/test_cpu_host.p
 
 Collective backend: RCCL ("nccl") when every local rank has its own GPU, else gloo (CPU tests, or several
 ranks sharing one GPU).  --lib selects another build of pmh_run_polymutt (the CPU tests pass the oracle one).
+
+PM_COLLECTIVE=nccl|gloo forces the backend, and at WORLD_SIZE 1 (still under torchrun) runs the sharded protocol
+over one rank -- the per-section all-gather then runs on the one GPU's RCCL communicator, so the exchange path of a
+multi-GPU run is exercised on a one-GPU box (tests/test_gpu_engine.py::test_cli_rccl_exchange_world_one).
 """
 import ctypes as C
 import os
@@ -36,17 +40,27 @@ def run(argv, lib_path=None):
     lib.pmh_run_polymutt.argtypes = [C.c_int, C.POINTER(C.c_char_p), C.c_int32, C.c_int32, C.c_int32, _FN, C.c_void_p]
     args = ["polymutt"] + list(argv)
     cargv = (C.c_char_p * len(args))(*[a.encode() for a in args])
-    if world <= 1:
+    forced = os.environ.get("PM_COLLECTIVE", "")
+    if forced not in ("", "nccl", "gloo"):
+        print(f"PM_COLLECTIVE={forced}: expected nccl or gloo", file=sys.stderr)
+        return 2
+    if world <= 1 and not forced:
         return lib.pmh_run_polymutt(len(args), cargv, 0, 1, -1, _FN(0), None)
 
     ngpu = torch.cuda.device_count()   # counts devices without initialising HIP in this process
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
-    use_rccl = lib_path is None and ngpu >= local_world
+    use_rccl = (forced == "nccl") if forced else (lib_path is None and ngpu >= local_world)
+    if use_rccl and ngpu == 0:
+        print("PM_COLLECTIVE=nccl needs a GPU", file=sys.stderr)
+        return 2
     device = local % ngpu if ngpu > 0 else -1
     if use_rccl:
         torch.cuda.set_device(device)
     dist.init_process_group("nccl" if use_rccl else "gloo")
     dev = torch.device("cuda", device) if use_rccl else torch.device("cpu")
+
+    if rank == 0 and forced:
+        print(f"polymutt_amd.launch: collective backend {dist.get_backend()}, world {world}", file=sys.stderr)
 
     def allgather(_ctx, send, n, recv):
         try:

@@ -10,7 +10,7 @@ extern "C" int pmh_run_polymutt(int argc, char** argv, int32_t rank, int32_t wor
   pmhost::ShardComm comm;
   comm.rank = rank;
   comm.world = world;
-  if (world > 1)
+  if (world > 1 || allgather)
     comm.allgather = [=](const int64_t* send, int n, int64_t* recv) {
       if (allgather(ctx, send, n, recv) != 0) throw pmhost::FatalError("shard exchange (allgather) failed\n");
     };

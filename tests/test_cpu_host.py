@@ -288,6 +288,24 @@ def test_sharded_driver_matches_one_process_gloo(cpu_driver, tmp_path, case, wor
     assert ("first record re-run" in r2.stderr) == (case == "late_chrX"), r2.stderr[-2000:]
 
 
+@pytest.mark.parametrize("case", ["example", "late_chrX"])
+def test_sharded_protocol_world_one_gloo(cpu_driver, tmp_path, monkeypatch, case):
+    """PM_COLLECTIVE=gloo at world 1: the sharded protocol (part file, per-section all-gather, merge) over one rank
+    writes the same VCF and summaries as the plain one-process run (the CPU twin of the RCCL world-1 GPU test)."""
+    cwd, args = _sharded_case(tmp_path, case)
+    one = str(tmp_path / "one.vcf")
+    r1 = subprocess.run([cpu_driver] + args + ["--out_vcf", one], cwd=cwd, capture_output=True, text=True, timeout=600)
+    assert r1.returncode == 0, r1.stdout[-2000:]
+    sh = str(tmp_path / "w1.vcf")
+    lib = os.path.join(ROOT, "tests", "native", "build", "libpm_cpu_driver.so")
+    monkeypatch.setenv("PM_COLLECTIVE", "gloo")
+    r2 = run_sharded(cwd, args + ["--out_vcf", sh], 1, lib=lib)
+    assert r2.returncode == 0, r2.stdout[-3000:] + r2.stderr[-3000:]
+    assert "collective backend gloo, world 1" in r2.stderr
+    assert vcf_body(sh) == vcf_body(one)
+    assert summary_lines(r2.stdout) == summary_lines(r1.stdout) and summary_lines(r1.stdout)
+
+
 @pytest.mark.parametrize("case,world", [("golden", 2), ("golden", 3), ("edits", 2), ("nodata", 2), ("nodata", 3),
                                         ("empty_rank", 3)])
 def test_sharded_vcf_input_matches_one_process_gloo(cpu_driver, tmp_path, case, world):

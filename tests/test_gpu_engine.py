@@ -285,6 +285,25 @@ def test_cli_two_shards_match_one_process(built, tmp_path, case):
     assert ("first record re-run" in r2.stderr) == (case == "late_chrX")
 
 
+@pytest.mark.parametrize("case", ["example", "quad_chrX"])
+def test_cli_rccl_exchange_world_one(built, tmp_path, monkeypatch, case):
+    """The CLI's section exchange (launch.py: the all-gather that replaces src/main.cpp:264-282's summary counters
+    and orders the VCF merge) forced onto RCCL at world 1 (PM_COLLECTIVE=nccl): the sharded protocol runs over one
+    rank with the all-gather on the GPU, and the VCF and section summaries equal the plain one-process CLI's."""
+    from test_cpu_host import _sharded_case, run_sharded, summary_lines, vcf_body
+    cwd, args = _sharded_case(tmp_path, case)
+    one = str(tmp_path / "one.vcf")
+    r1 = subprocess.run([pm.BIN_PATH] + args + ["--out_vcf", one], cwd=cwd, capture_output=True, text=True, timeout=300)
+    assert r1.returncode == 0, r1.stdout[-2000:]
+    sh = str(tmp_path / "rccl.vcf")
+    monkeypatch.setenv("PM_COLLECTIVE", "nccl")
+    r2 = run_sharded(cwd, args + ["--out_vcf", sh], 1)
+    assert r2.returncode == 0, r2.stdout[-3000:] + r2.stderr[-3000:]
+    assert "collective backend nccl, world 1" in r2.stderr, r2.stderr[-2000:]
+    assert vcf_body(sh) == vcf_body(one)
+    assert summary_lines(r2.stdout) == summary_lines(r1.stdout) and summary_lines(r1.stdout)
+
+
 def test_posterior_carry_matches_oracle(built, tmp_path):
     """famlk[0]'s stale posterior state (pm_engine_set_posterior_carry) set explicitly, as a shard start does:
     the engine's chrX genotype posteriors follow the oracle's for both states, and the state is visible in
