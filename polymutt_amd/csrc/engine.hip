@@ -844,8 +844,9 @@ static const pmjit::Kernel* jit_kernel(pm_engine* E) {
     const int dmode = !E->par.denovo ? 0 : (!E->vcf && !getenv("PM_ES_NOGROUP")) ? 2 : 1;
     if (!fams.empty() && pmjit::build(E->device, cls, fams, kTBA, dmode, &K, &err)) {
       const size_t ns = K.slot_e.size();
-      std::vector<int> tab(3 * ns);
+      std::vector<int> tab(3 * ns + K.pair_k.size());   // slot_e | slot_sig | slot_p0 | pair_k (pair mode)
       for (size_t i = 0; i < ns; i++) { tab[i] = K.slot_e[i]; tab[ns + i] = K.slot_sig[i]; tab[2 * ns + i] = K.slot_p0[i]; }
+      std::copy(K.pair_k.begin(), K.pair_k.end(), tab.begin() + 3 * ns);
       if (dalloc(&E->d_jit_slots[plan][cls], tab.size()) == PM_OK &&
           hipMemcpy(E->d_jit_slots[plan][cls], tab.data(), sizeof(int) * tab.size(), hipMemcpyHostToDevice) == hipSuccess)
         st = 1;
@@ -977,6 +978,7 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
         pmjit::Args J;
         J.items = A.items[list]; J.counts = A.counts; J.ref = A.ref; J.res = (const int*)A.res; J.pl = A.pl; J.lktab = A.lktab;
         J.coef = A.es_coef; J.slot_e = tab; J.slot_sig = tab + ns; J.slot_p0 = tab + 2 * ns;
+        J.pair_k = tab + 3 * ns; J.npairs = (int)K->pair_k.size() / 2;
         J.T10 = E->d_T10; J.T10dn = E->d_T10dn; J.tba = E->d_tba;
         J.list = list; J.it0 = A.es_it0; J.it1 = A.es_it1; J.nslots = ns; J.np = A.n_person; J.T = A.T; J.max_ext = A.max_ext;
         J.dcap = A.poly_dcap; J.vcf = A.vcf; J.res_words = sizeof(pm_site_result) / 4;

@@ -193,8 +193,8 @@ typedef unsigned char uint8_t;
 struct Args {
   const int* items; const int* counts; const uint8_t* ref; const int* res; const uint8_t* pl; const double* lktab;
   double* coef; const int* slot_e; const int* slot_sig; const int* slot_p0;
-  const double* T10; const double* T10dn; const double* tba; unsigned long long* prof;
-  int list, it0, it1, nslots, np, T, max_ext, dcap, vcf, res_words, res_a1, res_a2, denovo, group;
+  const double* T10; const double* T10dn; const double* tba; unsigned long long* prof; const int* pair_k;
+  int list, it0, it1, nslots, np, T, max_ext, dcap, vcf, res_words, res_a1, res_a2, denovo, group, npairs;
 };
 __device__ __forceinline__ int gi(int b1, int b2) {
   return b1 < b2 ? (b1 - 1) * (10 - b1) / 2 + (b2 - b1) : (b2 - 1) * (10 - b2) / 2 + (b1 - b2);
@@ -455,6 +455,12 @@ bool g_pack = true;    // PM_ES_PACK=0: independent type-2 steps one phase each
 int g_regp = 2;
 bool g_regf = true;    // PM_ES_REGF=0: pristine founders stored and read from LDS (with PM_ES_REGP != 0)
 int g_expt = 0;        // PM_ES_EXPT=1/2: timing experiments only (results wrong), see the uses
+// Family pairs (PM_ES_PAIR, default on): each half-wave (32 lanes) hoists one family of a pair of same-shape families
+// of the task, so every phase whose elements fit 32 lanes (type-2 steps over 10 states, founder-sparse type-1 runs
+// over 30 pairs, the final sum) does two families' work per instruction; g_wl = the lanes per family (64 or 32).
+// Pair mode reads partials across lanes through LDS only (no v_readlane from fixed lanes: PM_ES_REGP / REGF off).
+bool g_pair = false;
+int g_wl = 64;
 
 struct WaveGen {
   std::string code;
@@ -630,15 +636,15 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
   const int TB = off, NSZ = off + tmp - LSZ;
   *ws_doubles = part == 1 ? LSZ : LSZ + M * NSZ;   // (the leaf prefix writes its own regions only)
   auto S = [](long v) { return std::to_string(v); };
-  const std::string nsS = S(NS), nsq = S(NS * NS), R = S((NS * NS + 63) / 64);
+  const std::string nsS = S(NS), nsq = S(NS * NS), R = S((NS * NS + g_wl - 1) / g_wl), WL = S(g_wl);
   const bool mc = part == 2 && M > 1;   // offsets of the item's own regions carry cb (several items per call)
   auto PO = [&](int i) { return mc && !leafp[i] ? "(" + S(po[i]) + " + cb)" : S(po[i]); };
   auto MOf = [&](int s) { return mc && !leafs.count(s) ? "(" + S(mo[s]) + " + cb)" : S(mo[s]); };
   const std::string TBs = mc ? "(" + S(TB) + " + cb)" : S(TB);
   // a phase with lanes over (item c, index var < N); part 2: c's genotypes (packed 8 bits per item) and offset cb
   auto lanes = [&](int N, const std::string& var, const std::string& body) -> std::string {
-    if (!mc) return "  for (int " + var + " = lane; " + var + " < " + S(N) + "; " + var + " += 64) {\n" + body + "  }\n";
-    return "  for (int x_ = lane; x_ < " + S(M * N) + "; x_ += 64) {\n    const int c = x_ / " + S(N) + ", " + var + " = x_ - c * " +
+    if (!mc) return "  for (int " + var + " = lane; " + var + " < " + S(N) + "; " + var + " += " + WL + ") {\n" + body + "  }\n";
+    return "  for (int x_ = lane; x_ < " + S(M * N) + "; x_ += " + WL + ") {\n    const int c = x_ / " + S(N) + ", " + var + " = x_ - c * " +
            S(N) + ", cb = c * " + S(NSZ) + ";\n    const int g11 = (gg11 >> (8 * c)) & 255, g12 = (gg12 >> (8 * c)) & 255, "
            "g22 = (gg22 >> (8 * c)) & 255;\n    (void)g11; (void)g12; (void)g22; (void)cb;\n" + body + "  }\n";
   };
@@ -807,7 +813,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
           nops -= (1.0 - fr) * 100.0 * ((g.a + 1) * 10.0 + (create ? 0 : (g.a + 1) * (g.b + 1)));
           for (int k2 : run) frac1[k2] = fr;
         }
-        const int npair = sparse ? 1 : 2;
+        const int npair = sparse ? 1 : (100 + g_wl - 1) / g_wl;
         std::string c1 = "  {\n";
         if (sparse) {
           const std::string gq[3] = {"g11", "g12", "g22"};
@@ -815,7 +821,9 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
           for (int q = (int)sp_terms.size() - 2; q >= 0; q--) sF = "qi_ == " + S(q) + " ? " + gq[sp_terms[q].first] + " : " + sF;
           c1 += "    const int qi_ = lane / 10, o_ = lane - qi_ * 10, sF_ = " + sF + ";\n    const int e = " +
                 (sp_father ? "sF_ * 10 + o_" : "o_ * 10 + sF_") + ";\n    if (lane < " + S(10 * sp_terms.size()) + ") {\n";
-        } else c1 += "    const int e1 = lane + 64, e1c = e1 < 100 ? e1 : lane;\n";
+        } else
+          for (int pr = 1; pr < npair; pr++)
+            c1 += "    const int e" + S(pr) + " = lane + " + S(pr * g_wl) + ", e" + S(pr) + "c = e" + S(pr) + " < 100 ? e" + S(pr) + " : lane;\n";
         for (size_t q = 0; q < run.size(); q++) {
           const int ga = sd[run[q]].a;
           for (int pr = 0; pr < npair; pr++) {
@@ -827,7 +835,11 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
         // spills)
         c1 += "#pragma unroll 2\n    for (int k = 0; k < 10; k++) {\n";
         if (sparse) c1 += "      const double t0 = t10dn[e * 10 + k];\n";
-        else
+        else if (npair > 2) {   // (pair mode: the rows of this lane's four pairs)
+          c1 += "      const double t0 = t10dn[lane * 10 + k]";
+          for (int pr = 1; pr < npair; pr++) c1 += ", t" + S(pr) + " = t10dn[e" + S(pr) + "c * 10 + k]";
+          c1 += ";\n";
+        } else
           c1 += g_expt == 1 ? "      const double t0 = 0.001 * k, t1 = 0.002 * k;\n"   // (timing experiment only: wrong values)
                 : g_tr_regs ? "      const double t0 = tr0[k], t1 = tr1[k];\n"
                             : "      const double t0 = t10dn[lane * 10 + k], t1 = t10dn[e1c * 10 + k];\n";
@@ -850,8 +862,8 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
         c1 += "    }\n";
         // per pair: each marriage partial chained through its steps in registers, one write
         for (int pr = 0; pr < npair; pr++) {
-          const std::string sp = "s" + S(pr) + "_", e = spi.compact ? "lane" : sparse ? "e" : pr ? "e1" : "lane";
-          c1 += pr ? "    if (e1 < 100) {\n" : "    {\n";
+          const std::string sp = "s" + S(pr) + "_", e = spi.compact ? "lane" : sparse ? "e" : pr ? "e" + S(pr) : "lane";
+          c1 += pr ? "    if (e" + S(pr) + " < 100) {\n" : "    {\n";
           int cid = 0;
           for (int sl2 : slots) {
             const std::string mev = MOf(sl2) + " + " + e + " * " + S(capM[sl2]);
@@ -889,7 +901,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
         c1 += "  }\n  wave_sync();\n";
         code += c1;
       } else
-      code += "#pragma unroll\n  for (int r = 0; r < " + R + "; r++) {\n    const int e = lane + 64 * r;\n    if (e < " + nsq + ") {\n" + items(b) +
+      code += "#pragma unroll\n  for (int r = 0; r < " + R + "; r++) {\n    const int e = lane + " + WL + " * r;\n    if (e < " + nsq + ") {\n" + items(b) +
               "    }\n  }\n  wave_sync();\n";
     } else if (type == 2) {   // lanes over i: S(i) = sum_j P_from[j] M(j, i) in registers, then P_to[i] *= S(i) in place
       const int sf = from0, stt = to0, fcap = capP[sf], tcap = capP[stt];
@@ -907,7 +919,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
                                                                : -1};
         };
         const std::vector<int> sg0 = sig2(kstep);
-        for (int k2 = kstep + 1; k2 < nst && run.size() < 4; k2++) {
+        for (int k2 = kstep + 1; k2 < nst && (int)run.size() < g_wl / 16; k2++) {
           if ((part == 1 && !leaf[k2]) || (part == 2 && leaf[k2])) continue;
           const int2 Q = F.steps[k2];
           if ((Q.x & 255) != 2 || sig2(k2) != sg0) break;
@@ -1071,7 +1083,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
                  PO(mo_) + " + j * " + S(capP[mo_]) + " + " + S(c) + "], w[" + S(u + v + c) + "]);\n";
           }
       for (int a = 0; a <= dw; a++) b += "      W[" + TBs + " + e * " + S(ww) + " + " + S(a) + "] = w[" + S(a) + "];\n";
-      code += "#pragma unroll\n  for (int r = 0; r < " + R + "; r++) {\n    const int e = lane + 64 * r;\n    if (e < " + nsq + ") {\n" + items(b) +
+      code += "#pragma unroll\n  for (int r = 0; r < " + R + "; r++) {\n    const int e = lane + " + WL + " * r;\n    if (e < " + nsq + ") {\n" + items(b) +
               "    }\n  }\n  wave_sync();\n";
       std::string b2 = "    double s[" + S(ww) + "];\n";
       for (int a = 0; a <= dw; a++) b2 += "    s[" + S(a) + "] = 0.0;\n";
@@ -1107,7 +1119,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
 std::string gen_pen_fill(int n, const std::string& name) {
   const std::string N = std::to_string(n);
   return "__device__ __forceinline__ void " + name + "(const uint8_t* __restrict__ pl, size_t np, int p0, const double* lk, double* PEN, "
-         "int lane) {\n  for (int e = lane; e < " + std::to_string(10 * n) + "; e += 64) {\n    const int g = e / " + N + ", i = e - g * " + N +
+         "int lane) {\n  for (int e = lane; e < " + std::to_string(10 * n) + "; e += " + std::to_string(g_wl) + ") {\n    const int g = e / " + N + ", i = e - g * " + N +
          ";\n    PEN[e] = lk[pl[(size_t)g * np + p0 + i]];\n  }\n  wave_sync();\n}\n";
 }
 
@@ -1115,7 +1127,7 @@ std::string gen_pen_fill(int n, const std::string& name) {
 // the top variant's rest and (pps == 4) the 10-state rest of three items at once
 std::string gen_wave_kernel(const std::vector<std::string>& fns, const std::vector<std::string>& parts, const std::vector<std::string>& pens,
                             const std::vector<int>& shape_ns, int pps, int ws, int pensz, int wpb, bool parts_only) {
-  const int npf = pensz <= 4 * 64 ? (pensz + 63) / 64 : 0;   // prefetch registers per lane (0: families too large)
+  const int npf = pensz <= 4 * g_wl ? (pensz + g_wl - 1) / g_wl : 0;   // prefetch registers per lane (0: families too large)
   std::string s = R"(
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1129,12 +1141,14 @@ __device__ __forceinline__ void wave_sync() {
   std::string k = R"(
 extern "C" __global__ void __launch_bounds__(64 * WPB) WPEU es_hoist_wave(Args A) {   // blockDim = 64 WPB
   __shared__ double lk[256], tb[6 * 27];
-  __shared__ double ws[WPB][WSIZE + PENSZ];
+  __shared__ double ws[WPB][(PAIR ? 2 : 1) * (WSIZE + PENSZ)];
   for (int i = threadIdx.x; i < 256; i += blockDim.x) lk[i] = A.lktab[i];
   for (int i = threadIdx.x; i < 6 * 27; i += blockDim.x) tb[i] = i < 5 * 27 ? A.tba[i] : 1.0;
   __syncthreads();
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  double* W = ws[wave];
+  // PAIR: half-wave h = lane >> 5 hoists the pair's family h in its own slice; `lane` is the lane within the half
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & (PAIR ? 31 : 63);
+  const int half = PAIR ? (threadIdx.x >> 5) & 1 : 0;
+  double* W = ws[wave] + half * (WSIZE + PENSZ);
   double* PEN = W + WSIZE;   // the current (site, family)'s penetrances
   // the de novo transmission rows of this lane's marriage-partial pairs (lane, lane + 64), for every 10-state step
   double tr0[10], tr1[10];
@@ -1153,31 +1167,35 @@ extern "C" __global__ void __launch_bounds__(64 * WPB) WPEU es_hoist_wave(Args A
   // a task: G consecutive items of the list -- with A.group, the de novo items of one site (list 0: cfgs 0-3, list 1:
   // cfgs 4-6), whose 10-state leaf steps are taken once per (site, family) -- on one family
   const int G = A.group > 1 ? A.group : 1;
-  const long long units = ((long long)(nItems - A.it0) + G - 1) / G * A.nslots;
+  const int nfu = PAIR ? A.npairs : A.nslots;   // family units per task: slots, or slot pairs
+  const long long units = ((long long)(nItems - A.it0) + G - 1) / G * nfu;
   // the next task's penetrance bytes are loaded while this one is computed (NPF per lane: 10 n <= 64 NPF)
   unsigned pb[NPF > 0 ? NPF : 1];
   long long pf_u = -1;   // the task whose bytes pb holds
   auto prefetch = [&](long long uu) {
     pf_u = -1;
     if (NPF == 0 || uu >= units) return;
-    const int uqn = (int)(uu / A.nslots), kn = (int)(uu - (long long)uqn * A.nslots);
+    const int uqn = (int)(uu / nfu), kn0 = (int)(uu - (long long)uqn * nfu);
     const int itn = A.it0 + uqn * G;
     if (itn >= nItems) return;
     const int sn = __builtin_amdgcn_readfirstlane(A.items[itn]) >> 3;
-    const int p0n = __builtin_amdgcn_readfirstlane(A.slot_p0[kn]);
-    const int nn = shape_n(__builtin_amdgcn_readfirstlane(A.slot_sig[kn]));
-    if (10 * nn > 64 * NPF) return;
+    const int kn = PAIR ? A.pair_k[2 * kn0 + half] : kn0, ks = PAIR ? __builtin_amdgcn_readfirstlane(A.pair_k[2 * kn0]) : kn0;
+    const int p0n = PAIR ? A.slot_p0[kn] : __builtin_amdgcn_readfirstlane(A.slot_p0[kn]);
+    const int nn = shape_n(__builtin_amdgcn_readfirstlane(A.slot_sig[ks]));
+    if (10 * nn > LPF * NPF) return;
     const uint8_t* pln = A.pl + (size_t)sn * A.np * 10 + p0n;
 #pragma unroll
     for (int r = 0; r < (NPF > 0 ? NPF : 1); r++) {
-      const int e = lane + 64 * r, g = e / nn;
+      const int e = lane + LPF * r, g = e / nn;
       pb[r] = e < 10 * nn ? pln[(size_t)g * A.np + (e - g * nn)] : 0;
     }
     pf_u = uu;
   };
   prefetch((long long)blockIdx.x * WPB + wave);
   for (long long u = (long long)blockIdx.x * WPB + wave; u < units; u += (long long)gridDim.x * WPB) {
-    const int uq = (int)(u / A.nslots), k = (int)(u - (long long)uq * A.nslots);
+    const int uq = (int)(u / nfu), k0 = (int)(u - (long long)uq * nfu);
+    // (PAIR: k is this half's slot -- per lane; ks the pair's first slot, whose shape both halves share)
+    const int k = PAIR ? A.pair_k[2 * k0 + half] : k0, ks = PAIR ? __builtin_amdgcn_readfirstlane(A.pair_k[2 * k0]) : k0;
     int leaf_site = -1, pen_site = -1;
     unsigned long long tq = PROF ? __builtin_readcyclecounter() : 0;
     for (int t = 0; t < G; t++) {
@@ -1194,8 +1212,8 @@ extern "C" __global__ void __launch_bounds__(64 * WPB) WPEU es_hoist_wave(Args A
     const uint8_t* P11 = pl + (size_t)g11 * A.np;
     const uint8_t* P12 = pl + (size_t)g12 * A.np;
     const uint8_t* P22 = pl + (size_t)g22 * A.np;
-    const int e = __builtin_amdgcn_readfirstlane(A.slot_e[k]), q = e / A.T;
-    const int sig = __builtin_amdgcn_readfirstlane(A.slot_sig[k]), p0 = __builtin_amdgcn_readfirstlane(A.slot_p0[k]);
+    const int e = PAIR ? A.slot_e[k] : __builtin_amdgcn_readfirstlane(A.slot_e[k]), q = e / A.T;
+    const int sig = __builtin_amdgcn_readfirstlane(A.slot_sig[ks]), p0 = PAIR ? A.slot_p0[k] : __builtin_amdgcn_readfirstlane(A.slot_p0[k]);
     double* out = A.coef + ((size_t)(it - A.it0) * A.max_ext + q) * A.dcap * A.T + (e - q * A.T);
     const int dn = A.denovo && cfg != 7, top = dn && cfg == 0 && !A.vcf;   // variant: 0 bi-allelic, 1 10-state, 2 top
     if (site != pen_site) {
@@ -1203,7 +1221,7 @@ extern "C" __global__ void __launch_bounds__(64 * WPB) WPEU es_hoist_wave(Args A
         const int nn = shape_n(sig);
 #pragma unroll
         for (int r = 0; r < (NPF > 0 ? NPF : 1); r++)
-          if (lane + 64 * r < 10 * nn) PEN[lane + 64 * r] = lk[pb[r]];
+          if (lane + LPF * r < 10 * nn) PEN[lane + LPF * r] = lk[pb[r]];
         wave_sync();
         prefetch(u + (long long)gridDim.x * WPB);
       } else {
@@ -1251,8 +1269,10 @@ PARTS2      }
     switch (sig * 3 + (top ? 2 : dn ? 1 : 0)) {
 )";
   for (size_t at; (at = k.find("WSIZE")) != std::string::npos;) k.replace(at, 5, std::to_string(ws));
-  k.replace(k.find("PENSZ"), 5, std::to_string(pensz));
+  for (size_t at; (at = k.find("PENSZ")) != std::string::npos;) k.replace(at, 5, std::to_string(pensz));
   for (size_t at; (at = k.find("NPF")) != std::string::npos;) k.replace(at, 3, std::to_string(npf));
+  for (size_t at; (at = k.find("LPF")) != std::string::npos;) k.replace(at, 3, std::to_string(g_wl));
+  for (size_t at; (at = k.find("PAIR")) != std::string::npos;) k.replace(at, 4, g_pair ? "true" : "false");
   {
     std::string cases;
     for (size_t i = 0; i < pens.size(); i++) cases += "        case " + std::to_string(i) + ": " + pens[i] + "(pl, A.np, p0, lk, PEN, lane); break;\n";
@@ -1344,6 +1364,10 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
   g_regf = !(erf && erf[0] == '0');
   const char* eex = getenv("PM_ES_EXPT");
   g_expt = eex ? atoi(eex) : 0;
+  const char* epr = getenv("PM_ES_PAIR");
+  g_pair = denovo != 0 && !(epr && epr[0] == '0') && pps == 3;
+  g_wl = g_pair ? 32 : 64;
+  if (g_pair) { g_regp = 0; g_regf = false; g_tr_regs = false; }   // (cross-lane reads by LDS only in pair mode)
   int ws = 1;
   std::vector<std::pair<int, int>> order;   // (shape, index into fams)
   for (size_t i = 0; i < fams.size(); i++) {
@@ -1388,11 +1412,20 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
     order.push_back({id, (int)i});
   }
   std::stable_sort(order.begin(), order.end(), [](const std::pair<int, int>& a, const std::pair<int, int>& b) { return a.first < b.first; });
-  out->slot_e.clear(); out->slot_sig.clear(); out->slot_p0.clear();
+  out->slot_e.clear(); out->slot_sig.clear(); out->slot_p0.clear(); out->pair_k.clear();
   for (auto& o : order) {
     out->slot_e.push_back(fams[o.second].e);
     out->slot_sig.push_back(o.first);
     out->slot_p0.push_back(fams[o.second].p0);
+  }
+  // PAIR: consecutive slots of one shape form a pair; an odd one out is paired with itself (both halves compute the
+  // same family and store the same values to the same coefficients)
+  out->pair = g_pair;
+  for (size_t i = 0; g_pair && i < out->slot_sig.size();) {
+    const bool two = i + 1 < out->slot_sig.size() && out->slot_sig[i + 1] == out->slot_sig[i];
+    out->pair_k.push_back((int)i);
+    out->pair_k.push_back((int)(two ? i + 1 : i));
+    i += two ? 2 : 1;
   }
   out->n_shapes = (int)names.size();
   std::string src = kPrologue;
@@ -1407,8 +1440,9 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
     // waves per block: as many workspace slices as fit the 64 KB of static LDS next to the tables
     const int tables = (256 + 6 * 27) * 8;
     // (one wave per SIMD: the occupancy comes from blocks per CU, build() asks the runtime for them)
-    out->wpb = std::max(1, std::min(4, (64 * 1024 - tables) / ((ws + pensz) * 8)));
-    if ((64 * 1024 - tables) / ((ws + pensz) * 8) < 1) out->wpb = 0;   // a family too large for one slice: the engine's generic kernel
+    const int slice = (g_pair ? 2 : 1) * (ws + pensz) * 8;   // (a pair's two family slices per wave)
+    out->wpb = std::max(1, std::min(4, (64 * 1024 - tables) / slice));
+    if ((64 * 1024 - tables) / slice < 1) out->wpb = 0;   // a family too large for one slice: the engine's generic kernel
     std::string wk = gen_wave_kernel(wave_names, part_names, pen_names, shape_ns, pps, ws, pensz, std::max(1, out->wpb), denovo == 2);
     const size_t at = wk.find("extern \"C\"");   // device helpers first, then the family functions, then the kernel
     src += wk.substr(0, at);

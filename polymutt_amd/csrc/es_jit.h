@@ -39,8 +39,10 @@ struct Args {
   const double* T10dn;       // transmission_denovo
   const double* tba;         // transmission_BA tables [5][27]
   unsigned long long* prof;  // [5] PM_ES_PROF clock cycles (es_hoist_wave)
+  const int* pair_k;         // [2 npairs] es_hoist_wave pair mode: the two slots of family pair j (Kernel::pair_k)
   int list, it0, it1, nslots, np, T, max_ext, dcap, vcf, res_words, res_a1, res_a2, denovo,
-      group;                 // es_hoist_wave: items per task (the de novo items of one site share the leaf steps), 0/1 none
+      group,                 // es_hoist_wave: items per task (the de novo items of one site share the leaf steps), 0/1 none
+      npairs;
 };
 
 // Arguments of the generated posterior kernel es_post_jit (CalcPostProb_SingleExtendedPed_BA for every emitted row
@@ -72,6 +74,8 @@ struct Kernel {
   std::vector<double> shape_ops[6];
   int wpb = 0, ws = 0;       // waves per block, workspace doubles per wave
   int blocks_per_cu = 0;     // es_hoist_wave blocks resident per CU (the runtime's occupancy; 0 unknown)
+  bool pair = false;         // es_hoist_wave hoists two same-shape families per wave, one per half-wave (PM_ES_PAIR)
+  std::vector<int> pair_k;   // [2 npairs] slot indices of each pair (an unpaired slot: twice)
 };
 
 // Packs family f's ES_Peeling schedule (pm_pedigree.steps) with its marriage-partial slots resolved the way the
