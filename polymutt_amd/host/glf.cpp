@@ -70,6 +70,19 @@ bool GlfFile::nextSection() {
 // glfHandler::NextEntry (:206-261)
 bool GlfFile::nextEntry() {
   uint8_t b0;
+  if (!endOfSection && len_ - pos_ >= 20 && (buf_[pos_] >> 4) == 1) {   // a whole record in the buffer: parse in place
+    const uint8_t* r = (const uint8_t*)buf_.data() + pos_;
+    uint32_t off, dm;
+    memcpy(&off, r + 1, 4); memcpy(&dm, r + 5, 4);
+    refBase = kTranslateBase[r[0] & 0xF];
+    recordType = 1;
+    depth = dm & 0xFFFFFF;
+    mapQuality = r[9];
+    memcpy(lk, r + 10, 10);
+    position += (int)off;
+    pos_ += 20;
+    return true;
+  }
   if (endOfSection || read(&b0, 1) != 1) {
     endOfSection = true; recordType = 0; position = maxPosition + 1;
     return false;

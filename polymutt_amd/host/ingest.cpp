@@ -1,6 +1,9 @@
 // ingest.cpp -- see ingest.h.
 #include "ingest.h"
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 namespace pmhost {
@@ -57,7 +60,13 @@ void TaskPool::run(int n, const std::function<void(int)>& fn) {
 }
 
 // ---------------------------------------------------------------------------------------------
-ParallelSiteSource::~ParallelSiteSource() { delete pool_; }
+static double ing_now() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+
+ParallelSiteSource::~ParallelSiteSource() {
+  if (getenv("PM_TIMING"))
+    fprintf(stderr, "PM_TIMING glf ingest: decode %.3f s, merge %.3f s, fill %.3f s\n", t_decode_, t_merge_, t_fill_);
+  delete pool_;
+}
 
 void ParallelSiteSource::open(const Pedigree& ped, const std::string& glfIndexFile, int threads, int window) {
   auto index = read_glf_index(glfIndexFile);
@@ -101,6 +110,7 @@ void ParallelSiteSource::open(const Pedigree& ped, const std::string& glfIndexFi
     if (has_[j]) active_.push_back(j);
   headAtStart_.assign(n, -1);
   lastPos_.assign(window_, 0);
+  fast_ = !getenv("PM_SERIAL_MERGE");
   virtual_.pos = 0;
   virtual_.rt = 0xFF;   // never inspected: the first call of a section skips the end check (currentPos == 0)
 }
@@ -146,11 +156,12 @@ void ParallelSiteSource::refill(int j, int need) {
   Queue& Q = qs_[j];
   if (Q.head > 0) {   // drop consumed states
     std::memmove(Q.q.data(), Q.q.data() + Q.head, (size_t)(Q.tail - Q.head) * sizeof(GlfState));
+    std::memmove(Q.qp.data(), Q.qp.data() + Q.head, (size_t)(Q.tail - Q.head) * sizeof(int32_t));
     Q.tail -= Q.head;
     Q.head = 0;
   }
   const int target = std::max(Q.head, 0) + need;
-  if ((int)Q.q.size() < target) Q.q.resize(target);
+  if ((int)Q.q.size() < target) { Q.q.resize(target); Q.qp.resize(target); }
   GlfFile& g = files_[j];
   while (Q.tail < target && !Q.terminal) {   // glfHandler::NextBaseEntry, :195-204
     g.nextBaseEntry();
@@ -160,6 +171,7 @@ void ParallelSiteSource::refill(int j, int need) {
     std::memcpy(s.lk, g.lk, 10);
     s.ref = g.refBase;
     s.rt = g.recordType;
+    Q.qp[Q.tail - 1] = g.recordType == 0 ? INT32_MIN : g.position;   // (fastMerge's compact view)
     if (g.recordType == 0) Q.terminal = true;
   }
 }
@@ -169,13 +181,24 @@ int ParallelSiteSource::nextSites(int maxSites, int* pos, uint8_t* ref) {
   if (ended_ || maxSites <= 0) return 0;
   maxSites = std::min(maxSites, window_);
   // a call advances a person at most once: maxSites + 1 states from the head cover the whole window
+  const double t0 = ing_now();
   forChunks([&](int j) { refill(j, maxSites + 1); });
+  const double t1 = ing_now();
+  t_decode_ += t1 - t0;
   prevPos_ = currentPos_;
   for (int j : active_) headAtStart_[j] = qs_[j].head;
   const int maxPos = files_[nonNull_].maxPosition;
   const int na = (int)active_.size();
   int s = 0;
   for (; s < maxSites; s++) {   // PedigreeGLF::Move2NextBaseEntry, :282-324, one fused pass per call
+    if (fast_ && s < maxSites) {   // a run of calls merged in parallel where that is provably the same (fastMerge)
+      const int got = fastMerge(maxSites - s, maxPos, pos + s, ref + s);
+      if (got > 0) {
+        for (int t = 0; t < got; t++) lastPos_[s + t] = pos[s + t];
+        s += got - 1;
+        continue;
+      }
+    }
     const int cp = currentPos_;
     int mn = 0;
     uint8_t rf = 0;
@@ -201,10 +224,99 @@ int ParallelSiteSource::nextSites(int maxSites, int* pos, uint8_t* ref) {
     lastPos_[s] = mn;
   }
   nLast_ = s;
+  t_merge_ += ing_now() - t1;
   return s;
 }
 
+// A run of Move2NextBaseEntry calls merged in parallel.  From a state where every person's head is a record (not
+// the section-start placeholder, not an end-of-section record) and currentPos cp > 0, each person's upcoming heads
+// are its next queued states (after the one at cp, which this call advances past).  While those are records with
+// strictly increasing positions, the serial calls reduce to: the next currentPos is the smallest position > the
+// previous one that any person holds, its refBase that of the first person (in person order) holding it, and a
+// person's head after the run its first state past the run's second-to-last position.  lim = the least position up
+// to which every person's states are known to be such records (exclusive); positions in (cp, lim) are collected per
+// chunk of persons (first holder in the chunk), the chunks reduced in person order, and up to maxSites of them
+// emitted.  Returns the number of calls made (0: the next call needs the serial pass -- a section start or end, a
+// repeated position, a queue that ran short).  The emitted sites, refBases and heads are those of the serial pass.
+int ParallelSiteSource::fastMerge(int maxSites, int maxPos, int* pos, uint8_t* ref) {
+  const int cp = currentPos_;
+  if (cp <= 0 || maxSites <= 0) return 0;
+  const int na = (int)active_.size();
+  const int nchunk = std::min(na, 2 * pool_->threads());
+  if ((int)scratch_.size() < nchunk) scratch_.resize(nchunk);
+  if ((int)vend_.size() < na) vend_.resize(na);
+  std::vector<int> lim(nchunk, INT32_MAX);
+  std::vector<char> bad(nchunk, 0);
+  // one pass per person: its valid upcoming prefix (records, strictly increasing positions; vend_ = where it stops),
+  // and, per chunk, the first holder (active index, state) of every position in (cp, cp + kFastRange)
+  gen_++;
+  pool_->run(nchunk, [&](int c) {
+    Scratch& S = scratch_[c];
+    if (S.stamp.empty()) { S.stamp.assign(kFastRange, 0); S.who.assign(kFastRange, 0); }
+    const int i0 = (int)((long long)na * c / nchunk), i1 = (int)((long long)na * (c + 1) / nchunk);
+    int l = INT32_MAX;
+    for (int i = i0; i < i1; i++) {
+      const Queue& Q = qs_[active_[i]];
+      if (Q.head < 0) { bad[c] = 1; return; }
+      const int32_t* qp = Q.qp.data();
+      const int hp = qp[Q.head];   // (INT32_MIN: an end-of-section record)
+      if (hp == INT32_MIN) { bad[c] = 1; return; }
+      int k = hp == cp ? Q.head + 1 : Q.head, prev = cp;
+      const int top = cp + kFastRange;
+      // (INT32_MIN fails `> prev` too; positions past the range or the chunk's running limit need no stamp)
+      for (; k < Q.tail && qp[k] > prev && qp[k] <= top && qp[k] < l; k++) {
+        const int x = qp[k] - cp - 1;
+        if (S.stamp[x] != gen_) { S.stamp[x] = gen_; S.who[x] = (int64_t)i << 32 | (uint32_t)k; }
+        prev = qp[k];
+      }
+      vend_[i] = k;
+      if (k < Q.tail && qp[k] > prev) continue;   // (stopped at the range or the running limit, not at a bad record)
+      if (prev == cp) { bad[c] = 1; return; }     // no usable upcoming record
+      l = prev;   // the last record of the valid prefix (a repeat, an end record or the queue's end follows)
+    }
+    lim[c] = l;
+  });
+  int H = INT32_MAX;
+  for (int c = 0; c < nchunk; c++) {
+    if (bad[c]) return 0;
+    H = std::min(H, lim[c]);
+  }
+  H = std::min(H, maxPos + 1);   // (a position past maxPosition ends the section: the serial pass)
+  if (H - cp - 1 > kFastRange) H = cp + 1 + kFastRange;
+  const int R = H - cp - 1;   // positions cp + 1 .. H - 1: every person's states there are stamped
+  if (R <= 0) return 0;
+  // reduce in person order (chunks ascending), emit ascending
+  int m = 0;
+  for (int x = 0; x < R && m < maxSites; x++)
+    for (int c = 0; c < nchunk; c++)
+      if (scratch_[c].stamp[x] == gen_) {
+        const int64_t w = scratch_[c].who[x];
+        const int j = active_[(int)(w >> 32)];
+        pos[m] = cp + 1 + x;
+        ref[m] = qs_[j].q[(uint32_t)w].ref;
+        m++;
+        break;
+      }
+  if (m == 0) return 0;
+  // heads: each person's first state past the second-to-last emitted position (cp when one site was emitted), found
+  // by binary search in its valid prefix (strictly increasing; the head sought lies in it, at or below H)
+  const int before = m >= 2 ? pos[m - 2] : cp;
+  pool_->run(nchunk, [&](int c) {
+    const int i0 = (int)((long long)na * c / nchunk), i1 = (int)((long long)na * (c + 1) / nchunk);
+    for (int i = i0; i < i1; i++) {
+      Queue& Q = qs_[active_[i]];
+      if (Q.qp[Q.head] > before) continue;
+      const int32_t* b = Q.qp.data() + Q.head + 1;
+      Q.head = (int)(std::upper_bound(b, (const int32_t*)Q.qp.data() + vend_[i], before) - Q.qp.data());
+    }
+  });
+  currentPos_ = pos[m - 1];
+  return m;
+}
+
 void ParallelSiteSource::fill(const int* rowOf, uint8_t* pl, uint32_t* dm) {
+  const double t0 = ing_now();
+  struct Acc { double& t; double t0; ~Acc() { t += ing_now() - t0; } } acc{t_fill_, t0};
   const size_t np = files_.size();
   const int n = nLast_;
   for (size_t j = 0; j < np; j++) {   // persons without a handle: zero columns (SiteSource::fill)
@@ -215,24 +327,33 @@ void ParallelSiteSource::fill(const int* rowOf, uint8_t* pl, uint32_t* dm) {
       dm[(size_t)rowOf[s] * np + j] = 0;
     }
   }
-  forChunks([&](int j) {   // the merge's advance rule, replayed for this person
-    int k = headAtStart_[j];
-    int prev = prevPos_;
+  // the merge's advance rule replayed per person, for a chunk of up to 64 persons at a time with the sites outer, so each
+  // site row receives the chunk's contiguous 640 PL bytes (columns of a row) rather than one 10-byte piece per row
+  const int na = (int)active_.size();
+  const int nch = (na + 63) / 64;
+  pool_->run(nch, [&](int c) {
+    const int i0 = c * 64, i1 = std::min(na, i0 + 64);
+    int k[64], prev = prevPos_;
+    for (int i = i0; i < i1; i++) k[i - i0] = headAtStart_[active_[i]];
     for (int s = 0; s < n; s++) {
-      if (state(j, k).pos == prev) k = next(j, k);
-      const GlfState& st = state(j, k);
       const int cur = lastPos_[s];
-      prev = cur;
       const int r = rowOf[s];
-      if (r < 0) continue;
-      uint8_t* P = pl + ((size_t)r * np + j) * 10;
-      if (st.pos == cur) {
-        std::memcpy(P, st.lk, 10);
-        dm[(size_t)r * np + j] = st.dm;
-      } else {
-        std::memset(P, 0, 10);
-        dm[(size_t)r * np + j] = 0;
+      for (int i = i0; i < i1; i++) {
+        const int j = active_[i];
+        int& kk = k[i - i0];
+        if (state(j, kk).pos == prev) kk = next(j, kk);
+        if (r < 0) continue;
+        const GlfState& st = state(j, kk);
+        uint8_t* P = pl + ((size_t)r * np + j) * 10;
+        if (st.pos == cur) {
+          std::memcpy(P, st.lk, 10);
+          dm[(size_t)r * np + j] = st.dm;
+        } else {
+          std::memset(P, 0, 10);
+          dm[(size_t)r * np + j] = 0;
+        }
       }
+      prev = cur;
     }
   });
 }

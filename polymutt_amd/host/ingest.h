@@ -104,6 +104,7 @@ class ParallelSiteSource : public SiteStream {
  private:
   struct Queue {
     std::vector<GlfState> q;
+    std::vector<int32_t> qp;   // q[k].pos, or INT32_MIN for an end-of-section record (fastMerge reads only this)
     int head = -1;          // -1: before the section's first call (the state at position 0)
     int tail = 0;
     bool terminal = false;  // q[tail - 1] is the end-of-section state, which repeats forever
@@ -127,6 +128,15 @@ class ParallelSiteSource : public SiteStream {
   // the last nextSites call: currentPos and queue heads before it, and the merged positions
   int prevPos_ = 0, nLast_ = 0;
   std::vector<int> headAtStart_, lastPos_;
+  double t_decode_ = 0, t_merge_ = 0, t_fill_ = 0;   // PM_TIMING: wall seconds per stage
+  // the parallel merge of a run of calls (fastMerge; PM_SERIAL_MERGE=1 turns it off)
+  int fastMerge(int maxSites, int maxPos, int* pos, uint8_t* ref);
+  static constexpr int kFastRange = 1 << 14;   // positions scanned per parallel run at most
+  struct Scratch { std::vector<uint32_t> stamp; std::vector<int64_t> who; };
+  std::vector<Scratch> scratch_;
+  std::vector<int> vend_;   // per active person: where fastMerge's scan of its valid prefix stopped
+  uint32_t gen_ = 0;
+  bool fast_ = true;
 };
 
 }  // namespace pmhost

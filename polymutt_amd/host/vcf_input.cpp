@@ -67,6 +67,52 @@ struct LineReader {   // plain or gzip text, lines of any length; offsets are in
   }
 };
 
+// Whole lines of the stream, read in large blocks (one gzread per block instead of gzgets + append per line): a chunk's
+// lines are pointers into the block, valid until the next chunk() call (which compacts and refills first).
+struct BlockReader {
+  gzFile fh;
+  std::vector<char> buf = std::vector<char>((size_t)64 << 20);
+  size_t beg = 0, end = 0;
+  int64_t base;   // uncompressed offset of buf[0]
+  bool zeof = false;
+  struct Line { const char* p; size_t n; int64_t off; };
+  explicit BlockReader(LineReader& lr) : fh(lr.fh), base(lr.tell()) {}
+  // Up to `max` whole lines ('\n' and a trailing '\r' removed); fewer when the block ends (the next call continues).
+  void chunk(int max, std::vector<Line>& out) {
+    out.clear();
+    if (beg > 0) {   // compact and refill
+      memmove(buf.data(), buf.data() + beg, end - beg);
+      base += (int64_t)beg;
+      end -= beg;
+      beg = 0;
+    }
+    for (;;) {
+      while (!zeof && end < buf.size()) {
+        const int r = gzread(fh, buf.data() + end, (unsigned)std::min<size_t>(buf.size() - end, (size_t)1 << 30));
+        if (r < 0) throw FatalError("VCF input: read error\n");
+        if (r == 0) zeof = true;
+        end += (size_t)r;
+      }
+      size_t at = beg;
+      while ((int)out.size() < max && at < end) {
+        const char* nl = (const char*)memchr(buf.data() + at, '\n', end - at);
+        if (!nl) {
+          if (!zeof) break;   // (a partial line: the next chunk, after the refill)
+          nl = buf.data() + end;
+        }
+        size_t n = (size_t)(nl - (buf.data() + at));
+        const size_t adv = n + (nl < buf.data() + end ? 1 : 0);
+        if (n && buf[at + n - 1] == '\r') n--;
+        out.push_back({buf.data() + at, n, base + (int64_t)at});
+        at += adv;
+      }
+      beg = at;
+      if (!out.empty() || zeof) return;
+      buf.resize(buf.size() * 2);   // one line longer than the block
+    }
+  }
+};
+
 struct Span { int b = 0, e = 0; };
 
 void split(const std::string& s, char sep, std::vector<Span>& out) {
@@ -123,6 +169,9 @@ struct Pending {          // one record awaiting output, in file order
   bool indel = false;
   int dp_idx = -1;        // DP's FORMAT index as it stood when the record was read: the reference writes each record at
                           // once (PedVCF.cpp:118-160), with DP looked up per record until found (:311-314)
+  // classify_pre (parallel): the record's own facts; classify_apply (serial, in file order) the FORMAT state machine
+  int bial = 0;           // 1 biallelic, 0 not
+  int dp_c = -1, gl_c = -1, pl_c = -1;   // this record's FORMAT indices of DP / GL / PL
 };
 
 struct State {            // what FamilyLikelihoodSeq_VCF holds between records (stale output, :412-521)
@@ -241,7 +290,14 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
   const double tstv = 2.0, prior_ts = tstv / (tstv + 1), prior_tv = 0.5 / (tstv + 1);
 
   const int B = std::max(1, opt.batch);
-  std::vector<uint8_t> pl((size_t)B * np * 10), ref(B);
+  // the batch's PL rows in page-locked memory where the evaluator offers it (an asynchronous, faster host-to-device copy)
+  struct HostBuf {
+    SiteEvaluator& e; uint8_t* p;
+    ~HostBuf() { e.host_free(p); }
+    uint8_t* data() const { return p; }
+  } pl{eval, (uint8_t*)eval.host_alloc((size_t)B * np * 10)};
+  if (!pl.p) throw FatalError("out of host memory\n");
+  std::vector<uint8_t> ref(B);
   std::vector<uint32_t> dm((size_t)B * np, 0);
   std::vector<pm_site_result> res(B);
   std::vector<pm_geno_call> calls((size_t)B * np);
@@ -361,24 +417,37 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
     nb = 0;
   };
 
-  // parses a record's columns and its biallelic / allele / FORMAT-index bookkeeping (:296-324); false: not output
-  std::string refS, altS;
-  auto classify = [&](Pending& r) {
+  // parses a record's columns and its biallelic / allele / FORMAT-index bookkeeping (:296-324); false: not output.
+  // classify_pre: what depends on the record alone (any order, in parallel); classify_apply: the FORMAT bookkeeping
+  // that carries from record to record, in file order
+  auto classify_pre = [&](Pending& r) {
     split(r.line, '\t', r.cols);
-    if (r.cols.size() < 9) throw FatalError("Malformed VCF record (fewer than 9 columns)\n");
+    if (r.cols.size() < 9) return false;
     const std::string& L = r.line;
-    auto fld = [&](int k) { return L.substr(r.cols[k].b, r.cols[k].e - r.cols[k].b); };
-    refS = fld(3); altS = fld(4);
-    bool biallelic = refS != altS && altS.find(',') == std::string::npos;
-    if (biallelic) {
+    const Span cr = r.cols[3], ca = r.cols[4];
+    const std::string refS = L.substr(cr.b, cr.e - cr.b), altS = L.substr(ca.b, ca.e - ca.b);
+    r.bial = refS != altS && altS.find(',') == std::string::npos;
+    if (r.bial) {
       r.indel = refS.size() > 1 || altS.size() > 1;
       r.a1 = r.indel ? 1 : allele2int(refS);
       r.a2 = r.indel ? 2 : allele2int(altS);
-      if (fs.DP_index < 0) fs.DP_index = format_index(L, r.cols[8], "DP");
+      r.dp_c = format_index(L, r.cols[8], "DP");
+      r.gl_c = format_index(L, r.cols[8], "GL");
+      r.pl_c = format_index(L, r.cols[8], "PL");
+    }
+    return true;
+  };
+  auto classify_apply = [&](Pending& r) {
+    if (r.cols.size() < 9) throw FatalError("Malformed VCF record (fewer than 9 columns)\n");
+    const std::string& L = r.line;
+    auto fld = [&](int k) { return L.substr(r.cols[k].b, r.cols[k].e - r.cols[k].b); };
+    const bool biallelic = r.bial;
+    if (biallelic) {
+      if (fs.DP_index < 0) fs.DP_index = r.dp_c;
       r.dp_idx = fs.DP_index;
       if (fs.GL_idx < 0 && fs.PL_idx < 0) {
-        fs.GL_idx = format_index(L, r.cols[8], "GL");
-        fs.PL_idx = format_index(L, r.cols[8], "PL");
+        fs.GL_idx = r.gl_c;
+        fs.PL_idx = r.pl_c;
         if (fs.GL_idx < 0 && fs.PL_idx < 0) {
           fprintf(stderr, "NO GL or PL field was found. Please check the vcf file at chr:%s and position:%d", fld(0).c_str(),
                   atoi(fld(1).c_str()));
@@ -413,7 +482,8 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
         if (line.empty() || line[0] == '#') continue;
         Pending r;
         r.line.swap(line);
-        classify(r);
+        classify_pre(r);
+        classify_apply(r);
       }
       in.seek(lo - 1);   // the first line starting at or after lo: skip the rest of the line holding byte lo - 1
       in.next(line);
@@ -481,20 +551,37 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
     withdata[k] = wd;
   };
   bool eof = false;
+  BlockReader br(in);
+  std::vector<BlockReader::Line> lines;
+  std::vector<char> keep(CH);
   while (!eof) {
-    int nc = 0;
-    while (nc < CH) {
-      if (in.tell() >= hi || !in.next(line)) { eof = true; break; }
-      if (line.empty() || line[0] == '#') continue;
-      Pending& r = chunk[nc];
+    // a chunk of lines from the block (in order), copied, split and classified in parallel, then the FORMAT
+    // bookkeeping applied in file order
+    br.chunk(CH, lines);
+    if (lines.empty()) break;
+    int nl = (int)lines.size();
+    for (int k = 0; k < nl; k++)
+      if (lines[k].off >= hi) { nl = k; eof = true; break; }   // (a shard's byte range ends before this line)
+    pool.run(nl, [&](int k) {
+      const BlockReader::Line& l = lines[k];
+      keep[k] = l.n > 0 && l.p[0] != '#';
+      if (!keep[k]) return;
+      Pending& r = chunk[k];
       r = Pending();
-      r.line.swap(line);
+      r.line.assign(l.p, l.n);
+      classify_pre(r);
+    });
+    int nc = 0;
+    for (int k = 0; k < nl; k++) {
+      if (!keep[k]) continue;
+      if (nc != k) std::swap(chunk[nc], chunk[k]);
+      Pending& r = chunk[nc];
       if (first)   // FillPenetrance on the first record (:270-282) ...
         for (size_t i = 0; i < samples.size(); i++) {
           if (col_person[i] < 0) { printf("Sample ID \"%s\" not included in the analysis!\n", samples[i].c_str()); continue; }
           n_samples_with_data++;
         }
-      kinds[nc] = classify(r);
+      kinds[nc] = classify_apply(r);
       if (first) {   // ... then VarCallFromVCF's banner (:117)
         printf("Total samples in both VCF and PED files: %d\n\n", n_samples_with_data);
         first = false;

@@ -73,8 +73,12 @@ def write_vcf(pm, d, families, records, seed):
                  "##FORMAT=<ID=PL,Number=3,Type=Integer,Description=\"Phred-scaled Genotype Likelihoods\">\n")
         fh.write("#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\t" + "\t".join(pids) + "\n")
         chunk = 2048
+        distinct = []   # the first 2048 records are generated; later ones repeat them at new positions (speed)
         for s0 in range(0, records, chunk):
             n = min(chunk, records - s0)
+            if distinct:
+                fh.write("".join(f"1\t{s0 + i + 1}\t{distinct[i % len(distinct)]}" for i in range(n)))
+                continue
             pl, dm, ref = pm.synth_block_host(ped.view, n, seed, s0)
             pl = pl.reshape(n, np_, 10)
             lines = []
@@ -86,6 +90,7 @@ def write_vcf(pm, d, families, records, seed):
                                    np.char.add(np.char.add(trip[:, 1].astype(str), ","), trip[:, 2].astype(str)))
                 lines.append(f"1\t{s0 + i + 1}\t.\t{bases[r]}\t{bases[a]}\t50\tPASS\t.\tGT:PL\t" + "\t".join(strs.tolist()))
             fh.write("\n".join(lines) + "\n")
+            distinct = [l.split("\t", 2)[2] + "\n" for l in lines]
     return np_
 
 
@@ -100,6 +105,8 @@ def main():
     ap.add_argument("--vcf-records", type=int, default=0, help="also time --in_vcf on a config-5 VCF of this many records")
     ap.add_argument("--vcf-families", type=int, default=2000)
     ap.add_argument("--keep", default=None, help="work directory to keep (default: a temporary one, removed)")
+    ap.add_argument("--glf", action="store_true", help="also time the CLI on the GLF files themselves (the reference's input)")
+    ap.add_argument("--vcf-small", type=int, default=2000, help="--in_vcf start-up run: records (subtracted for the steady rate)")
     a = ap.parse_args()
     tmp = a.keep or tempfile.mkdtemp(prefix="pm_cli_", dir=os.environ.get("TMPDIR", "/tmp"))
     os.makedirs(tmp, exist_ok=True)
@@ -134,6 +141,23 @@ def main():
                 rec.update(timing_fields(r.stderr))
                 out["runs"].append(rec)
                 print(json.dumps(rec), file=sys.stderr, flush=True)
+        if a.glf:   # the drop-in on GLF: decode, merge and fill in the ingest thread; start-up from the 64-site GLF set
+            for e in a.engines:
+                t_small = min(run_cli(base + ["-g", "test.gif", "--out_vcf", "s.vcf", "--engines", str(e)] + extra, small)[0]
+                              for _ in range(3))
+                runs = [run_cli(base + ["-g", "test.gif", "--out_vcf", "g.vcf", "--engines", str(e)] + extra, tmp) for _ in range(3)]
+                dt, r = min(runs, key=lambda x: x[0])
+                bd = body(os.path.join(tmp, "g.vcf"))
+                rec = {"input": "glf", "engines": e, "seconds": dt, "startup_seconds": t_small, "sites_per_s": a.sites / dt,
+                       "sites_per_s_past_startup": a.sites / max(1e-9, dt - t_small), "records": len(bd) - 1,
+                       "vcf_identical_to_blocks": ref_body is None or bd == ref_body}
+                rec.update(timing_fields(r.stderr))
+                m = re.search(r"PM_TIMING glf ingest: decode ([\d.]+) s, merge ([\d.]+) s, fill ([\d.]+) s", r.stderr)
+                if m:
+                    rec.update({"glf_decode_s": float(m.group(1)), "glf_merge_s": float(m.group(2)), "glf_fill_s": float(m.group(3))})
+                out.setdefault("glf_runs", []).append(rec)
+                print(json.dumps(rec), file=sys.stderr, flush=True)
+            out["glf_best"] = max(out["glf_runs"], key=lambda x: x["sites_per_s_past_startup"])
         best = max(out["runs"], key=lambda x: x["sites_per_s_past_startup"])
         out["best"] = {k: best[k] for k in ("engines", "batch", "sites_per_s", "sites_per_s_past_startup")}
         out["all_vcf_identical"] = all(x["vcf_identical_to_first"] for x in out["runs"])
@@ -144,9 +168,21 @@ def main():
             npers = write_vcf(pm, vd, a.vcf_families, a.vcf_records, 11)
             t_write = time.perf_counter() - t0
             vbytes = os.path.getsize(os.path.join(vd, "in.vcf"))
-            t_one, _ = run_cli(base + ["--in_vcf", "in.vcf", "--out_vcf", "o.vcf"], vd)
+            t_one = min(run_cli(base + ["--in_vcf", "in.vcf", "--out_vcf", "o.vcf"], vd)[0] for _ in range(3))
+            # the steady rate: a small VCF of the same samples (the first records of in.vcf) timed the same way, subtracted
+            with open(os.path.join(vd, "in.vcf")) as fi, open(os.path.join(vd, "small.vcf"), "w") as fo:
+                n = 0
+                for l in fi:
+                    if not l.startswith("#"):
+                        n += 1
+                        if n > a.vcf_small:
+                            break
+                    fo.write(l)
+            t_small = min(run_cli(base + ["--in_vcf", "small.vcf", "--out_vcf", "s.vcf"], vd)[0] for _ in range(3))
             out["in_vcf"] = {"families": a.vcf_families, "samples": npers, "records": a.vcf_records, "vcf_bytes": vbytes,
                              "seconds_write": t_write, "seconds": t_one, "records_per_s": a.vcf_records / t_one,
+                             "small_records": a.vcf_small, "small_seconds": t_small,
+                             "records_per_s_steady": (a.vcf_records - a.vcf_small) / max(1e-9, t_one - t_small),
                              "MB_per_s": vbytes / t_one / 1e6, "records_out": len(body(os.path.join(vd, "o.vcf"))) - 1}
         print(json.dumps(out, indent=1), flush=True)
         return 0 if out["all_vcf_identical"] else 1
