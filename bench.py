@@ -242,10 +242,13 @@ def pmc_traffic():
     if not files:
         return None, None
     d = json.load(open(files[-1]))
+    # the source is stamped with the tree revision its PMC passes ran on (the summary's "revision", else "unknown"),
+    # so a traffic figure from an older kernel shows as such
+    src = os.path.basename(files[-1]) + "@" + str(d.get("revision", "unknown"))[:20]
     for k, v in d.items():
-        if k.startswith("k_brent") and "hbm_read_bytes_per_dispatch" in v:
-            return v["hbm_read_bytes_per_dispatch"] + v.get("hbm_write_bytes_per_dispatch", 0.0), os.path.basename(files[-1])
-    return None, os.path.basename(files[-1])
+        if k.startswith("k_brent") and isinstance(v, dict) and "hbm_read_bytes_per_dispatch" in v:
+            return v["hbm_read_bytes_per_dispatch"] + v.get("hbm_write_bytes_per_dispatch", 0.0), src
+    return None, src
 
 
 def phase_split(st):

@@ -88,6 +88,8 @@ struct pm_engine {
   int Tq = 0, Sq = 0, grid_q = 0;
   int quad_bpc16 = 0, quad_bpc8 = 0;   // QUAD k_brent blocks resident per CU (occupancy query, first launch)
   bool units_empty = false, units1_empty = false;   // a lane plan with no nuclear or founder unit (every family peeled)
+  int ep_bpc[2] = {0, 0};   // EP one-wave k_brent blocks resident per CU (bi-allelic / --denovo instantiation)
+  bool all_trio = false;   // every unit of the lane plan is a 3-person nuclear family (or empty): k_brent's NF = 3
   int4* d_units_q = nullptr;
   int* d_items[N_LISTS] = {nullptr, nullptr, nullptr};
   int* d_counts = nullptr;
@@ -427,6 +429,8 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
   HIP_TRY(hipMemcpy(E->d_sex, ped->sex, ped->n_person, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(E->d_units, units.data(), sizeof(int4) * units.size(), hipMemcpyHostToDevice));
   E->units_empty = std::all_of(units.begin(), units.end(), [](const int4& u) { return u.x == U_NONE; });
+  E->all_trio = !E->units_empty &&
+                std::all_of(units.begin(), units.end(), [](const int4& u) { return u.x == U_NONE || (u.x == U_NUC && (u.w & 0xFF) == 3); });
   {   // k_posterior's family order: by kind, then size (mixed trio / quad pedigrees: no divergent family-size paths)
     std::vector<int> perm(ped->n_fam);
     for (int f = 0; f < ped->n_fam; f++) perm[f] = f;
@@ -772,7 +776,7 @@ static DevArgs make_args(pm_engine* E, int n, const uint8_t* pl, const uint32_t*
 typedef void (*BrentFn)(DevArgs, int);
 // numerics: PM_NUM_PRODUCT / PM_NUM_EXACT for every flavour; PM_NUM_POLY only for the lean kernel
 // (the generic and ES flavours fall back to PRODUCT numerics).
-static BrentFn brent_kernel(int T, int S, int num, bool gen, bool es, bool dn = false, bool pf = false, bool ep = false) {
+static BrentFn brent_kernel(int T, int S, int num, bool gen, bool es, bool dn = false, bool pf = false, bool ep = false, bool trio = false) {
   const int n = (num == PM_NUM_POLY && gen) ? PM_NUM_PRODUCT : num;
   if (es && ep) {   // extended families in polynomial form (PM_NUM_POLY); DN: with the 10-state (--denovo) hoisting
 #define PMKEP(t, s) \
@@ -784,10 +788,12 @@ static BrentFn brent_kernel(int T, int S, int num, bool gen, bool es, bool dn = 
   if (dn && !gen && !es && n == PM_NUM_POLY && pf && T == 64 && S == 16)   // lean --denovo, LDS-staged hoisting only
     return k_brent<64, 16, PM_NUM_POLY, false, false, true, true>;
   if (pf && !dn) {   // lean autosomal kernel with LDS plane prefetch
-#define PMKP(s) if (T == 64 && S == s) return k_brent<64, s, PM_NUM_POLY, false, false, false, true>;
+#define PMKP(s) if (T == 64 && S == s) return trio ? k_brent<64, s, PM_NUM_POLY, false, false, false, true, false, false, 3> \
+                                                   : k_brent<64, s, PM_NUM_POLY, false, false, false, true>;
     PMKP(1) PMKP(2) PMKP(4) PMKP(8) PMKP(16)
 #undef PMKP
-    if (T == 128 && S == 16) return k_brent<128, 16, PM_NUM_POLY, false, false, false, true>;   // 1025-2048 families
+    if (T == 128 && S == 16)   // 1025-2048 families
+      return trio ? k_brent<128, 16, PM_NUM_POLY, false, false, false, true, false, false, 3> : k_brent<128, 16, PM_NUM_POLY, false, false, false, true>;
     return nullptr;
   }
   if (dn && !gen && !es && n == PM_NUM_POLY) {   // lean autosomal --denovo
@@ -913,7 +919,8 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
   }
   const bool ep = !unrelated && n_ext > 0 && E->es_poly && E->par.numerics == PM_NUM_POLY;
   BrentFn fn = quad ? qfn
-                   : brent_kernel(T, S, E->par.numerics, gen, !unrelated && n_ext > 0, A.denovo != 0, A.pf_npad > 0 || A.dn_pf, ep);
+                   : brent_kernel(T, S, E->par.numerics, gen, !unrelated && n_ext > 0, A.denovo != 0, A.pf_npad > 0 || A.dn_pf, ep,
+                                  E->all_trio && !unrelated && !getenv("PM_NO_TRIO"));
   if (!fn) { pm_set_last_error("launch_brent: no kernel variant for the lane plan"); return PM_EINVAL; }
   // multi-wave de novo plans (T = 512 / 1024: more than 1024 families) stage 2 buffers per wave: above the
   // default 64 KB dynamic-LDS limit the kernel must opt in, and the block (plus its static LDS: lane plan,
@@ -940,6 +947,19 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
         grid = E->n_cu * std::max(1, std::min(1024 / T, (int)((160 * 1024) / (need + 8 * 1024))));
       } else (void)hipGetLastError();
     }
+  }
+  if (ep && T == 64) {   // EP one-wave plans: a persistent grid of exactly the resident blocks (no partial second round)
+    int& bpc = E->ep_bpc[fn == brent_kernel(64, S, E->par.numerics, true, true, true, false, true) ? 1 : 0];
+    if (bpc == 0) {
+      int n = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)fn, T, shmem) != hipSuccess || n <= 0) {
+        (void)hipGetLastError();
+        n = 1024 / T;
+      }
+      bpc = n;
+    }
+    grid = std::min(grid, E->n_cu * bpc);
+    grid -= grid % 8;
   }
   // HIP events around every Brent launch (and, for EP, every hoisting launch: pm_kernel_stats reports the two apart)
   auto mark = [&](std::vector<std::pair<hipEvent_t, hipEvent_t>>& v, bool begin) -> int {

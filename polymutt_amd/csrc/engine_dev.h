@@ -45,6 +45,9 @@
 #ifndef PM_QD_WAVES
 #define PM_QD_WAVES 2   // QUAD plans: waves per SIMD the k_brent instantiation is compiled for (launch bounds, grid)
 #endif
+#ifndef PM_EP_WAVES
+#define PM_EP_WAVES 2   // EP (polynomial-form extended families) k_brent: waves per SIMD of the launch bounds
+#endif
 #ifndef PM_QD_KIDSEQ
 #define PM_QD_KIDSEQ 0   // QUAD de novo hoisting: the two kids' lookups one kid at a time
 #endif
@@ -705,15 +708,18 @@ __device__ __forceinline__ void load_units(const int* su, int* uu) {
 // (father, mother, kids), nn persons (0 = empty slot -> the phantom family).  Branch-free: lanes whose
 // family has fewer persons multiply by exactly 1.0 and select, so no exec-masked regions (and no waits
 // per region) are generated; the arithmetic and its order are hoist_nuc's.
+// NF = 3: the plan's every nuclear family is a trio (or the slot is empty): one kid, no second-kid loads or selects (an
+// empty slot's kid terms multiply lF = 0 and are then replaced by the phantom family)
+template <int NF = 0>
 __device__ __forceinline__ void fam_poly4(const uint32_t* by, int nn, const double* lk, double* a) {
   double kids[9];
 #pragma unroll
   for (int k = 0; k < 9; k++) kids[k] = 1.0;
 #pragma unroll
-  for (int q = 2; q < 4; q++) {
+  for (int q = 2; q < (NF == 3 ? 3 : 4); q++) {
     // a missing kid reads l = 1: every autosomal d_one_kid term is then exactly 1.0 (0.5 * (1 + 1),
     // 0.25 + 0.5 + 0.25), the factor the reference never multiplies in -- three selects instead of nine
-    const bool kid = q < nn;
+    const bool kid = NF == 3 || q < nn;
     const double l11 = kid ? lk[by[3 * q]] : 1.0, l12 = kid ? lk[by[3 * q + 1]] : 1.0, l22 = kid ? lk[by[3 * q + 2]] : 1.0;
 #pragma unroll
     for (int k = 0; k < 9; k++) kids[k] *= d_one_kid(k, PM_CHR_AUTO, 0, l11, l12, l22);
@@ -816,7 +822,7 @@ __device__ __forceinline__ void prefetch_planes(const DevArgs& A, const int* ite
 #ifndef PM_HOIST_CHUNK_LDS
 #define PM_HOIST_CHUNK_LDS 2
 #endif
-template <int S, int T>
+template <int S, int T, int NF = 0>
 __device__ __forceinline__ void hoist_poly4_lds(const DevArgs& A, const int* su, const uint8_t* buf, const double* lk,
                                                 double (*a)[5]) {
   const int npad = A.pf_npad;
@@ -830,13 +836,13 @@ __device__ __forceinline__ void hoist_poly4_lds(const DevArgs& A, const int* su,
     const int nn = unit_nn(u);
     uint32_t by[12];
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
+    for (int q = 0; q < (NF == 3 ? 3 : 4); q++) {
       const int pp = unit_first(u) + (q < nn ? q : 0);   // in range for every lane: no branch around the read
       by[3 * q + 0] = buf[pp];
       by[3 * q + 1] = buf[npad + pp];
       by[3 * q + 2] = buf[2 * npad + pp];
     }
-    fam_poly4(by, nn, lk, a[s]);
+    fam_poly4<NF>(by, nn, lk, a[s]);
   }
 }
 
@@ -1736,8 +1742,9 @@ constexpr int brent_waves() { return (NUM == PM_NUM_POLY && !GEN && (T == 64 || 
 // EP: extended families in polynomial form (coefficients from k_es_hoist, es_poly_eval per evaluation); the
 // reference-order peel (d_es_lk) is compiled out, and the block asks for 2 waves per SIMD.
 // QD: lean --denovo kernel on a QUAD plan (hoist_quad: coalesced dword loads, prefetched across items).
-template <int T, int S, int NUM, bool GEN, bool ES, bool DN = false, bool PF = false, bool EP = false, bool QD = false>
-__global__ void __launch_bounds__(T, (EP ? 2 : QD ? PM_QD_WAVES : brent_waves<T, S, NUM, GEN>())) k_brent(DevArgs A, int list) {
+// NF: 3 = every nuclear family of the plan is a trio (the lean PF kernel's hoisting drops the second kid), 0 = any.
+template <int T, int S, int NUM, bool GEN, bool ES, bool DN = false, bool PF = false, bool EP = false, bool QD = false, int NF = 0>
+__global__ void __launch_bounds__(T, (EP ? PM_EP_WAVES : QD ? PM_QD_WAVES : brent_waves<T, S, NUM, GEN>())) k_brent(DevArgs A, int list) {
   constexpr bool PROD = NUM != PM_NUM_EXACT;
   constexpr bool POLYK = NUM == PM_NUM_POLY && !GEN;
   __shared__ double s_lk[256];
@@ -1835,7 +1842,7 @@ __global__ void __launch_bounds__(T, (EP ? 2 : QD ? PM_QD_WAVES : brent_waves<T,
         if (pf) {
           __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's pieces of the item's planes have landed
           if constexpr (T > 64) __syncthreads();   // ... and the other waves' pieces
-          hoist_poly4_lds<S, T>(A, s_u, s_pf, s_lk, cond);
+          hoist_poly4_lds<S, T, NF>(A, s_u, s_pf, s_lk, cond);
           __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): every read of the buffer is done ...
           if constexpr (T > 64) __syncthreads();   // ... by every wave of the block ...
           __builtin_amdgcn_sched_barrier(0);
@@ -1976,6 +1983,8 @@ __global__ void __launch_bounds__(T, (EP ? 2 : QD ? PM_QD_WAVES : brent_waves<T,
             // bracket; non-negative terms, no cancellation), by FMA Horner over the PDM + 1 registers (zeros above D
             // leave the sum's bits unchanged); g^D of all the lane's families as one power g^edl (edl <= 32).  The
             // t (one division) and the powers of g are shared by the lane's families.
+            // (measured and rejected: the powers as one uniform D_total log10(g) added after the reduction -- the two
+            // terms then cancel on flat objectives, whose rounding noise moves Brent's minimiser off the reference's)
             const double t = pos_div(x, g);
             double gp = g, pw = 1.0;
 #pragma unroll

@@ -332,25 +332,40 @@ void ParallelSiteSource::fill(const int* rowOf, uint8_t* pl, uint32_t* dm) {
   const int na = (int)active_.size();
   const int nch = (na + 63) / 64;
   pool_->run(nch, [&](int c) {
-    const int i0 = c * 64, i1 = std::min(na, i0 + 64);
-    int k[64], prev = prevPos_;
-    for (int i = i0; i < i1; i++) k[i - i0] = headAtStart_[active_[i]];
+    const int i0 = c * 64, i1 = std::min(na, i0 + 64), m = i1 - i0;
+    // per person of the chunk: its column, queue base and last index (the section-start placeholder only
+    // as the first head: handled by state() before the site loop)
+    int k[64], col[64], last[64];
+    const GlfState* qb[64];
+    int prev = prevPos_;
+    for (int i = 0; i < m; i++) {
+      const int j = active_[i0 + i];
+      col[i] = j;
+      qb[i] = qs_[j].q.data();
+      last[i] = qs_[j].tail - 1;
+      k[i] = headAtStart_[j];
+    }
     for (int s = 0; s < n; s++) {
       const int cur = lastPos_[s];
       const int r = rowOf[s];
-      for (int i = i0; i < i1; i++) {
-        const int j = active_[i];
-        int& kk = k[i - i0];
-        if (state(j, kk).pos == prev) kk = next(j, kk);
-        if (r < 0) continue;
-        const GlfState& st = state(j, kk);
-        uint8_t* P = pl + ((size_t)r * np + j) * 10;
-        if (st.pos == cur) {
-          std::memcpy(P, st.lk, 10);
-          dm[(size_t)r * np + j] = st.dm;
+      uint8_t* prow = r >= 0 ? pl + (size_t)r * np * 10 : nullptr;
+      uint32_t* drow = r >= 0 ? dm + (size_t)r * np : nullptr;
+      for (int i = 0; i < m; i++) {
+        int kk = k[i];
+        const GlfState* st = kk < 0 ? &virtual_ : qb[i] + kk;
+        if (st->pos == prev) {   // next(): the queue's last state repeats (the end-of-section record)
+          kk = kk < last[i] ? kk + 1 : kk;
+          k[i] = kk;
+          st = kk < 0 ? &virtual_ : qb[i] + kk;
+        }
+        if (!prow) continue;
+        uint8_t* P = prow + (size_t)col[i] * 10;
+        if (st->pos == cur) {
+          std::memcpy(P, st->lk, 10);
+          drow[col[i]] = st->dm;
         } else {
           std::memset(P, 0, 10);
-          dm[(size_t)r * np + j] = 0;
+          drow[col[i]] = 0;
         }
       }
       prev = cur;

@@ -10,6 +10,7 @@ ROUND=${1:-r01}
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$R/gpurun_out/prof_$ROUND
 mkdir -p "$OUT"
+echo "revision: $(cat "$R/REVISION" 2>/dev/null || echo unknown)" > "$OUT/revision.txt"
 cd /tmp && export TMPDIR=/tmp
 BENCH="python3 $R/bench.py --no-cpu-baseline --steps 40 --calib-steps 4"
 step() {   # step NAME SECONDS CMD...

@@ -90,9 +90,17 @@ def main():
         if "WRITE_SIZE_per_dispatch" in d:
             d["hbm_write_bytes_per_dispatch"] = d["WRITE_SIZE_per_dispatch"] * 1024
         out[k] = d
+    # the tree the passes ran on (profile_round.sh writes revision.txt from REVISION): bench.py stamps
+    # roofline.traffic_source with it
+    rev = "unknown"
+    for cand in (os.path.join(src, "revision.txt"), os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "REVISION")):
+        if os.path.exists(cand):
+            rev = open(cand).read().split()[-1] if "revision:" in open(cand).read() else open(cand).read().strip()
+            break
+    out["revision"] = rev
     with open(os.path.join(dst, f"{rnd}_pmc.json"), "w") as fh:
         json.dump(out, fh, indent=1, sort_keys=True)
-    print(json.dumps({k: {kk: round(vv, 1) for kk, vv in v.items()} for k, v in out.items()}, indent=1))
+    print(json.dumps({k: ({kk: round(vv, 1) for kk, vv in v.items()} if isinstance(v, dict) else v) for k, v in out.items()}, indent=1))
 
 
 if __name__ == "__main__":
