@@ -1,5 +1,7 @@
 // glf.cpp -- see glf.h.
 #include "glf.h"
+#include <fcntl.h>
+#include <unistd.h>
 #include <cstdio>
 #include <cstring>
 
@@ -7,13 +9,25 @@ namespace pmhost {
 
 static const uint8_t kTranslateBase[16] = {0, 1, 2, 0, 3, 0, 0, 0, 4, 0, 0, 0, 0, 0, 0, 0};   // glfHandler.cpp:4
 
-GlfFile::~GlfFile() { if (fh_) gzclose(fh_); }
+GlfFile::~GlfFile() {
+  if (fh_) gzclose(fh_);
+  if (fd_ >= 0) ::close(fd_);
+}
 
 bool GlfFile::open(const std::string& path) {
   fh_ = gzopen(path.c_str(), "rb");
   if (!fh_) return false;
   gzbuffer(fh_, 1 << 16);
-  buf_.resize(1 << 15);
+  buf_.resize(1 << 16);
+  if (gzdirect(fh_)) {   // not gzip: plain reads of the file (same bytes, one copy fewer)
+    const int fd = ::open(path.c_str(), O_RDONLY);
+    if (fd >= 0) {
+      posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);
+      fd_ = fd;
+      gzclose(fh_);   // (one descriptor per person, as before)
+      fh_ = nullptr;
+    }
+  }
   pos_ = len_ = 0;
   zeof_ = false;
   // glfHandler::ReadHeader (:87-134): "GLF\3", u32 header length, header text
@@ -21,11 +35,20 @@ bool GlfFile::open(const std::string& path) {
   uint32_t hlen = 0;
   if (read(magic, 4) != 4 || magic[0] != 'G' || magic[1] != 'L' || magic[2] != 'F' || magic[3] != 3 ||
       read(&hlen, 4) != 4 || hlen > 1024 * 1024) {
-    gzclose(fh_); fh_ = nullptr;
+    if (fh_) gzclose(fh_);
+    fh_ = nullptr;
+    if (fd_ >= 0) ::close(fd_);
+    fd_ = -1;
     return false;
   }
   std::vector<char> h(hlen);
-  if (hlen && read(h.data(), hlen) != hlen) { gzclose(fh_); fh_ = nullptr; return false; }
+  if (hlen && read(h.data(), hlen) != hlen) {
+    if (fh_) gzclose(fh_);
+    fh_ = nullptr;
+    if (fd_ >= 0) ::close(fd_);
+    fd_ = -1;
+    return false;
+  }
   endOfSection = true;
   return true;
 }
@@ -36,7 +59,7 @@ size_t GlfFile::read(void* dst, size_t n) {
   while (got < n) {
     if (pos_ == len_) {
       if (zeof_) break;
-      int r = gzread(fh_, buf_.data(), (unsigned)buf_.size());
+      const int r = fd_ >= 0 ? (int)::read(fd_, buf_.data(), buf_.size()) : gzread(fh_, buf_.data(), (unsigned)buf_.size());
       if (r <= 0) { zeof_ = true; break; }
       len_ = (size_t)r; pos_ = 0;
     }

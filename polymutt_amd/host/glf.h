@@ -23,7 +23,7 @@ class GlfFile {
  public:
   ~GlfFile();
   bool open(const std::string& path);   // false if the file cannot be opened
-  bool isOpen() const { return fh_ != nullptr; }
+  bool isOpen() const { return fh_ != nullptr || fd_ >= 0; }
   bool nextSection();
   bool nextEntry();
   bool nextBaseEntry();
@@ -41,6 +41,7 @@ class GlfFile {
   size_t read(void* dst, size_t n);
   bool eof();
   gzFile fh_ = nullptr;
+  int fd_ = -1;   // an uncompressed file: read() straight into buf_ (gzread's transparent mode copies once more)
   std::vector<uint8_t> buf_;
   size_t pos_ = 0, len_ = 0;
   bool zeof_ = false;

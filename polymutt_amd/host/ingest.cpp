@@ -63,9 +63,34 @@ void TaskPool::run(int n, const std::function<void(int)>& fn) {
 static double ing_now() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 
 ParallelSiteSource::~ParallelSiteSource() {
+  joinAhead();
   if (getenv("PM_TIMING"))
-    fprintf(stderr, "PM_TIMING glf ingest: decode %.3f s, merge %.3f s, fill %.3f s\n", t_decode_, t_merge_, t_fill_);
+    fprintf(stderr, "PM_TIMING glf ingest: decode %.3f s, merge %.3f s, fill %.3f s (decode ahead %.3f s)\n", t_decode_, t_merge_,
+            t_fill_, t_ahead_);
+  delete dpool_;
   delete pool_;
+}
+
+// The decode-ahead of the next window (on its own pool, while the caller fills this window's rows): each person's
+// queue grows at its tail only, within the capacity reserved at the section start, so the states fill() reads --
+// those between the heads before and after the last merge -- are neither moved nor reallocated under it.
+void ParallelSiteSource::startAhead() {
+  if (!dpool_) return;
+  ahead_ = std::thread([this] {
+    const double t0 = ing_now();
+    const int na = (int)active_.size();
+    const int chunk = std::max(1, std::min(64, na / (4 * dpool_->threads()) + 1));
+    dpool_->run((na + chunk - 1) / chunk, [&](int c) {
+      for (int i = c * chunk; i < std::min(na, (c + 1) * chunk); i++) {
+        const int j = active_[i];
+        extend(j, std::max(qs_[j].head, 0) + window_ + 1);
+      }
+    });
+    t_ahead_ += ing_now() - t0;
+  });
+}
+void ParallelSiteSource::joinAhead() {
+  if (ahead_.joinable()) ahead_.join();
 }
 
 void ParallelSiteSource::open(const Pedigree& ped, const std::string& glfIndexFile, int threads, int window) {
@@ -109,6 +134,8 @@ void ParallelSiteSource::open(const Pedigree& ped, const std::string& glfIndexFi
   for (int j = 0; j < n; j++)
     if (has_[j]) active_.push_back(j);
   headAtStart_.assign(n, -1);
+  tailAtMerge_.assign(n, 0);
+  if (threads > 1 && !getenv("PM_NO_DECODE_AHEAD")) dpool_ = new TaskPool(std::max(1, threads / 2));
   lastPos_.assign(window_, 0);
   fast_ = !getenv("PM_SERIAL_MERGE");
   virtual_.pos = 0;
@@ -128,11 +155,14 @@ void ParallelSiteSource::forChunks(F f) {
 }
 
 bool ParallelSiteSource::nextSection() {   // PedigreeGLF::Move2NextSection, :197-220
+  joinAhead();
   std::vector<char> flag(files_.size(), 0);
   forChunks([&](int j) {
     flag[j] = files_[j].nextSection();
     Queue& Q = qs_[j];
     Q.head = -1; Q.tail = 0; Q.terminal = false;
+    const size_t cap = 2 * (size_t)window_ + 4;   // (the decode-ahead never reallocates a queue)
+    if (Q.q.size() < cap) { Q.q.resize(cap); Q.qp.resize(cap); }
   });
   const GlfFile& ref = files_[nonNull_];
   for (int j : active_) {   // checks in person order, as the serial loop makes them
@@ -162,6 +192,13 @@ void ParallelSiteSource::refill(int j, int need) {
   }
   const int target = std::max(Q.head, 0) + need;
   if ((int)Q.q.size() < target) { Q.q.resize(target); Q.qp.resize(target); }
+  extend(j, target);
+}
+
+// Decodes states at the queue's tail until it holds `target` (or the section's end record).
+void ParallelSiteSource::extend(int j, int target) {
+  Queue& Q = qs_[j];
+  target = std::min(target, (int)Q.q.size());
   GlfFile& g = files_[j];
   while (Q.tail < target && !Q.terminal) {   // glfHandler::NextBaseEntry, :195-204
     g.nextBaseEntry();
@@ -182,6 +219,7 @@ int ParallelSiteSource::nextSites(int maxSites, int* pos, uint8_t* ref) {
   maxSites = std::min(maxSites, window_);
   // a call advances a person at most once: maxSites + 1 states from the head cover the whole window
   const double t0 = ing_now();
+  joinAhead();   // (the previous window's fill is done: states before the heads may move now)
   forChunks([&](int j) { refill(j, maxSites + 1); });
   const double t1 = ing_now();
   t_decode_ += t1 - t0;
@@ -224,7 +262,9 @@ int ParallelSiteSource::nextSites(int maxSites, int* pos, uint8_t* ref) {
     lastPos_[s] = mn;
   }
   nLast_ = s;
+  for (int j : active_) tailAtMerge_[j] = qs_[j].tail;
   t_merge_ += ing_now() - t1;
+  if (!ended_) startAhead();   // the next window's states decode while fill() writes this one's rows
   return s;
 }
 
@@ -342,7 +382,7 @@ void ParallelSiteSource::fill(const int* rowOf, uint8_t* pl, uint32_t* dm) {
       const int j = active_[i0 + i];
       col[i] = j;
       qb[i] = qs_[j].q.data();
-      last[i] = qs_[j].tail - 1;
+      last[i] = tailAtMerge_[j] - 1;   // (the tail as the merge saw it: the decode-ahead may be extending it)
       k[i] = headAtStart_[j];
     }
     for (int s = 0; s < n; s++) {

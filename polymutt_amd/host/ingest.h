@@ -110,6 +110,9 @@ class ParallelSiteSource : public SiteStream {
     bool terminal = false;  // q[tail - 1] is the end-of-section state, which repeats forever
   };
   void refill(int j, int need);
+  void extend(int j, int target);
+  void startAhead();
+  void joinAhead();
   const GlfState& state(int j, int k) const { return k < 0 ? virtual_ : qs_[j].q[k]; }
   int next(int j, int k) const { return (k + 1 < qs_[j].tail) ? k + 1 : k; }
   template <class F> void forChunks(F f);
@@ -127,7 +130,10 @@ class ParallelSiteSource : public SiteStream {
   bool ended_ = false;
   // the last nextSites call: currentPos and queue heads before it, and the merged positions
   int prevPos_ = 0, nLast_ = 0;
-  std::vector<int> headAtStart_, lastPos_;
+  std::vector<int> headAtStart_, lastPos_, tailAtMerge_;
+  TaskPool* dpool_ = nullptr;   // the decode-ahead's workers (startAhead)
+  std::thread ahead_;
+  double t_ahead_ = 0;
   double t_decode_ = 0, t_merge_ = 0, t_fill_ = 0;   // PM_TIMING: wall seconds per stage
   // the parallel merge of a run of calls (fastMerge; PM_SERIAL_MERGE=1 turns it off)
   int fastMerge(int maxSites, int maxPos, int* pos, uint8_t* ref);

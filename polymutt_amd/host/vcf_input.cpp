@@ -14,6 +14,9 @@
 #include <string>
 #include <thread>
 #include <vector>
+#include <unistd.h>
+#include <chrono>
+#include <memory>
 #include "ingest.h"
 #include "vcf_fmt.h"
 
@@ -172,6 +175,10 @@ struct Pending {          // one record awaiting output, in file order
   // classify_pre (parallel): the record's own facts; classify_apply (serial, in file order) the FORMAT state machine
   int bial = 0;           // 1 biallelic, 0 not
   int dp_c = -1, gl_c = -1, pl_c = -1;   // this record's FORMAT indices of DP / GL / PL
+  void reset() {          // (keeps the line's and the columns' buffers: records are recycled, not reallocated)
+    line.clear(); cols.clear();
+    computed = false; slot = -1; a1 = a2 = 0; indel = false; dp_idx = -1; bial = 0; dp_c = gl_c = pl_c = -1;
+  }
 };
 
 struct State {            // what FamilyLikelihoodSeq_VCF holds between records (stale output, :412-521)
@@ -301,7 +308,16 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
   std::vector<uint32_t> dm((size_t)B * np, 0);
   std::vector<pm_site_result> res(B);
   std::vector<pm_geno_call> calls((size_t)B * np);
-  std::vector<Pending> pend;
+  // records are recycled through a free list (their 10-100 KB line and column buffers are reused, not reallocated and
+  // first-touched for every record); pend: the records awaiting output, in file order
+  std::vector<std::unique_ptr<Pending>> store;
+  std::vector<Pending*> freel, pend;
+  auto take = [&]() -> Pending* {
+    if (freel.empty()) { store.emplace_back(new Pending); return store.back().get(); }
+    Pending* r = freel.back();
+    freel.pop_back();
+    return r;
+  };
   int nb = 0, cur_chrom = -1, n_samples_with_data = 0, bad_allele = 0;
   FormatState fs;
   bool first = R == 0;   // FillPenetrance's first-record banner (:270-282): rank 0 owns the file's first record
@@ -393,26 +409,71 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
   };
 
   TaskPool pool(std::max(1, std::min(16, opt.io_threads > 0 ? opt.io_threads : (int)std::thread::hardware_concurrency())));
+  // PM_TIMING=1: wall seconds per stage on stderr at the end (read, split + classify, PL parse, engine, format, write)
+  double tm[6] = {0, 0, 0, 0, 0, 0};
+  auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  struct TimingOut {
+    double* t;
+    ~TimingOut() {
+      if (getenv("PM_TIMING"))
+        fprintf(stderr, "PM_TIMING vcf input: read %.3f s, classify %.3f s, parse %.3f s, engine %.3f s, format %.3f s, write %.3f s\n",
+                t[0], t[1], t[2], t[3], t[4], t[5]);
+    }
+  } timing_out{tm};
   std::vector<std::string> texts;
   std::vector<RecState> states;
   auto flush = [&]() {
     int rows = 0;
+    double t0 = now();
     if (nb > 0) eval.run(nb, pl.data(), dm.data(), ref.data(), res.data(), calls.data(), &rows);
+    double t1 = now();
+    tm[3] += t1 - t0;
     // the state each record prints with (sequential: a record without data takes the last computed one's)
     states.resize(pend.size());
     RecState cur{st.qual, st.min, st.calls.data()};
     for (size_t k = 0; k < pend.size(); k++) {
-      const Pending& r = pend[k];
+      const Pending& r = *pend[k];
       if (r.computed) cur = fresh_state(r, &res[r.slot], calls.data() + (size_t)res[r.slot].call_row * np);
       states[k] = cur;
     }
     if (texts.size() < pend.size()) texts.resize(pend.size());
-    pool.run((int)pend.size(), [&](int k) { texts[k].clear(); format_record(texts[k], pend[k], states[k]); });
-    for (size_t k = 0; k < pend.size(); k++) fwrite(texts[k].data(), 1, texts[k].size(), out);
+    pool.run((int)pend.size(), [&](int k) { texts[k].clear(); format_record(texts[k], *pend[k], states[k]); });
+    const double t2 = now();
+    tm[4] += t2 - t1;
+    {   // the batch's records written in parallel, each group of records at its own offset (pwrite), in file order
+      const int nr = (int)pend.size();
+      std::vector<int64_t> at(nr + 1, 0);
+      for (int k = 0; k < nr; k++) at[k + 1] = at[k] + (int64_t)texts[k].size();
+      fflush(out);
+      const int64_t base = (int64_t)ftello(out);
+      const int fd = fileno(out);
+      const int ng = std::min(nr, 4 * pool.threads());
+      std::vector<char> werr(std::max(ng, 1), 0);
+      if (nr > 0 && base >= 0 && at[nr] > ((int64_t)1 << 20)) {
+        pool.run(ng, [&](int g) {
+          for (int k = (int)((int64_t)nr * g / ng); k < (int)((int64_t)nr * (g + 1) / ng); k++) {
+            const char* p = texts[k].data();
+            size_t left = texts[k].size();
+            int64_t off = base + at[k];
+            while (left > 0) {
+              const ssize_t w = pwrite(fd, p, left, (off_t)off);
+              if (w <= 0) { werr[g] = 1; return; }
+              p += w; left -= (size_t)w; off += w;
+            }
+          }
+        });
+        for (char e : werr)
+          if (e) throw FatalError("Write to the output VCF failed\n");
+        if (fseeko(out, (off_t)(base + at[nr]), SEEK_SET) != 0) throw FatalError("Write to the output VCF failed\n");
+      } else
+        for (int k = 0; k < nr; k++) fwrite(texts[k].data(), 1, texts[k].size(), out);
+    }
+    tm[5] += now() - t2;
     if (!pend.empty()) {   // the last state carries into the next batch
       st.qual = cur.qual; st.min = cur.min;
       if (cur.calls != st.calls.data()) std::copy(cur.calls, cur.calls + np, st.calls.begin());
     }
+    for (Pending* r : pend) freel.push_back(r);
     pend.clear();
     nb = 0;
   };
@@ -495,13 +556,13 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
   // Chunks of records: read and classified in order (the FORMAT bookkeeping carries from record to record), their
   // PL / GL fields parsed in parallel into per-record rows, then handled in order as the reference does.
   const int CH = 256;
-  std::vector<Pending> chunk(CH);
+  std::vector<Pending*> chunk(CH, nullptr);
   std::vector<int> kinds(CH), withdata(CH);
   std::vector<std::string> perr(CH);
   std::vector<uint8_t> rows((size_t)CH * np * 10);
   // FillPenetrance's per-sample loop (:338-382) for record k of the chunk: phred bytes of (geno11, geno12, geno22)
   auto parse_row = [&](int k) {
-    const Pending& r = chunk[k];
+    const Pending& r = *chunk[k];
     const std::string& L = r.line;
     uint8_t* row = rows.data() + (size_t)k * np * 10;
     memset(row, 0, (size_t)np * 10);
@@ -557,17 +618,22 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
   while (!eof) {
     // a chunk of lines from the block (in order), copied, split and classified in parallel, then the FORMAT
     // bookkeeping applied in file order
+    double ta = now();
     br.chunk(CH, lines);
+    double tb = now();
+    tm[0] += tb - ta;
     if (lines.empty()) break;
     int nl = (int)lines.size();
     for (int k = 0; k < nl; k++)
       if (lines[k].off >= hi) { nl = k; eof = true; break; }   // (a shard's byte range ends before this line)
+    for (int k = 0; k < nl; k++)
+      if (!chunk[k]) chunk[k] = take();
     pool.run(nl, [&](int k) {
       const BlockReader::Line& l = lines[k];
       keep[k] = l.n > 0 && l.p[0] != '#';
       if (!keep[k]) return;
-      Pending& r = chunk[k];
-      r = Pending();
+      Pending& r = *chunk[k];
+      r.reset();
       r.line.assign(l.p, l.n);
       classify_pre(r);
     });
@@ -575,7 +641,7 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
     for (int k = 0; k < nl; k++) {
       if (!keep[k]) continue;
       if (nc != k) std::swap(chunk[nc], chunk[k]);
-      Pending& r = chunk[nc];
+      Pending& r = *chunk[nc];
       if (first)   // FillPenetrance on the first record (:270-282) ...
         for (size_t i = 0; i < samples.size(); i++) {
           if (col_person[i] < 0) { printf("Sample ID \"%s\" not included in the analysis!\n", samples[i].c_str()); continue; }
@@ -588,13 +654,16 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
       }
       nc++;
     }
+    ta = now();
+    tm[1] += ta - tb;
     pool.run(nc, [&](int k) { if (kinds[k] > 0) parse_row(k); });
+    tm[2] += now() - ta;
     for (int k = 0; k < nc; k++) {
       const int kind = kinds[k];
       if (kind < 0) bad_allele++;
       if (kind <= 0) continue;   // OutputVCF returns at once for these records (:419)
       if (!perr[k].empty()) throw FatalError(perr[k]);
-      Pending& r = chunk[k];
+      Pending& r = *chunk[k];
       const std::string& L = r.line;
       // chromosome class of the record (PedVCF.cpp:121-124)
       const std::string chrom = L.substr(r.cols[0].b, r.cols[0].e - r.cols[0].b);
@@ -603,7 +672,10 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
         if (lead && !computed_any) {   // ... which an earlier rank computed: written after the exchange
           fprintf(lead, "%d\t%s\n", r.dp_idx, r.line.c_str());   // (with its DP index snapshot)
           n_lead++;
-        } else pend.push_back(std::move(r));
+        } else {
+          pend.push_back(chunk[k]);
+          chunk[k] = nullptr;
+        }
         continue;
       }
       computed_any = true;
@@ -617,7 +689,8 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
       r.slot = nb;
       ref[nb] = (uint8_t)(r.a1 | (r.a2 << 4));
       nb++;
-      pend.push_back(std::move(r));
+      pend.push_back(chunk[k]);
+      chunk[k] = nullptr;
       if (nb == B) flush();
     }
   }
