@@ -620,12 +620,56 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
   std::map<int, int> leafs;   // the marriage slots the leaf steps write
   for (int k = 0; k < nst; k++)
     if (leaf[k]) leafs[(F.steps[k].y >> 8) & 255] = 1;
+  // (computed before the layout: persons never stored get no workspace region)
+  std::vector<char> regf(n, 0), regn(n, 0), iinit(n, 0);
+  // (the initial partials formed in the type-2 lanes need no cross-lane read: pair mode keeps them too)
+  if (NS == 10 && part == 2 && multi <= 1 && (g_regp || g_pair)) {
+    const int finp = (F.steps.back().x >> 24) & 255;
+    // (pair mode: such a founder's terms read its penetrance straight from the PEN table, no v_readlane)
+    for (int i = 0; i < n; i++) regf[i] = ((g_regp && g_regf) || g_pair) && F.founder[i] && i < F.nf && !leafp[i] && i != finp;
+    for (int k = 0; k < nst; k++) {
+      if (!inpart(k)) continue;
+      const int ty2 = F.steps[k].x & 255, f0 = (F.steps[k].x >> 8) & 255, f1 = (F.steps[k].x >> 16) & 255, t0 = (F.steps[k].x >> 24) & 255;
+      if (ty2 == 2) { regf[t0] = 0; if (!pristine[k]) regf[f0] = 0; }
+      else if (ty2 == 3) regf[f0] = regf[f1] = regf[t0] = 0;
+      else regf[f0] = 0;
+    }
+    // non-founders whose partial is the penetrance until one type-2 step peels a spouse into it, and is then read
+    // only as a type-1 offspring (by v_readlane from that step's registers): never stored either
+    std::vector<int> t2to(n, 0);
+    for (int i = 0; i < n; i++) regn[i] = !(F.founder[i] && i < F.nf) && !leafp[i] && i != finp;
+    for (int k = 0; k < nst; k++) {
+      if (!inpart(k)) continue;
+      const int ty2 = F.steps[k].x & 255, f0 = (F.steps[k].x >> 8) & 255, f1 = (F.steps[k].x >> 16) & 255, t0 = (F.steps[k].x >> 24) & 255;
+      if (ty2 == 2) { t2to[t0]++; regn[f0] = 0; }
+      else if (ty2 == 3) regn[f0] = regn[f1] = regn[t0] = 0;
+      else if (!t2to[f0]) regn[f0] = 0;   // (a type-1 read before the type-2 step)
+    }
+    for (int i = 0; i < n; i++)
+      if (t2to[i] != 1 || g_regp == 2 || !g_regp) regn[i] = 0;
+    // persons whose first use is as the to-person of a type-2 step: their initial partial (penetrance, or prior x
+    // penetrance) is formed inside that step's lanes instead of being stored and read back
+    std::vector<char> seen(n, 0);
+    for (int k = 0; k < nst; k++) {
+      if (!inpart(k)) continue;
+      const int ty2 = F.steps[k].x & 255, f0 = (F.steps[k].x >> 8) & 255, f1 = (F.steps[k].x >> 16) & 255, t0 = (F.steps[k].x >> 24) & 255;
+      if (ty2 == 2 && !seen[t0] && !regf[t0]) iinit[t0] = 1;
+      seen[f0] = 1;
+      if (ty2 != 1) seen[t0] = 1;
+      if (ty2 == 3) seen[f1] = 1;
+    }
+    for (int i = 0; i < n; i++)
+      if (leafp[i]) iinit[i] = 0;
+  }
   std::vector<int> po(n);
   std::map<int, int> mo;
   int off = 0, LSZ = 0;
   for (int L = part ? 1 : 0; L >= 0; L--) {
     for (int i = 0; i < n; i++)
-      if (!part || leafp[i] == L) { po[i] = off; off += NS * capP[i]; }
+      if (!part || leafp[i] == L) {
+        po[i] = off;
+        if (!regf[i] && !regn[i]) off += NS * capP[i];   // (a register- or PEN-read founder / register-only non-founder: no region)
+      }
     for (auto& m : capM)
       if (!part || (int)leafs.count(m.first) == L) {
         mo[m.first] = off;
@@ -653,55 +697,17 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
     if (!mc) return body;
     return "#pragma unroll\n      for (int c = 0; c < " + S(M) + "; c++) {\n      const int cb = c * " + S(NSZ) + ";\n" + body + "      }\n";
   };
-  std::string code = mc ? "" : "  const int g11 = gg11, g12 = gg12, g22 = gg22;\n  (void)g11; (void)g12; (void)g22;\n";
+  std::string code = mc ? "" : "  const int g11 = gg11, g12 = gg12, g22 = gg22;\n  (void)g11; (void)g12; (void)g22;\n";  for (int i = 0; i < n; i++)
+    if (regf[i] && !g_pair) code += "  double fp" + std::to_string(i) + " = 0.0;\n";
+
   // Founders whose partial this part reads only through pristine type-2 steps (their states' prior x penetrance
   // terms): the partial is never stored; lane x keeps the state's penetrance (fp<i>) and the terms take it by
   // v_readlane at the term's (wave-uniform) state -- the same value the stored partial would have held
-  std::vector<char> regf(n, 0), regn(n, 0), iinit(n, 0);
-  if (NS == 10 && part == 2 && multi <= 1 && g_regp) {
-    const int finp = (F.steps.back().x >> 24) & 255;
-    for (int i = 0; i < n; i++) regf[i] = g_regf && F.founder[i] && i < F.nf && !leafp[i] && i != finp;
-    for (int k = 0; k < nst; k++) {
-      if (!inpart(k)) continue;
-      const int ty2 = F.steps[k].x & 255, f0 = (F.steps[k].x >> 8) & 255, f1 = (F.steps[k].x >> 16) & 255, t0 = (F.steps[k].x >> 24) & 255;
-      if (ty2 == 2) { regf[t0] = 0; if (!pristine[k]) regf[f0] = 0; }
-      else if (ty2 == 3) regf[f0] = regf[f1] = regf[t0] = 0;
-      else regf[f0] = 0;
-    }
-    for (int i = 0; i < n; i++)
-      if (regf[i]) code += "  double fp" + S(i) + " = 0.0;\n";
-    // non-founders whose partial is the penetrance until one type-2 step peels a spouse into it, and is then read
-    // only as a type-1 offspring (by v_readlane from that step's registers): never stored either
-    std::vector<int> t2to(n, 0);
-    for (int i = 0; i < n; i++) regn[i] = !(F.founder[i] && i < F.nf) && !leafp[i] && i != finp;
-    for (int k = 0; k < nst; k++) {
-      if (!inpart(k)) continue;
-      const int ty2 = F.steps[k].x & 255, f0 = (F.steps[k].x >> 8) & 255, f1 = (F.steps[k].x >> 16) & 255, t0 = (F.steps[k].x >> 24) & 255;
-      if (ty2 == 2) { t2to[t0]++; regn[f0] = 0; }
-      else if (ty2 == 3) regn[f0] = regn[f1] = regn[t0] = 0;
-      else if (!t2to[f0]) regn[f0] = 0;   // (a type-1 read before the type-2 step)
-    }
-    for (int i = 0; i < n; i++)
-      if (t2to[i] != 1 || g_regp == 2) regn[i] = 0;
-    // persons whose first use is as the to-person of a type-2 step: their initial partial (penetrance, or prior x
-    // penetrance) is formed inside that step's lanes instead of being stored and read back
-    std::vector<char> seen(n, 0);
-    for (int k = 0; k < nst; k++) {
-      if (!inpart(k)) continue;
-      const int ty2 = F.steps[k].x & 255, f0 = (F.steps[k].x >> 8) & 255, f1 = (F.steps[k].x >> 16) & 255, t0 = (F.steps[k].x >> 24) & 255;
-      if (ty2 == 2 && !seen[t0] && !regf[t0]) iinit[t0] = 1;
-      seen[f0] = 1;
-      if (ty2 != 1) seen[t0] = 1;
-      if (ty2 == 3) seen[f1] = 1;
-    }
-    for (int i = 0; i < n; i++)
-      if (leafp[i]) iinit[i] = 0;
-  }
   // InitializePartials x SetFounderPriors, one person at a time (lanes over its states)
   for (int i = 0; i < n; i++) {
     if ((part == 1 && !leafp[i]) || (part == 2 && leafp[i])) continue;
     if (regf[i]) {
-      code += lanes(NS, "x", "    fp" + S(i) + " = PEN[x * " + S(n) + " + " + S(i) + "];\n");
+      if (!g_pair) code += lanes(NS, "x", "    fp" + S(i) + " = PEN[x * " + S(n) + " + " + S(i) + "];\n");
       continue;
     }
     if (regn[i] || iinit[i]) continue;   // (its type-2 step forms the initial partial itself)
@@ -971,8 +977,15 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
               return "__hiloint2double(__builtin_amdgcn_readlane(__double2hiint(" + v + "), j), __builtin_amdgcn_readlane(__double2loint(" +
                      v + "), j))";
             };
-            std::string pe = pj((F.steps[run.back()].x >> 8) & 255);
-            for (int r2 = (int)run.size() - 2; r2 >= 0; r2--) pe = "q_ == " + S(r2) + " ? " + pj((F.steps[run[r2]].x >> 8) & 255) + " : " + pe;
+            std::string pe;
+            if (g_pair) {   // the penetrance the init phase would have stored, from PEN (one read: the person index selected)
+              std::string who = S((F.steps[run.back()].x >> 8) & 255);
+              for (int r2 = (int)run.size() - 2; r2 >= 0; r2--) who = "q_ == " + S(r2) + " ? " + S((F.steps[run[r2]].x >> 8) & 255) + " : " + who;
+              pe = "PEN[j * " + S(n) + " + (" + who + ")]";
+            } else {
+              pe = pj((F.steps[run.back()].x >> 8) & 255);
+              for (int r2 = (int)run.size() - 2; r2 >= 0; r2--) pe = "q_ == " + S(r2) + " ? " + pj((F.steps[run[r2]].x >> 8) & 255) + " : " + pe;
+            }
             t += "        const double pj_ = " + pe + ";\n";
             t += (!top && d0[sf] == 2 && q == 1) ? "        const double f = 2 * pj_;\n" : "        const double f = pj_;\n";
           } else t += "        const double f = W[" + OF + " + j * " + S(fcap) + " + " + S(u) + "];\n";
@@ -1031,7 +1044,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
       const bool keep = NS == 10 && !mc && g_regp;   // (the outputs stay in registers for a following type-1 phase)
       const bool rn = keep && regn[stt];   // (the to-person is register-only: its partial was its penetrance)
       b += "    double t[" + S(g.c + 1) + "];\n";
-      if (keep && iinit[stt]) {   // the initial partial at state i (InitializePartials x SetFounderPriors, as the init phase)
+      if ((keep || (NS == 10 && !mc && g_pair)) && iinit[stt]) {   // the initial partial at state i (InitializePartials x SetFounderPriors)
         std::string tp = S((F.steps[run.back()].x >> 24) & 255);   // (packed: the lane group's to-person)
         for (int r2 = (int)run.size() - 2; r2 >= 0; r2--) tp = "q_ == " + S(r2) + " ? " + S((F.steps[run[r2]].x >> 24) & 255) + " : " + tp;
         const bool fo2 = F.founder[stt] && stt < F.nf;
