@@ -460,6 +460,8 @@ int g_expt = 0;        // PM_ES_EXPT=1/2: timing experiments only (results wrong
 // over 30 pairs, the final sum) does two families' work per instruction; g_wl = the lanes per family (64 or 32).
 // Pair mode reads partials across lanes through LDS only (no v_readlane from fixed lanes: PM_ES_REGP / REGF off).
 bool g_pair = false;
+bool g_xcd = true;        // PM_ES_XCD=0: units dealt to the blocks in plain order
+bool g_no_penp = false;   // PM_ES_PENP=0: leaf offspring partials stored and read from the workspace
 int g_wl = 64;
 
 struct WaveGen {
@@ -661,6 +663,11 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
     for (int i = 0; i < n; i++)
       if (leafp[i]) iinit[i] = 0;
   }
+  // leaf offspring (parts): a non-founder whose partial is its penetrance, never changed, read by leaf steps only --
+  // the steps read PEN directly (the site's penetrances stay in the slice for the task), no region, no init
+  std::vector<char> penp(n, 0);
+  if (NS == 10 && part && !g_no_penp)
+    for (int i = 0; i < n; i++) penp[i] = leafp[i] && !(F.founder[i] && i < F.nf);
   std::vector<int> po(n);
   std::map<int, int> mo;
   int off = 0, LSZ = 0;
@@ -668,7 +675,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
     for (int i = 0; i < n; i++)
       if (!part || leafp[i] == L) {
         po[i] = off;
-        if (!regf[i] && !regn[i]) off += NS * capP[i];   // (a register- or PEN-read founder / register-only non-founder: no region)
+        if (!regf[i] && !regn[i] && !penp[i]) off += NS * capP[i];   // (a register- or PEN-read founder / register-only non-founder: no region)
       }
     for (auto& m : capM)
       if (!part || (int)leafs.count(m.first) == L) {
@@ -679,6 +686,12 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
   }
   const int TB = off, NSZ = off + tmp - LSZ;
   *ws_doubles = part == 1 ? LSZ : LSZ + M * NSZ;   // (the leaf prefix writes its own regions only)
+  if (getenv("PM_JIT_LAYOUT")) {
+    fprintf(stderr, "layout %s NS %d part %d top %d: LSZ %d NSZ %d tmp %d ws %d |", name.c_str(), NS, part, (int)top, LSZ, NSZ, tmp, *ws_doubles);
+    for (int i = 0; i < n; i++) fprintf(stderr, " p%d:%d%s", i, (!regf[i] && !regn[i]) ? NS * capP[i] : 0, leafp[i] ? "L" : "");
+    for (auto& m : capM) fprintf(stderr, " m%d:%d", m.first, (crows.count(m.first) ? crows[m.first] : NS * NS) * m.second);
+    fprintf(stderr, "\n");
+  }
   auto S = [](long v) { return std::to_string(v); };
   const std::string nsS = S(NS), nsq = S(NS * NS), R = S((NS * NS + g_wl - 1) / g_wl), WL = S(g_wl);
   const bool mc = part == 2 && M > 1;   // offsets of the item's own regions carry cb (several items per call)
@@ -697,7 +710,8 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
     if (!mc) return body;
     return "#pragma unroll\n      for (int c = 0; c < " + S(M) + "; c++) {\n      const int cb = c * " + S(NSZ) + ";\n" + body + "      }\n";
   };
-  std::string code = mc ? "" : "  const int g11 = gg11, g12 = gg12, g22 = gg22;\n  (void)g11; (void)g12; (void)g22;\n";  for (int i = 0; i < n; i++)
+  std::string code = mc ? "" : "  const int g11 = gg11, g12 = gg12, g22 = gg22;\n  (void)g11; (void)g12; (void)g22;\n";
+  for (int i = 0; i < n; i++)
     if (regf[i] && !g_pair) code += "  double fp" + std::to_string(i) + " = 0.0;\n";
 
   // Founders whose partial this part reads only through pristine type-2 steps (their states' prior x penetrance
@@ -710,7 +724,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
       if (!g_pair) code += lanes(NS, "x", "    fp" + S(i) + " = PEN[x * " + S(n) + " + " + S(i) + "];\n");
       continue;
     }
-    if (regn[i] || iinit[i]) continue;   // (its type-2 step forms the initial partial itself)
+    if (regn[i] || iinit[i] || penp[i]) continue;   // (its type-2 step forms the initial partial itself / PEN)
     const bool fo = F.founder[i] && i < F.nf;
     const int sx = F.sex[i];
     const bool yf = NS == 3 && Y && sx == FEMALE;
@@ -781,8 +795,8 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
       for (int a = 0; a <= g.a; a++) {
         b += "      s[" + S(a) + "] = 0.0;\n";
         b += "#pragma unroll\n      for (int k = 0; k < " + nsS + "; k++) s[" + S(a) + "] = fma(" +
-             (NS == 10 ? std::string(g_tr_regs ? "(r == 0 ? tr0[k] : tr1[k])" : "t10dn[e * 10 + k]") : tt(csex, "e", "k", false)) + ", W[" + PO(off_) + " + k * " +
-             S(pcap) + " + " + S(a) + "], s[" + S(a) + "]);\n";
+             (NS == 10 ? std::string(g_tr_regs ? "(r == 0 ? tr0[k] : tr1[k])" : "t10dn[e * 10 + k]") : tt(csex, "e", "k", false)) + ", " +
+             (penp[off_] ? "PEN[k * " + S(n) + " + " + S(off_) + "]" : "W[" + PO(off_) + " + k * " + S(pcap) + " + " + S(a) + "]") + ", s[" + S(a) + "]);\n";
       }
       const std::string me = MOf(slot) + " + e * " + S(mcap);
       if (create) {
@@ -859,6 +873,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
                     "), __builtin_amdgcn_readlane(__double2loint(" + v + "), " + L + "));\n";
             } else
             c1 += g_expt == 2 ? "      {\n        const double p = 0.5 + 0.01 * k + " + S(a) + ";\n"   // (timing experiment only)
+                              : penp[offq] ? "      {\n        const double p = PEN[k * " + S(n) + " + " + S(offq) + "];\n"
                               : "      {\n        const double p = W[" + PO(offq) + " + k * " + S(capP[offq]) + " + " + S(a) + "];\n";
             for (int pr = 0; pr < npair; pr++)
               c1 += "        s" + S(pr) + "_" + S(q) + "[" + S(a) + "] = fma(t" + S(pr) + ", p, s" + S(pr) + "_" + S(q) + "[" + S(a) + "]);\n";
@@ -1204,8 +1219,14 @@ extern "C" __global__ void __launch_bounds__(64 * WPB) WPEU es_hoist_wave(Args A
     }
     pf_u = uu;
   };
-  prefetch((long long)blockIdx.x * WPB + wave);
-  for (long long u = (long long)blockIdx.x * WPB + wave; u < units; u += (long long)gridDim.x * WPB) {
+  // XCD-aware unit order: blocks are dealt round-robin over the 8 XCDs, so the units of one round are split into 8
+  // contiguous ranges, one per XCD -- a task's family units (one site's penetrance rows) stay in one XCD's L2
+  const long long stride = (long long)gridDim.x * WPB;
+  const long long u_first = (XCD && gridDim.x % 8 == 0)
+      ? (long long)(blockIdx.x % 8) * (gridDim.x / 8) * WPB + (long long)(blockIdx.x / 8) * WPB + wave
+      : (long long)blockIdx.x * WPB + wave;
+  prefetch(u_first);
+  for (long long u = u_first; u < units; u += stride) {
     const int uq = (int)(u / nfu), k0 = (int)(u - (long long)uq * nfu);
     // (PAIR: k is this half's slot -- per lane; ks the pair's first slot, whose shape both halves share)
     const int k = PAIR ? A.pair_k[2 * k0 + half] : k0, ks = PAIR ? __builtin_amdgcn_readfirstlane(A.pair_k[2 * k0]) : k0;
@@ -1236,7 +1257,7 @@ extern "C" __global__ void __launch_bounds__(64 * WPB) WPEU es_hoist_wave(Args A
         for (int r = 0; r < (NPF > 0 ? NPF : 1); r++)
           if (lane + LPF * r < 10 * nn) PEN[lane + LPF * r] = lk[pb[r]];
         wave_sync();
-        prefetch(u + (long long)gridDim.x * WPB);
+        prefetch(u + stride);
       } else {
         switch (sig) {
 PENS        }
@@ -1286,6 +1307,7 @@ PARTS2      }
   for (size_t at; (at = k.find("NPF")) != std::string::npos;) k.replace(at, 3, std::to_string(npf));
   for (size_t at; (at = k.find("LPF")) != std::string::npos;) k.replace(at, 3, std::to_string(g_wl));
   for (size_t at; (at = k.find("PAIR")) != std::string::npos;) k.replace(at, 4, g_pair ? "true" : "false");
+  k.replace(k.find("XCD &&"), 3, g_xcd ? "true" : "false");
   {
     std::string cases;
     for (size_t i = 0; i < pens.size(); i++) cases += "        case " + std::to_string(i) + ": " + pens[i] + "(pl, A.np, p0, lk, PEN, lane); break;\n";
@@ -1380,6 +1402,10 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
   const char* epr = getenv("PM_ES_PAIR");
   g_pair = denovo != 0 && !(epr && epr[0] == '0') && pps == 3;
   g_wl = g_pair ? 32 : 64;
+  const char* epp = getenv("PM_ES_PENP");
+  g_no_penp = epp && epp[0] == '0';
+  const char* exd = getenv("PM_ES_XCD");
+  g_xcd = !(exd && exd[0] == '0');
   if (g_pair) { g_regp = 0; g_regf = false; g_tr_regs = false; }   // (cross-lane reads by LDS only in pair mode)
   int ws = 1;
   std::vector<std::pair<int, int>> order;   // (shape, index into fams)
@@ -1454,8 +1480,12 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
     const int tables = (256 + 6 * 27) * 8;
     // (one wave per SIMD: the occupancy comes from blocks per CU, build() asks the runtime for them)
     const int slice = (g_pair ? 2 : 1) * (ws + pensz) * 8;   // (a pair's two family slices per wave)
-    out->wpb = std::max(1, std::min(4, (64 * 1024 - tables) / slice));
-    if ((64 * 1024 - tables) / slice < 1) out->wpb = 0;   // a family too large for one slice: the engine's generic kernel
+    // (at most 4: one wave per SIMD and block; measured on config 4 --denovo, 4 beat 1, 2, 5 and 6 even where those
+    // gave more waves per CU -- profiles/r05k_ab_es_wpb.txt)
+    const int fit = (64 * 1024 - tables) / slice;
+    out->wpb = std::max(0, std::min(4, fit));
+    if (const char* ew = getenv("PM_ES_WPB")) out->wpb = std::max(1, std::min(fit, atoi(ew)));
+    // (wpb 0: a family too large for one slice -- the engine's generic kernel)
     std::string wk = gen_wave_kernel(wave_names, part_names, pen_names, shape_ns, pps, ws, pensz, std::max(1, out->wpb), denovo == 2);
     const size_t at = wk.find("extern \"C\"");   // device helpers first, then the family functions, then the kernel
     src += wk.substr(0, at);
@@ -1530,6 +1560,7 @@ bool build(int device, int chrom, const std::vector<Family>& fams, const double 
     int nb = 0;
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, out->fn, 64 * out->wpb, 0) != hipSuccess) nb = 0;
     out->blocks_per_cu = nb;
+    if (getenv("PM_JIT_LAYOUT")) fprintf(stderr, "es_hoist_wave: wpb %d ws %d blocks/CU %d\n", out->wpb, out->ws, nb);
   }
   out->compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return true;

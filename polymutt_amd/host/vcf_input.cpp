@@ -14,9 +14,12 @@
 #include <string>
 #include <thread>
 #include <vector>
+#include <fcntl.h>
 #include <unistd.h>
 #include <chrono>
 #include <memory>
+#include <mutex>
+#include <exception>
 #include "ingest.h"
 #include "vcf_fmt.h"
 
@@ -72,14 +75,60 @@ struct LineReader {   // plain or gzip text, lines of any length; offsets are in
 
 // Whole lines of the stream, read in large blocks (one gzread per block instead of gzgets + append per line): a chunk's
 // lines are pointers into the block, valid until the next chunk() call (which compacts and refills first).
+// An uncompressed file is read with pread, in pieces of >= 4 MB on the pool's threads (the page-cache copy is the
+// cost; one thread moved ~7 GB/s).
 struct BlockReader {
   gzFile fh;
+  int fd = -1;
+  TaskPool* pool;
   std::vector<char> buf = std::vector<char>((size_t)64 << 20);
   size_t beg = 0, end = 0;
   int64_t base;   // uncompressed offset of buf[0]
   bool zeof = false;
   struct Line { const char* p; size_t n; int64_t off; };
-  explicit BlockReader(LineReader& lr) : fh(lr.fh), base(lr.tell()) {}
+  BlockReader(LineReader& lr, TaskPool* tp) : fh(lr.fh), pool(tp), base(lr.tell()) {
+    if (gzdirect(fh) && !getenv("PM_VCF_GZREAD")) {
+      fd = ::open(lr.path.c_str(), O_RDONLY);
+      if (fd >= 0) posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);
+    }
+  }
+  ~BlockReader() { if (fd >= 0) ::close(fd); }
+  void fill() {   // buf[end, size) from the stream; zeof at its end
+    if (fd < 0) {
+      while (!zeof && end < buf.size()) {
+        const int r = gzread(fh, buf.data() + end, (unsigned)std::min<size_t>(buf.size() - end, (size_t)1 << 30));
+        if (r < 0) throw FatalError("VCF input: read error\n");
+        if (r == 0) zeof = true;
+        end += (size_t)r;
+      }
+      return;
+    }
+    const size_t want = buf.size() - end;
+    const int64_t off0 = base + (int64_t)end;
+    const int np = std::max(1, std::min(pool ? pool->threads() : 1, (int)(want >> 22)));
+    std::vector<size_t> got(np, 0);
+    std::vector<char> bad(np, 0);
+    auto piece = [&](int i) {
+      const size_t b = want * i / np, e = want * (i + 1) / np;
+      size_t g = 0;
+      while (b + g < e) {
+        const ssize_t r = pread(fd, buf.data() + end + b + g, e - b - g, (off_t)(off0 + (int64_t)(b + g)));
+        if (r < 0) { bad[i] = 1; break; }
+        if (r == 0) break;
+        g += (size_t)r;
+      }
+      got[i] = g;
+    };
+    if (np > 1) pool->run(np, piece);
+    else piece(0);
+    size_t total = 0;
+    for (int i = 0; i < np; i++) {
+      if (bad[i]) throw FatalError("VCF input: read error\n");
+      total += got[i];
+      if (got[i] < want * (i + 1) / np - want * i / np) { zeof = true; break; }   // (a regular file reads short only at its end)
+    }
+    end += total;
+  }
   // Up to `max` whole lines ('\n' and a trailing '\r' removed); fewer when the block ends (the next call continues).
   void chunk(int max, std::vector<Line>& out) {
     out.clear();
@@ -90,12 +139,7 @@ struct BlockReader {
       beg = 0;
     }
     for (;;) {
-      while (!zeof && end < buf.size()) {
-        const int r = gzread(fh, buf.data() + end, (unsigned)std::min<size_t>(buf.size() - end, (size_t)1 << 30));
-        if (r < 0) throw FatalError("VCF input: read error\n");
-        if (r == 0) zeof = true;
-        end += (size_t)r;
-      }
+      if (!zeof && end < buf.size()) fill();
       size_t at = beg;
       while ((int)out.size() < max && at < end) {
         const char* nl = (const char*)memchr(buf.data() + at, '\n', end - at);
@@ -160,6 +204,25 @@ int allele2int(const std::string& a) {   // FamilyLikelihoodSeq_VCF::Allele2Int 
   return 0;
 }
 
+// atoi(s) (the field runs to the next ':' / tab / end of line): plain digits without a call, anything else atoi itself
+inline int atoi_fast(const char* s) {
+  int v = 0;
+  const char* q = s;
+  while (*q >= '0' && *q <= '9' && q - s < 9) v = v * 10 + (*q++ - '0');
+  if (q > s && !(*q >= '0' && *q <= '9')) return v;
+  return atoi(s);
+}
+
+inline char* put_int_buf(char* w, int v) {   // fmt_int into a buffer
+  char b[16];
+  int n = 0;
+  unsigned u = v < 0 ? 0u - (unsigned)v : (unsigned)v;
+  do { b[n++] = char('0' + u % 10); u /= 10; } while (u);
+  if (v < 0) *w++ = '-';
+  while (n) *w++ = b[--n];
+  return w;
+}
+
 int gi(int b1, int b2) { return b1 < b2 ? (b1 - 1) * (10 - b1) / 2 + (b2 - b1) : (b2 - 1) * (10 - b2) / 2 + (b1 - b2); }
 bool is_ts(int a1, int a2) { return (a1 == 1 && a2 == 3) || (a1 == 2 && a2 == 4); }   // PedVCF::isTs (:25-28)
 
@@ -187,13 +250,6 @@ struct State {            // what FamilyLikelihoodSeq_VCF holds between records 
   int a_ref = 0;                     // allele of the label convention (always allele1 in this path)
 };
 
-std::string label_text(const pm_geno_call& c) {   // GetBestGenoLabel_vcfv4 (NucFamGenotypeLikelihood.cpp:1590-1608)
-  static const char* dip[3] = {"0/0", "0/1", "1/1"};
-  static const char* hap[3] = {"0", "ERROR", "1"};
-  if (c.label == PM_LBL_DOT) return ".";
-  const int b = c.best < 0 || c.best > 2 ? 0 : c.best;
-  return c.label == PM_LBL_VCF_HAPLOID ? hap[b] : dip[b];
-}
 
 }  // namespace
 
@@ -266,6 +322,10 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
     if (it != pid2person.end()) { col_person[i] = it->second; included.push_back(samples[i]); }
   }
 
+  std::vector<std::pair<int, int>> inc_cols;   // (VCF column, person) of the included samples, in VCF order
+  for (size_t i = 0; i < samples.size(); i++)
+    if (col_person[i] >= 0) inc_cols.push_back({(int)i, col_person[i]});
+
   auto write_header = [&](FILE* out) {
     std::string header = "#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT";
     for (auto& s : included) header += "\t" + s;
@@ -297,28 +357,40 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
   const double tstv = 2.0, prior_ts = tstv / (tstv + 1), prior_tv = 0.5 / (tstv + 1);
 
   const int B = std::max(1, opt.batch);
-  // the batch's PL rows in page-locked memory where the evaluator offers it (an asynchronous, faster host-to-device copy)
-  struct HostBuf {
-    SiteEvaluator& e; uint8_t* p;
-    ~HostBuf() { e.host_free(p); }
-    uint8_t* data() const { return p; }
-  } pl{eval, (uint8_t*)eval.host_alloc((size_t)B * np * 10)};
-  if (!pl.p) throw FatalError("out of host memory\n");
-  std::vector<uint8_t> ref(B);
+  // Two batches: the main thread reads, classifies and parses records into one while the flusher thread runs the
+  // engine on the other, formats its records and hands their text to the writer thread.  A batch's PL rows are in
+  // page-locked memory where the evaluator offers it (an asynchronous, faster host-to-device copy); pend: its records
+  // awaiting output, in file order; nb: its computed records.
+  struct BatchBuf {
+    SiteEvaluator& e;
+    uint8_t* pl;
+    std::vector<uint8_t> ref;
+    std::vector<pm_site_result> res;
+    std::unique_ptr<pm_geno_call[]> calls;   // (written by the engine before any read: not value-initialised)
+    std::vector<Pending*> pend;
+    int nb = 0;
+    BatchBuf(SiteEvaluator& ev, int b, int n)
+        : e(ev), pl((uint8_t*)ev.host_alloc((size_t)b * n * 10)), ref(b), res(b), calls(new pm_geno_call[(size_t)b * n]) {}
+    ~BatchBuf() { e.host_free(pl); }
+  };
+  BatchBuf bb0(eval, B, np), bb1(eval, B, np);
+  BatchBuf* const bbs[2] = {&bb0, &bb1};
+  if (!bb0.pl || !bb1.pl) throw FatalError("out of host memory\n");
+  int cb = 0;   // the batch the main thread fills
   std::vector<uint32_t> dm((size_t)B * np, 0);
-  std::vector<pm_site_result> res(B);
-  std::vector<pm_geno_call> calls((size_t)B * np);
   // records are recycled through a free list (their 10-100 KB line and column buffers are reused, not reallocated and
-  // first-touched for every record); pend: the records awaiting output, in file order
+  // first-touched for every record); the flusher returns a batch's records to it
   std::vector<std::unique_ptr<Pending>> store;
-  std::vector<Pending*> freel, pend;
+  std::vector<Pending*> freel;
+  std::mutex free_mu;
   auto take = [&]() -> Pending* {
+    std::lock_guard<std::mutex> lk(free_mu);
     if (freel.empty()) { store.emplace_back(new Pending); return store.back().get(); }
     Pending* r = freel.back();
     freel.pop_back();
     return r;
   };
-  int nb = 0, cur_chrom = -1, n_samples_with_data = 0, bad_allele = 0;
+  int cur_chrom = -1, n_samples_with_data = 0, bad_allele = 0;
   FormatState fs;
   bool first = R == 0;   // FillPenetrance's first-record banner (:270-282): rank 0 owns the file's first record
   bool computed_any = false;
@@ -351,54 +423,85 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
     S.calls = C;
     return S;
   };
-  // OutputVCF (FamilyLikelihoodSeq_VCF.cpp:412-521): one record's text appended to `out` (no shared state: the
-  // records of a batch are formatted in parallel)
+  // OutputVCF (FamilyLikelihoodSeq_VCF.cpp:412-521): one record's text into `out` (no shared state: the records of a
+  // batch are formatted in parallel).  One pass over each sample's column finds both its DP and its PL / GL subfield
+  // (VCFIndividual::get: missing when absent or empty), then the text is written straight into `out`, sized to a bound
+  // first (each sample adds at most 17 characters to the input bytes it copies)
+  struct Fields { int db, de, pb, pe; };   // the DP and PL / GL subfields' spans (b < 0: missing)
+  // GetBestGenoLabel_vcfv4 (NucFamGenotypeLikelihood.cpp:1590-1608)
+  static const char* kDip[3] = {"0/0", "0/1", "1/1"};
+  static const char* kHap[3] = {"0", "ERROR", "1"};
   auto format_record = [&](std::string& out, const Pending& r, const RecState& S) {
+    thread_local std::vector<Fields> fv;
     const std::string& L = r.line;
+    const char* lp = L.data();
+    const int ia = r.dp_idx > 0 ? r.dp_idx : -1, ib = fs.PL_idx > 0 ? fs.PL_idx : fs.GL_idx, kmax = std::max(ia, ib);
+    const size_t ns = inc_cols.size();
+    fv.resize(ns);
     int AC = 0, totalDepth = 0;
-    bool missing = false;
-    Span f;
-    for (size_t i = 0; i < samples.size(); i++) {
-      if (col_person[i] < 0) continue;
-      AC += S.calls[col_person[i]].best;
-      int dp = 0;
-      if (r.dp_idx > 0) {
-        missing = get_field(L, r.cols[9 + i], r.dp_idx, f);
-        dp = missing ? 0 : atoi(L.c_str() + f.b);
+    for (size_t s = 0; s < ns; s++) {
+      const Span col = r.cols[9 + inc_cols[s].first];
+      AC += S.calls[inc_cols[s].second].best;
+      Fields F{-1, -1, -1, -1};
+      int k = 0, b = col.b;
+      for (int p = col.b; k <= kmax; p++) {
+        const bool end = p == col.e;
+        if (end || lp[p] == ':') {
+          if (k == ia && p > b) { F.db = b; F.de = p; }
+          if (k == ib && p > b) { F.pb = b; F.pe = p; }
+          k++;
+          b = p + 1;
+          if (end) break;
+        }
       }
-      if (missing) continue;
-      totalDepth += dp;
+      fv[s] = F;
+      if (F.db >= 0) totalDepth += atoi_fast(lp + F.db);
     }
-    auto fld = [&](int k) { return L.substr(r.cols[k].b, r.cols[k].e - r.cols[k].b); };
-    char head[256];
-    out += fld(0); out += '\t'; out += fld(1); out += '\t'; out += fld(2); out += '\t'; out += fld(3); out += '\t';
-    out += fld(4);
-    snprintf(head, sizeof(head), "\t%.2f\t", S.qual);
-    out += head;
-    out += fld(6);
-    snprintf(head, sizeof(head), "\tAF=%.2f;AC=%d;DP=%d\t%s", 1 - S.min, AC, totalDepth, fs.PL_idx > 0 ? "GT:GQ:DP:PL" : "GT:GQ:DP:GL");
-    out += head;
-    for (size_t i = 0; i < samples.size(); i++) {
-      const int p = col_person[i];
-      if (p < 0) continue;
-      const pm_geno_call& c = S.calls[p];
-      const std::string lab = label_text(c);
-      out += '\t';
-      out += (c.gq > 0 || lab == ".") ? lab : std::string("./.");
-      out += ':';
-      fmt_int(out, (int)c.gq);
-      out += ':';
-      if (r.dp_idx > 0) {
-        missing = get_field(L, r.cols[9 + i], r.dp_idx, f);
-        if (missing) out += '.';
-        else out.append(L, f.b, f.e - f.b);
-      } else out += missing ? "." : ".";
-      out += ':';
-      missing = get_field(L, r.cols[9 + i], fs.PL_idx > 0 ? fs.PL_idx : fs.GL_idx, f);
-      if (missing) out += '.';
-      else out.append(L, f.b, f.e - f.b);
+    out.resize(L.size() + 17 * ns + 1024);
+    char* w = &out[0];
+    auto put = [&](const char* p, size_t n) { memcpy(w, p, n); w += n; };
+    auto fld = [&](int k) { put(lp + r.cols[k].b, (size_t)(r.cols[k].e - r.cols[k].b)); };
+    for (int k = 0; k < 5; k++) {
+      fld(k);
+      if (k < 4) *w++ = '\t';
     }
-    out += '\n';
+    char head[512];
+    auto putf = [&](int n) {   // (a text longer than head -- a QUAL of hundreds of digits -- grows the bound)
+      if (n < (int)sizeof(head)) { put(head, (size_t)n); return; }
+      const size_t at = (size_t)(w - &out[0]);
+      out.resize(out.size() + (size_t)n);
+      w = &out[0] + at;
+    };
+    int hn = snprintf(head, sizeof(head), "\t%.2f\t", S.qual);
+    if (hn >= (int)sizeof(head)) { putf(hn); w += snprintf(w, (size_t)hn + 1, "\t%.2f\t", S.qual); } else putf(hn);
+    fld(6);
+    const char* fmt_s = fs.PL_idx > 0 ? "GT:GQ:DP:PL" : "GT:GQ:DP:GL";
+    hn = snprintf(head, sizeof(head), "\tAF=%.2f;AC=%d;DP=%d\t%s", 1 - S.min, AC, totalDepth, fmt_s);
+    if (hn >= (int)sizeof(head)) { putf(hn); w += snprintf(w, (size_t)hn + 1, "\tAF=%.2f;AC=%d;DP=%d\t%s", 1 - S.min, AC, totalDepth, fmt_s); }
+    else putf(hn);
+    for (size_t s = 0; s < ns; s++) {
+      const pm_geno_call& c = S.calls[inc_cols[s].second];
+      const Fields& F = fv[s];
+      const char* lab;
+      if (c.label == PM_LBL_DOT) lab = ".";
+      else if (c.gq <= 0) lab = "./.";
+      else {
+        const int bb = c.best < 0 || c.best > 2 ? 0 : c.best;
+        lab = c.label == PM_LBL_VCF_HAPLOID ? kHap[bb] : kDip[bb];
+      }
+      *w++ = '\t';
+      put(lab, strlen(lab));
+      *w++ = ':';
+      w = put_int_buf(w, (int)c.gq);
+      *w++ = ':';
+      if (F.db >= 0) put(lp + F.db, (size_t)(F.de - F.db));
+      else *w++ = '.';
+      *w++ = ':';
+      if (F.pb >= 0) put(lp + F.pb, (size_t)(F.pe - F.pb));
+      else *w++ = '.';
+    }
+    *w++ = '\n';
+    out.resize((size_t)(w - &out[0]));
   };
   // the lead records of a shard, printed with the carried state, one at a time
   auto write_record = [&](FILE* fo, const Pending& r) {
@@ -410,22 +513,43 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
 
   TaskPool pool(std::max(1, std::min(16, opt.io_threads > 0 ? opt.io_threads : (int)std::thread::hardware_concurrency())));
   // PM_TIMING=1: wall seconds per stage on stderr at the end (read, split + classify, PL parse, engine, format, write)
-  double tm[6] = {0, 0, 0, 0, 0, 0};
+  // (tm[6]: the whole record loop, wall)
   auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  double tm[8] = {0, 0, 0, 0, 0, 0, now(), 0};
   struct TimingOut {
     double* t;
     ~TimingOut() {
       if (getenv("PM_TIMING"))
-        fprintf(stderr, "PM_TIMING vcf input: read %.3f s, classify %.3f s, parse %.3f s, engine %.3f s, format %.3f s, write %.3f s\n",
-                t[0], t[1], t[2], t[3], t[4], t[5]);
+        fprintf(stderr, "PM_TIMING vcf input: read %.3f s, classify %.3f s, parse %.3f s, engine %.3f s, format %.3f s, write %.3f s, "
+                "loop %.3f s, flush wait %.3f s\n", t[0], t[1], t[2], t[3], t[4], t[5], t[6], t[7]);
     }
   } timing_out{tm};
-  std::vector<std::string> texts;
+  // one writer thread: fwrite of a formatted batch, in order, overlapped with the work on the next batch
+  struct Writer {
+    std::thread th;
+    bool fail = false;
+    void start(FILE* f, const std::vector<std::string>* t, int n) {
+      th = std::thread([this, f, t, n] {
+        for (int k = 0; k < n && !fail; k++)
+          if (fwrite((*t)[k].data(), 1, (*t)[k].size(), f) != (*t)[k].size()) fail = true;
+      });
+    }
+    void wait() {
+      if (th.joinable()) th.join();
+      if (fail) throw FatalError("Write to the output VCF failed\n");
+    }
+    ~Writer() { if (th.joinable()) th.join(); }
+  } writer;
+  std::vector<std::string> texts[2];
+  int tcur = 0;
   std::vector<RecState> states;
-  auto flush = [&]() {
+  TaskPool fpool(pool.threads());   // (the flusher's: the main thread's pool parses the next batch meanwhile)
+  auto process = [&](BatchBuf& bb) {   // the flusher's work on one batch, in batch order
+    std::vector<Pending*>& pend = bb.pend;
+    const pm_geno_call* calls = bb.calls.get();
     int rows = 0;
     double t0 = now();
-    if (nb > 0) eval.run(nb, pl.data(), dm.data(), ref.data(), res.data(), calls.data(), &rows);
+    if (bb.nb > 0) eval.run(bb.nb, bb.pl, dm.data(), bb.ref.data(), bb.res.data(), bb.calls.get(), &rows);
     double t1 = now();
     tm[3] += t1 - t0;
     // the state each record prints with (sequential: a record without data takes the last computed one's)
@@ -433,49 +557,50 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
     RecState cur{st.qual, st.min, st.calls.data()};
     for (size_t k = 0; k < pend.size(); k++) {
       const Pending& r = *pend[k];
-      if (r.computed) cur = fresh_state(r, &res[r.slot], calls.data() + (size_t)res[r.slot].call_row * np);
+      if (r.computed) cur = fresh_state(r, &bb.res[r.slot], calls + (size_t)bb.res[r.slot].call_row * np);
       states[k] = cur;
     }
-    if (texts.size() < pend.size()) texts.resize(pend.size());
-    pool.run((int)pend.size(), [&](int k) { texts[k].clear(); format_record(texts[k], *pend[k], states[k]); });
+    std::vector<std::string>& T = texts[tcur];
+    if (T.size() < pend.size()) T.resize(pend.size());
+    fpool.run((int)pend.size(), [&](int k) { format_record(T[k], *pend[k], states[k]); });
     const double t2 = now();
     tm[4] += t2 - t1;
-    {   // the batch's records written in parallel, each group of records at its own offset (pwrite), in file order
-      const int nr = (int)pend.size();
-      std::vector<int64_t> at(nr + 1, 0);
-      for (int k = 0; k < nr; k++) at[k + 1] = at[k] + (int64_t)texts[k].size();
-      fflush(out);
-      const int64_t base = (int64_t)ftello(out);
-      const int fd = fileno(out);
-      const int ng = std::min(nr, 4 * pool.threads());
-      std::vector<char> werr(std::max(ng, 1), 0);
-      if (nr > 0 && base >= 0 && at[nr] > ((int64_t)1 << 20)) {
-        pool.run(ng, [&](int g) {
-          for (int k = (int)((int64_t)nr * g / ng); k < (int)((int64_t)nr * (g + 1) / ng); k++) {
-            const char* p = texts[k].data();
-            size_t left = texts[k].size();
-            int64_t off = base + at[k];
-            while (left > 0) {
-              const ssize_t w = pwrite(fd, p, left, (off_t)off);
-              if (w <= 0) { werr[g] = 1; return; }
-              p += w; left -= (size_t)w; off += w;
-            }
-          }
-        });
-        for (char e : werr)
-          if (e) throw FatalError("Write to the output VCF failed\n");
-        if (fseeko(out, (off_t)(base + at[nr]), SEEK_SET) != 0) throw FatalError("Write to the output VCF failed\n");
-      } else
-        for (int k = 0; k < nr; k++) fwrite(texts[k].data(), 1, texts[k].size(), out);
-    }
-    tm[5] += now() - t2;
+    // the batch's text goes out on the writer thread while the next batch is read, parsed and computed; the
+    // previous batch's write finishes first (file order), then the buffers alternate
+    writer.wait();
+    tm[5] += now() - t2;   // (write: the time this thread waited for the writer)
+    writer.start(out, &texts[tcur], (int)pend.size());
+    tcur ^= 1;
     if (!pend.empty()) {   // the last state carries into the next batch
       st.qual = cur.qual; st.min = cur.min;
       if (cur.calls != st.calls.data()) std::copy(cur.calls, cur.calls + np, st.calls.begin());
     }
-    for (Pending* r : pend) freel.push_back(r);
+    {
+      std::lock_guard<std::mutex> lk(free_mu);
+      for (Pending* r : pend) freel.push_back(r);
+    }
     pend.clear();
-    nb = 0;
+    bb.nb = 0;
+  };
+  std::thread flusher;
+  std::exception_ptr ferr;
+  auto drain = [&]() {   // the flusher's batch done (its errors raised here)
+    const double tw = now();
+    if (flusher.joinable()) flusher.join();
+    tm[7] += now() - tw;
+    if (ferr) std::rethrow_exception(ferr);
+  };
+  struct JoinAtExit {
+    std::thread& t;
+    ~JoinAtExit() { if (t.joinable()) t.join(); }
+  } join_flusher{flusher};
+  auto flush = [&]() {   // the filled batch to the flusher; the main thread goes on with the other (already drained)
+    drain();
+    BatchBuf* bb = bbs[cb];
+    flusher = std::thread([&, bb] {
+      try { process(*bb); } catch (...) { ferr = std::current_exception(); }
+    });
+    cb ^= 1;
   };
 
   // parses a record's columns and its biallelic / allele / FORMAT-index bookkeeping (:296-324); false: not output.
@@ -612,7 +737,7 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
     withdata[k] = wd;
   };
   bool eof = false;
-  BlockReader br(in);
+  BlockReader br(in, &pool);
   std::vector<BlockReader::Line> lines;
   std::vector<char> keep(CH);
   while (!eof) {
@@ -673,28 +798,38 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
           fprintf(lead, "%d\t%s\n", r.dp_idx, r.line.c_str());   // (with its DP index snapshot)
           n_lead++;
         } else {
-          pend.push_back(chunk[k]);
+          bbs[cb]->pend.push_back(chunk[k]);
           chunk[k] = nullptr;
         }
         continue;
       }
       computed_any = true;
+      BatchBuf& bb = *bbs[cb];
       if (cls != cur_chrom) {
-        if (nb > 0 || !pend.empty()) flush();
+        if (bb.nb > 0 || !bb.pend.empty()) flush();
+        drain();   // (the engine's section changes: no batch of the old one in flight)
         eval.begin_section(cls);
         cur_chrom = cls;
       }
-      memcpy(pl.data() + (size_t)nb * np * 10, rows.data() + (size_t)k * np * 10, (size_t)np * 10);
+      BatchBuf& bc = *bbs[cb];
+      memcpy(bc.pl + (size_t)bc.nb * np * 10, rows.data() + (size_t)k * np * 10, (size_t)np * 10);
       r.computed = true;
-      r.slot = nb;
-      ref[nb] = (uint8_t)(r.a1 | (r.a2 << 4));
-      nb++;
-      pend.push_back(chunk[k]);
+      r.slot = bc.nb;
+      bc.ref[bc.nb] = (uint8_t)(r.a1 | (r.a2 << 4));
+      bc.nb++;
+      bc.pend.push_back(chunk[k]);
       chunk[k] = nullptr;
-      if (nb == B) flush();
+      if (bc.nb == B) flush();
     }
   }
   flush();
+  drain();
+  {
+    const double tw = now();
+    writer.wait();
+    tm[5] += now() - tw;
+  }
+  tm[6] = now() - tm[6];
   if (!sharded) {
     fclose(out);
     if (bad_allele) fprintf(stderr, "%d biallelic records with non-ACGT alleles were skipped\n", bad_allele);

@@ -48,7 +48,7 @@ int main(int argc, char** argv) {
     pmjit::Kernel K;
     const std::string src = pmjit::generate(cls, fams, kTBA, &K, dn);
     if (!emit.empty() && cls == 0) {
-      FILE* fh = fopen((dn ? emit + ".dn" : emit).c_str(), "w");
+      FILE* fh = fopen((dn ? emit + ".dn" + std::to_string(dn) : emit).c_str(), "w");
       if (fh) { fputs(src.c_str(), fh); fclose(fh); }
     }
     std::vector<char> code;
@@ -56,7 +56,7 @@ int main(int argc, char** argv) {
     const auto t0 = std::chrono::steady_clock::now();
     if (!pmjit::compile(src, &code, &err)) { fprintf(stderr, "class %d: %s\n", cls, err.c_str()); return 1; }
     if (!emit.empty() && cls == 0) {   // the code object too (register and LDS use: llvm-readelf --notes)
-      FILE* fh = fopen(((dn ? emit + ".dn" : emit) + ".co").c_str(), "wb");
+      FILE* fh = fopen(((dn ? emit + ".dn" + std::to_string(dn) : emit) + ".co").c_str(), "wb");
       if (fh) { fwrite(code.data(), 1, code.size(), fh); fclose(fh); }
     }
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

@@ -38,6 +38,14 @@ def timing_fields(stderr):
     m = re.search(r"PM_TIMING ingest ([\d.]+) s, engine ([\d.]+) s, vcf ([\d.]+) s", stderr)
     if m:
         out = {"ingest_busy_s": float(m.group(1)), "engine_stage_busy_s": float(m.group(2)), "vcf_busy_s": float(m.group(3))}
+    m = re.search(r"PM_TIMING vcf input: read ([\d.]+) s, classify ([\d.]+) s, parse ([\d.]+) s, engine ([\d.]+) s, "
+                  r"format ([\d.]+) s, write ([\d.]+) s", stderr)
+    if m:
+        for k, v in zip(("read", "classify", "parse", "engine", "format", "write"), m.groups()):
+            out["vcf_" + k + "_s"] = float(v)
+    m = re.search(r"PM_TIMING open inputs ([\d.]+) s", stderr)
+    if m:
+        out["open_inputs_s"] = float(m.group(1))
     m = re.search(r"PM_TIMING engine create ([\d.]+) s", stderr)
     if m:
         out["engine_create_s"] = float(m.group(1))
@@ -106,6 +114,7 @@ def main():
     ap.add_argument("--vcf-families", type=int, default=2000)
     ap.add_argument("--keep", default=None, help="work directory to keep (default: a temporary one, removed)")
     ap.add_argument("--glf", action="store_true", help="also time the CLI on the GLF files themselves (the reference's input)")
+    ap.add_argument("--vcf-only", action="store_true", help="only the --in_vcf timing (no GLF / block runs)")
     ap.add_argument("--vcf-small", type=int, default=2000, help="--in_vcf start-up run: records (subtracted for the steady rate)")
     a = ap.parse_args()
     tmp = a.keep or tempfile.mkdtemp(prefix="pm_cli_", dir=os.environ.get("TMPDIR", "/tmp"))
@@ -114,53 +123,54 @@ def main():
     try:
         base = [pm.BIN_PATH, "-p", "test.ped", "-d", "test.dat"]
         extra = ["--denovo"] if a.denovo else []
-        t0 = time.perf_counter()
-        pm.synth_write_dataset(tmp, "quad", a.families, a.sites, 7)
-        out["seconds_synth_glf"] = time.perf_counter() - t0
-        out["seconds_glf2blocks"], _ = run_cli(base + ["-g", "test.gif", "--glf2blocks", "in.pmb"], tmp)
-        out["pmb_bytes"] = os.path.getsize(os.path.join(tmp, "in.pmb"))
-        small = os.path.join(tmp, "small")
-        pm.synth_write_dataset(small, "quad", a.families, 64, 7)
-        run_cli(base + ["-g", "test.gif", "--glf2blocks", "small.pmb"], small)
-        ref_body = None
-        for e in a.engines:
-            for b in a.batch:
-                # start-up (a 64-site run) and the full run, each the best of 3: single start-up samples varied
-                # 0.48-0.85 s on one box, which made their difference meaningless
-                t_small = min(run_cli(base + ["--in_blocks", "small.pmb", "--out_vcf", "s.vcf", "--engines", str(e), "--batch", str(b)] + extra,
-                                      small)[0] for _ in range(3))
-                runs = [run_cli(base + ["--in_blocks", "in.pmb", "--out_vcf", "o.vcf", "--engines", str(e), "--batch", str(b)] + extra, tmp)
-                        for _ in range(3)]
-                dt, r = min(runs, key=lambda x: x[0])
-                bd = body(os.path.join(tmp, "o.vcf"))
-                if ref_body is None:
-                    ref_body = bd
-                rec = {"engines": e, "batch": b, "seconds": dt, "startup_seconds": t_small, "sites_per_s": a.sites / dt,
-                       "sites_per_s_past_startup": a.sites / max(1e-9, dt - t_small), "records": len(bd) - 1,
-                       "vcf_identical_to_first": bd == ref_body}
-                rec.update(timing_fields(r.stderr))
-                out["runs"].append(rec)
-                print(json.dumps(rec), file=sys.stderr, flush=True)
-        if a.glf:   # the drop-in on GLF: decode, merge and fill in the ingest thread; start-up from the 64-site GLF set
+        if not a.vcf_only:
+            t0 = time.perf_counter()
+            pm.synth_write_dataset(tmp, "quad", a.families, a.sites, 7)
+            out["seconds_synth_glf"] = time.perf_counter() - t0
+            out["seconds_glf2blocks"], _ = run_cli(base + ["-g", "test.gif", "--glf2blocks", "in.pmb"], tmp)
+            out["pmb_bytes"] = os.path.getsize(os.path.join(tmp, "in.pmb"))
+            small = os.path.join(tmp, "small")
+            pm.synth_write_dataset(small, "quad", a.families, 64, 7)
+            run_cli(base + ["-g", "test.gif", "--glf2blocks", "small.pmb"], small)
+            ref_body = None
             for e in a.engines:
-                t_small = min(run_cli(base + ["-g", "test.gif", "--out_vcf", "s.vcf", "--engines", str(e)] + extra, small)[0]
-                              for _ in range(3))
-                runs = [run_cli(base + ["-g", "test.gif", "--out_vcf", "g.vcf", "--engines", str(e)] + extra, tmp) for _ in range(3)]
-                dt, r = min(runs, key=lambda x: x[0])
-                bd = body(os.path.join(tmp, "g.vcf"))
-                rec = {"input": "glf", "engines": e, "seconds": dt, "startup_seconds": t_small, "sites_per_s": a.sites / dt,
-                       "sites_per_s_past_startup": a.sites / max(1e-9, dt - t_small), "records": len(bd) - 1,
-                       "vcf_identical_to_blocks": ref_body is None or bd == ref_body}
-                rec.update(timing_fields(r.stderr))
-                m = re.search(r"PM_TIMING glf ingest: decode ([\d.]+) s, merge ([\d.]+) s, fill ([\d.]+) s", r.stderr)
-                if m:
-                    rec.update({"glf_decode_s": float(m.group(1)), "glf_merge_s": float(m.group(2)), "glf_fill_s": float(m.group(3))})
-                out.setdefault("glf_runs", []).append(rec)
-                print(json.dumps(rec), file=sys.stderr, flush=True)
-            out["glf_best"] = max(out["glf_runs"], key=lambda x: x["sites_per_s_past_startup"])
-        best = max(out["runs"], key=lambda x: x["sites_per_s_past_startup"])
-        out["best"] = {k: best[k] for k in ("engines", "batch", "sites_per_s", "sites_per_s_past_startup")}
-        out["all_vcf_identical"] = all(x["vcf_identical_to_first"] for x in out["runs"])
+                for b in a.batch:
+                    # start-up (a 64-site run) and the full run, each the best of 3: single start-up samples varied
+                    # 0.48-0.85 s on one box, which made their difference meaningless
+                    t_small = min(run_cli(base + ["--in_blocks", "small.pmb", "--out_vcf", "s.vcf", "--engines", str(e), "--batch", str(b)] + extra,
+                                          small)[0] for _ in range(3))
+                    runs = [run_cli(base + ["--in_blocks", "in.pmb", "--out_vcf", "o.vcf", "--engines", str(e), "--batch", str(b)] + extra, tmp)
+                            for _ in range(3)]
+                    dt, r = min(runs, key=lambda x: x[0])
+                    bd = body(os.path.join(tmp, "o.vcf"))
+                    if ref_body is None:
+                        ref_body = bd
+                    rec = {"engines": e, "batch": b, "seconds": dt, "startup_seconds": t_small, "sites_per_s": a.sites / dt,
+                           "sites_per_s_past_startup": a.sites / max(1e-9, dt - t_small), "records": len(bd) - 1,
+                           "vcf_identical_to_first": bd == ref_body}
+                    rec.update(timing_fields(r.stderr))
+                    out["runs"].append(rec)
+                    print(json.dumps(rec), file=sys.stderr, flush=True)
+            if a.glf:   # the drop-in on GLF: decode, merge and fill in the ingest thread; start-up from the 64-site GLF set
+                for e in a.engines:
+                    t_small = min(run_cli(base + ["-g", "test.gif", "--out_vcf", "s.vcf", "--engines", str(e)] + extra, small)[0]
+                                  for _ in range(3))
+                    runs = [run_cli(base + ["-g", "test.gif", "--out_vcf", "g.vcf", "--engines", str(e)] + extra, tmp) for _ in range(3)]
+                    dt, r = min(runs, key=lambda x: x[0])
+                    bd = body(os.path.join(tmp, "g.vcf"))
+                    rec = {"input": "glf", "engines": e, "seconds": dt, "startup_seconds": t_small, "sites_per_s": a.sites / dt,
+                           "sites_per_s_past_startup": a.sites / max(1e-9, dt - t_small), "records": len(bd) - 1,
+                           "vcf_identical_to_blocks": ref_body is None or bd == ref_body}
+                    rec.update(timing_fields(r.stderr))
+                    m = re.search(r"PM_TIMING glf ingest: decode ([\d.]+) s, merge ([\d.]+) s, fill ([\d.]+) s", r.stderr)
+                    if m:
+                        rec.update({"glf_decode_s": float(m.group(1)), "glf_merge_s": float(m.group(2)), "glf_fill_s": float(m.group(3))})
+                    out.setdefault("glf_runs", []).append(rec)
+                    print(json.dumps(rec), file=sys.stderr, flush=True)
+                out["glf_best"] = max(out["glf_runs"], key=lambda x: x["sites_per_s_past_startup"])
+            best = max(out["runs"], key=lambda x: x["sites_per_s_past_startup"])
+            out["best"] = {k: best[k] for k in ("engines", "batch", "sites_per_s", "sites_per_s_past_startup")}
+            out["all_vcf_identical"] = all(x["vcf_identical_to_first"] for x in out["runs"])
         if a.vcf_records:
             vd = os.path.join(tmp, "vcf")
             os.makedirs(vd, exist_ok=True)
@@ -168,7 +178,8 @@ def main():
             npers = write_vcf(pm, vd, a.vcf_families, a.vcf_records, 11)
             t_write = time.perf_counter() - t0
             vbytes = os.path.getsize(os.path.join(vd, "in.vcf"))
-            t_one = min(run_cli(base + ["--in_vcf", "in.vcf", "--out_vcf", "o.vcf"], vd)[0] for _ in range(3))
+            big = min((run_cli(base + ["--in_vcf", "in.vcf", "--out_vcf", "o.vcf"], vd) for _ in range(3)), key=lambda x: x[0])
+            t_one = big[0]
             # the steady rate: a small VCF of the same samples (the first records of in.vcf) timed the same way, subtracted
             with open(os.path.join(vd, "in.vcf")) as fi, open(os.path.join(vd, "small.vcf"), "w") as fo:
                 n = 0
@@ -178,14 +189,16 @@ def main():
                         if n > a.vcf_small:
                             break
                     fo.write(l)
-            t_small = min(run_cli(base + ["--in_vcf", "small.vcf", "--out_vcf", "s.vcf"], vd)[0] for _ in range(3))
+            small_r = min((run_cli(base + ["--in_vcf", "small.vcf", "--out_vcf", "s.vcf"], vd) for _ in range(3)), key=lambda x: x[0])
+            t_small = small_r[0]
             out["in_vcf"] = {"families": a.vcf_families, "samples": npers, "records": a.vcf_records, "vcf_bytes": vbytes,
                              "seconds_write": t_write, "seconds": t_one, "records_per_s": a.vcf_records / t_one,
                              "small_records": a.vcf_small, "small_seconds": t_small,
                              "records_per_s_steady": (a.vcf_records - a.vcf_small) / max(1e-9, t_one - t_small),
-                             "MB_per_s": vbytes / t_one / 1e6, "records_out": len(body(os.path.join(vd, "o.vcf"))) - 1}
+                             "MB_per_s": vbytes / t_one / 1e6, "records_out": len(body(os.path.join(vd, "o.vcf"))) - 1,
+                             "timing": timing_fields(big[1].stderr), "small_timing": timing_fields(small_r[1].stderr)}
         print(json.dumps(out, indent=1), flush=True)
-        return 0 if out["all_vcf_identical"] else 1
+        return 0 if out.get("all_vcf_identical", True) else 1
     finally:
         if not a.keep:
             shutil.rmtree(tmp, ignore_errors=True)
