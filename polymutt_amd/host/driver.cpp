@@ -520,6 +520,15 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, c
     Channel<Msg> toEngine, toWriter;
     std::atomic<bool> abort{false};
     std::exception_ptr perr, eerr, werr;
+    // PM_TIMING: wall clock of the pipeline (since the inputs were opened): first batch handed on, ingest done, end
+    double w_first = 0, w_ingest = 0;
+    struct WallReport {
+      double t0, &first, &ingest;
+      ~WallReport() {
+        if (getenv("PM_TIMING"))
+          fprintf(stderr, "PM_TIMING wall: first batch %.3f s, ingest done %.3f s, end %.3f s\n", first - t0, ingest - t0, now_s() - t0);
+      }
+    } wall_report{t_open0, w_first, w_ingest};
     std::thread producer([&] {
       try {
         size_t done = 0;
@@ -549,6 +558,7 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, c
             src.fill(rowOf.data(), b->pl, b->dm);
             t_ingest += now_s() - ti;
             if (b->n == b->cap) {
+              if (w_first == 0) w_first = now_s();
               toEngine.push({M_BATCH, b, label, chrom, 0, {}});
               b = freeq.pop();
               b->n = 0;
@@ -562,6 +572,7 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, c
       } catch (...) {
         perr = std::current_exception();
       }
+      w_ingest = now_s();
       toEngine.push({M_DONE, nullptr, "", 0, 0, {}});
     });
     std::thread writer([&] {

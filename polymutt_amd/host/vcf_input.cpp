@@ -132,14 +132,7 @@ struct BlockReader {
   // Up to `max` whole lines ('\n' and a trailing '\r' removed); fewer when the block ends (the next call continues).
   void chunk(int max, std::vector<Line>& out) {
     out.clear();
-    if (beg > 0) {   // compact and refill
-      memmove(buf.data(), buf.data() + beg, end - beg);
-      base += (int64_t)beg;
-      end -= beg;
-      beg = 0;
-    }
     for (;;) {
-      if (!zeof && end < buf.size()) fill();
       size_t at = beg;
       while ((int)out.size() < max && at < end) {
         const char* nl = (const char*)memchr(buf.data() + at, '\n', end - at);
@@ -155,7 +148,16 @@ struct BlockReader {
       }
       beg = at;
       if (!out.empty() || zeof) return;
-      buf.resize(buf.size() * 2);   // one line longer than the block
+      // no whole line left: the partial one moved to the front (only now: compacting on every call moved most of the
+      // block each time), then refilled; a line longer than the block grows it
+      if (beg > 0) {
+        memmove(buf.data(), buf.data() + beg, end - beg);
+        base += (int64_t)beg;
+        end -= beg;
+        beg = 0;
+      } else if (end == buf.size())
+        buf.resize(buf.size() * 2);
+      fill();
     }
   }
 };
@@ -361,23 +363,33 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
   // engine on the other, formats its records and hands their text to the writer thread.  A batch's PL rows are in
   // page-locked memory where the evaluator offers it (an asynchronous, faster host-to-device copy); pend: its records
   // awaiting output, in file order; nb: its computed records.
+  // The calls (B x np of them, 0.45 GB at 7000 samples) come back in page-locked memory too: from pageable memory
+  // that copy was most of the engine stage.
   struct BatchBuf {
     SiteEvaluator& e;
     uint8_t* pl;
+    pm_geno_call* calls;   // (written by the engine before any read)
     std::vector<uint8_t> ref;
     std::vector<pm_site_result> res;
-    std::unique_ptr<pm_geno_call[]> calls;   // (written by the engine before any read: not value-initialised)
     std::vector<Pending*> pend;
     int nb = 0;
     BatchBuf(SiteEvaluator& ev, int b, int n)
-        : e(ev), pl((uint8_t*)ev.host_alloc((size_t)b * n * 10)), ref(b), res(b), calls(new pm_geno_call[(size_t)b * n]) {}
-    ~BatchBuf() { e.host_free(pl); }
+        : e(ev), pl((uint8_t*)ev.host_alloc((size_t)b * n * 10)), calls((pm_geno_call*)ev.host_alloc((size_t)b * n * sizeof(pm_geno_call))),
+          ref(b), res(b) {}
+    ~BatchBuf() { e.host_free(pl); e.host_free(calls); }
   };
   BatchBuf bb0(eval, B, np), bb1(eval, B, np);
   BatchBuf* const bbs[2] = {&bb0, &bb1};
-  if (!bb0.pl || !bb1.pl) throw FatalError("out of host memory\n");
+  if (!bb0.pl || !bb1.pl || !bb0.calls || !bb1.calls) throw FatalError("out of host memory\n");
   int cb = 0;   // the batch the main thread fills
-  std::vector<uint32_t> dm((size_t)B * np, 0);
+  // (the depth / map-quality words: all zero in this path, page-locked as well)
+  struct DmBuf {
+    SiteEvaluator& e; uint32_t* p;
+    ~DmBuf() { e.host_free(p); }
+    uint32_t* data() const { return p; }
+  } dm{eval, (uint32_t*)eval.host_alloc((size_t)B * np * sizeof(uint32_t))};
+  if (!dm.p) throw FatalError("out of host memory\n");
+  memset(dm.p, 0, (size_t)B * np * sizeof(uint32_t));
   // records are recycled through a free list (their 10-100 KB line and column buffers are reused, not reallocated and
   // first-touched for every record); the flusher returns a batch's records to it
   std::vector<std::unique_ptr<Pending>> store;
@@ -546,10 +558,10 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
   TaskPool fpool(pool.threads());   // (the flusher's: the main thread's pool parses the next batch meanwhile)
   auto process = [&](BatchBuf& bb) {   // the flusher's work on one batch, in batch order
     std::vector<Pending*>& pend = bb.pend;
-    const pm_geno_call* calls = bb.calls.get();
+    const pm_geno_call* calls = bb.calls;
     int rows = 0;
     double t0 = now();
-    if (bb.nb > 0) eval.run(bb.nb, bb.pl, dm.data(), bb.ref.data(), bb.res.data(), bb.calls.get(), &rows);
+    if (bb.nb > 0) eval.run(bb.nb, bb.pl, dm.data(), bb.ref.data(), bb.res.data(), bb.calls, &rows);
     double t1 = now();
     tm[3] += t1 - t0;
     // the state each record prints with (sequential: a record without data takes the last computed one's)
@@ -736,6 +748,18 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
     }
     withdata[k] = wd;
   };
+  // a record's parsed row goes to its batch slot by a deferred copy, all of a chunk's (or a batch's) copies in parallel
+  std::vector<std::pair<uint8_t*, int>> copies;   // (destination row, chunk record)
+  auto do_copies = [&]() {
+    const int nc2 = (int)copies.size();
+    if (nc2 == 0) return;
+    const int nt = std::min(nc2, 4 * pool.threads());
+    pool.run(nt, [&](int t) {
+      for (int q = (int)((int64_t)nc2 * t / nt); q < (int)((int64_t)nc2 * (t + 1) / nt); q++)
+        memcpy(copies[q].first, rows.data() + (size_t)copies[q].second * np * 10, (size_t)np * 10);
+    });
+    copies.clear();
+  };
   bool eof = false;
   BlockReader br(in, &pool);
   std::vector<BlockReader::Line> lines;
@@ -806,21 +830,26 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
       computed_any = true;
       BatchBuf& bb = *bbs[cb];
       if (cls != cur_chrom) {
+        do_copies();
         if (bb.nb > 0 || !bb.pend.empty()) flush();
         drain();   // (the engine's section changes: no batch of the old one in flight)
         eval.begin_section(cls);
         cur_chrom = cls;
       }
       BatchBuf& bc = *bbs[cb];
-      memcpy(bc.pl + (size_t)bc.nb * np * 10, rows.data() + (size_t)k * np * 10, (size_t)np * 10);
+      copies.push_back({bc.pl + (size_t)bc.nb * np * 10, k});
       r.computed = true;
       r.slot = bc.nb;
       bc.ref[bc.nb] = (uint8_t)(r.a1 | (r.a2 << 4));
       bc.nb++;
       bc.pend.push_back(chunk[k]);
       chunk[k] = nullptr;
-      if (bc.nb == B) flush();
+      if (bc.nb == B) {
+        do_copies();
+        flush();
+      }
     }
+    do_copies();
   }
   flush();
   drain();

@@ -46,6 +46,12 @@ def timing_fields(stderr):
     m = re.search(r"PM_TIMING open inputs ([\d.]+) s", stderr)
     if m:
         out["open_inputs_s"] = float(m.group(1))
+    m = re.search(r"PM_TIMING wall: first batch ([\d.]+) s, ingest done ([\d.]+) s, end ([\d.]+) s", stderr)
+    if m:
+        out.update({"wall_first_batch_s": float(m.group(1)), "wall_ingest_done_s": float(m.group(2)), "wall_end_s": float(m.group(3))})
+    m = re.search(r"PM_TIMING glf ingest: .*decode ahead ([\d.]+) s", stderr)
+    if m:
+        out["glf_decode_ahead_s"] = float(m.group(1))
     m = re.search(r"PM_TIMING engine create ([\d.]+) s", stderr)
     if m:
         out["engine_create_s"] = float(m.group(1))
