@@ -213,6 +213,15 @@ int pm_engine_begin_section(pm_engine *eng, int32_t chrom);
 int pm_engine_run(pm_engine *eng, int32_t n, const uint8_t *pl, const uint32_t *dm, const uint8_t *ref,
                   int32_t inputs_on_device, pm_site_result *res, pm_geno_call *calls, int32_t *n_rows);
 
+/* vcf_mode engines only: pm_engine_run on host inputs (no depth plane) with the genotype rows returned in the
+ * compact pm_vcf_call form the device writes -- best / GQ / label, all FamilyLikelihoodSeq_VCF::OutputVCF
+ * (src/FamilyLikelihoodSeq_VCF.cpp:412-521) prints -- instead of widened into pm_geno_call rows: a quarter of
+ * the bytes, copied straight into `calls` (page-locked from pm_host_alloc: an asynchronous copy).  Replaces, for
+ * the --in_vcf path, the per-record FamilyLikelihoodSeq_VCF::FillPenetrance -> CalcLikelihood -> OutputVCF calls of
+ * PedVCF::VarCallFromVCF (src/PedVCF.cpp:103-160).  PM_EINVAL on an engine created without vcf_mode. */
+int pm_engine_run_vcf(pm_engine *eng, int32_t n, const uint8_t *pl, const uint8_t *ref, pm_site_result *res,
+                      pm_vcf_call *calls, int32_t *n_rows);
+
 /* pm_engine_run split in two, so a driver keeps several batches in flight (one per engine; each engine has its
  * own HIP stream): pm_engine_submit queues the batch's host-to-device copies (asynchronous when pl/dm/ref are
  * page-locked, pm_host_alloc), the pipeline and the copy-back of the per-site results on the engine's stream and

@@ -1267,6 +1267,27 @@ int pm_engine_collect(pm_engine* E, pm_site_result* res, pm_geno_call* calls, in
   return PM_OK;
 }
 
+int pm_engine_run_vcf(pm_engine* E, int32_t n, const uint8_t* pl, const uint8_t* ref, pm_site_result* res, pm_vcf_call* calls,
+                      int32_t* n_rows) {
+  if (!E || !E->vcf || n < 0 || n > E->max_batch || !res || !n_rows) { pm_set_last_error("pm_engine_run_vcf: invalid arguments"); return PM_EINVAL; }
+  *n_rows = 0;
+  if (n == 0) return PM_OK;
+  int rc = pm_engine_submit(E, n, pl, nullptr, ref);
+  if (rc) { E->pending_n = -1; return rc; }
+  E->pending_n = -1;
+  HIP_TRY(hipSetDevice(E->device));
+  HIP_TRY(hipStreamSynchronize(E->stream));
+  int counts[16];
+  memcpy(counts, E->h_counts, sizeof(counts));
+  rc = finish_batch(E, counts);
+  if (rc) return rc;
+  memcpy(res, E->h_res, sizeof(pm_site_result) * n);
+  *n_rows = counts[3];
+  if (calls && counts[3] > 0)   // the device rows as they are (4 B per person)
+    HIP_TRY(hipMemcpy(calls, E->d_calls, sizeof(pm_vcf_call) * E->n_person * (size_t)counts[3], hipMemcpyDeviceToHost));
+  return PM_OK;
+}
+
 int pm_engine_run(pm_engine* E, int32_t n, const uint8_t* pl, const uint32_t* dm, const uint8_t* ref, int32_t on_device,
                   pm_site_result* res, pm_geno_call* calls, int32_t* n_rows) {
   if (!E || n < 0 || n > E->max_batch || !res || !n_rows) { pm_set_last_error("pm_engine_run: invalid arguments"); return PM_EINVAL; }

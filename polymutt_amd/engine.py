@@ -99,6 +99,7 @@ EXPORTS = {
     "pm_engine_set_posterior_carry": (i32, [C.c_void_p, i32]),
     "pm_engine_begin_section": (i32, [C.c_void_p, i32]),
     "pm_engine_run": (i32, [C.c_void_p, i32, C.c_void_p, C.c_void_p, C.c_void_p, i32, C.c_void_p, C.c_void_p, P(i32)]),
+    "pm_engine_run_vcf": (i32, [C.c_void_p, i32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, P(i32)]),
     "pm_engine_run_device": (i32, [C.c_void_p, i32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "pm_engine_sync": (i32, [C.c_void_p]),
     "pm_engine_submit": (i32, [C.c_void_p, i32, C.c_void_p, C.c_void_p, C.c_void_p]),

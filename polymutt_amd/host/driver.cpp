@@ -104,6 +104,18 @@ void* SiteEvaluator::host_alloc(size_t bytes) {
 }
 void SiteEvaluator::host_free(void* p) { free(p); }
 
+void SiteEvaluator::run_vcf(int n, int n_person, const uint8_t* pl, const uint8_t* ref, pm_site_result* res, pm_vcf_call* calls,
+                            int* n_rows) {
+  std::vector<uint32_t> dm((size_t)n * n_person, 0);
+  std::vector<pm_geno_call> wide((size_t)n * n_person);
+  run(n, pl, dm.data(), ref, res, wide.data(), n_rows);
+  for (size_t i = 0; i < (size_t)*n_rows * n_person; i++) {   // (GQ <= 100, best <= 2 in vcf_mode: the device's 4-B form)
+    pm_vcf_call c;
+    c.best = (int8_t)wide[i].best; c.gq = (int8_t)wide[i].gq; c.label = wide[i].label; c.pad = 0;
+    calls[i] = c;
+  }
+}
+
 int default_io_threads(const Options& opt) {
   return opt.io_threads > 0 ? opt.io_threads : std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
 }

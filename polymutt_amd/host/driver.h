@@ -40,6 +40,9 @@ class SiteEvaluator {
   virtual void begin_section(int chrom) = 0;
   virtual void run(int n, const uint8_t* pl, const uint32_t* dm, const uint8_t* ref, pm_site_result* res, pm_geno_call* calls,
                    int* n_rows) = 0;
+  // vcf_mode: the genotype rows in their compact form (pm_engine_run_vcf); the default runs run() and narrows them
+  virtual void run_vcf(int n, int n_person, const uint8_t* pl, const uint8_t* ref, pm_site_result* res, pm_vcf_call* calls,
+                       int* n_rows);
   virtual void counters(pm_counters* out) = 0;
   // famlk[0]'s stale posterior state at a shard start (pm_engine_set_posterior_carry)
   virtual void set_posterior_carry(bool seen) = 0;

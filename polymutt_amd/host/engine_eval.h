@@ -58,6 +58,15 @@ class EngineEvaluator : public SiteEvaluator {
     check(rc);
     note(res, n);
   }
+  void run_vcf(int n, int n_person, const uint8_t* pl, const uint8_t* ref, pm_site_result* res, pm_vcf_call* calls,
+               int* n_rows) override {
+    (void)n_person;
+    check(pm_engine_set_posterior_carry(eng_[0], seen_ ? 1 : 0));
+    int rc = pm_engine_run_vcf(eng_[0], n, pl, ref, res, calls, n_rows);
+    if (rc == PM_EBRENT) throw BrentError();
+    check(rc);
+    note(res, n);
+  }
   void counters(pm_counters* out) override {   // the section totals summed over the engines
     memset(out, 0, sizeof(*out));
     for (auto* e : eng_) {

@@ -135,7 +135,10 @@ void ParallelSiteSource::open(const Pedigree& ped, const std::string& glfIndexFi
     if (has_[j]) active_.push_back(j);
   headAtStart_.assign(n, -1);
   tailAtMerge_.assign(n, 0);
-  if (threads > 1 && !getenv("PM_NO_DECODE_AHEAD")) dpool_ = new TaskPool(std::max(1, threads / 2));
+  if (threads > 1 && !getenv("PM_NO_DECODE_AHEAD")) {   // (PM_DECODE_THREADS: the decode-ahead pool's size, default threads / 2)
+    const char* ed = getenv("PM_DECODE_THREADS");
+    dpool_ = new TaskPool(std::max(1, ed ? atoi(ed) : threads / 2));
+  }
   lastPos_.assign(window_, 0);
   fast_ = !getenv("PM_SERIAL_MERGE");
   virtual_.pos = 0;

@@ -248,7 +248,7 @@ struct Pending {          // one record awaiting output, in file order
 
 struct State {            // what FamilyLikelihoodSeq_VCF holds between records (stale output, :412-521)
   double qual = 0.0, min = 0.0;
-  std::vector<pm_geno_call> calls;   // per flattened person
+  std::vector<pm_vcf_call> calls;    // per flattened person
   int a_ref = 0;                     // allele of the label convention (always allele1 in this path)
 };
 
@@ -272,11 +272,11 @@ void copy_file_into(const std::string& path, FILE* out) {
   while ((got = fread(buf.data(), 1, buf.size(), in)) > 0) fwrite(buf.data(), 1, got, out);
   fclose(in);
 }
-int64_t pack_call(const pm_geno_call& c) {
-  return (int64_t)(uint16_t)c.best | ((int64_t)(uint16_t)c.gq << 16) | ((int64_t)(uint8_t)c.label << 32);
+int64_t pack_call(const pm_vcf_call& c) {
+  return (int64_t)(uint8_t)c.best | ((int64_t)(uint8_t)c.gq << 8) | ((int64_t)(uint8_t)c.label << 16);
 }
-pm_geno_call unpack_call(int64_t v) {
-  pm_geno_call c{0.0, (int16_t)(v & 0xFFFF), (int16_t)((v >> 16) & 0xFFFF), (int8_t)((v >> 32) & 0xFF), {0, 0, 0}};
+pm_vcf_call unpack_call(int64_t v) {
+  pm_vcf_call c{(int8_t)(v & 0xFF), (int8_t)((v >> 8) & 0xFF), (int8_t)((v >> 16) & 0xFF), 0};
   return c;
 }
 double bits2d(int64_t v) { double d; memcpy(&d, &v, 8); return d; }
@@ -363,18 +363,18 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
   // engine on the other, formats its records and hands their text to the writer thread.  A batch's PL rows are in
   // page-locked memory where the evaluator offers it (an asynchronous, faster host-to-device copy); pend: its records
   // awaiting output, in file order; nb: its computed records.
-  // The calls (B x np of them, 0.45 GB at 7000 samples) come back in page-locked memory too: from pageable memory
-  // that copy was most of the engine stage.
+  // The calls come back in their compact 4-B form (pm_engine_run_vcf), into page-locked memory too: widened into
+  // pm_geno_call rows in pageable memory (0.45 GB per batch at 7000 samples) they were most of the engine stage.
   struct BatchBuf {
     SiteEvaluator& e;
     uint8_t* pl;
-    pm_geno_call* calls;   // (written by the engine before any read)
+    pm_vcf_call* calls;   // (written by the engine before any read)
     std::vector<uint8_t> ref;
     std::vector<pm_site_result> res;
     std::vector<Pending*> pend;
     int nb = 0;
     BatchBuf(SiteEvaluator& ev, int b, int n)
-        : e(ev), pl((uint8_t*)ev.host_alloc((size_t)b * n * 10)), calls((pm_geno_call*)ev.host_alloc((size_t)b * n * sizeof(pm_geno_call))),
+        : e(ev), pl((uint8_t*)ev.host_alloc((size_t)b * n * 10)), calls((pm_vcf_call*)ev.host_alloc((size_t)b * n * sizeof(pm_vcf_call))),
           ref(b), res(b) {}
     ~BatchBuf() { e.host_free(pl); e.host_free(calls); }
   };
@@ -382,14 +382,6 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
   BatchBuf* const bbs[2] = {&bb0, &bb1};
   if (!bb0.pl || !bb1.pl || !bb0.calls || !bb1.calls) throw FatalError("out of host memory\n");
   int cb = 0;   // the batch the main thread fills
-  // (the depth / map-quality words: all zero in this path, page-locked as well)
-  struct DmBuf {
-    SiteEvaluator& e; uint32_t* p;
-    ~DmBuf() { e.host_free(p); }
-    uint32_t* data() const { return p; }
-  } dm{eval, (uint32_t*)eval.host_alloc((size_t)B * np * sizeof(uint32_t))};
-  if (!dm.p) throw FatalError("out of host memory\n");
-  memset(dm.p, 0, (size_t)B * np * sizeof(uint32_t));
   // records are recycled through a free list (their 10-100 KB line and column buffers are reused, not reallocated and
   // first-touched for every record); the flusher returns a batch's records to it
   std::vector<std::unique_ptr<Pending>> store;
@@ -409,12 +401,12 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
   int64_t n_lead = 0;
   FILE* lead = nullptr;   // sharded, R > 0: raw lines met before this rank's first record with data
   State st;
-  st.calls.assign(np, pm_geno_call{0.0, 0, 0, PM_LBL_VCF_DIPLOID, {0, 0, 0}});
+  st.calls.assign(np, pm_vcf_call{0, 0, PM_LBL_VCF_DIPLOID, 0});
 
   // The state a record is printed with: its own (a computed record) or the previous computed record's (a record
   // without data, PedVCF.cpp:113-122): QUAL, the AF minimiser and every person's call.
-  struct RecState { double qual, min; const pm_geno_call* calls; };
-  auto fresh_state = [&](const Pending& r, const pm_site_result* Rs, const pm_geno_call* C) {
+  struct RecState { double qual, min; const pm_vcf_call* calls; };
+  auto fresh_state = [&](const Pending& r, const pm_site_result* Rs, const pm_vcf_call* C) {
     // mono/poly -> QUAL (PedVCF.cpp:136-152), with the reference's operator-precedence slip
     const double mono = Rs->varllk[0], poly = Rs->varllk[1];
     double llk_alt, llk_ref;
@@ -492,7 +484,7 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
     if (hn >= (int)sizeof(head)) { putf(hn); w += snprintf(w, (size_t)hn + 1, "\tAF=%.2f;AC=%d;DP=%d\t%s", 1 - S.min, AC, totalDepth, fmt_s); }
     else putf(hn);
     for (size_t s = 0; s < ns; s++) {
-      const pm_geno_call& c = S.calls[inc_cols[s].second];
+      const pm_vcf_call& c = S.calls[inc_cols[s].second];
       const Fields& F = fv[s];
       const char* lab;
       if (c.label == PM_LBL_DOT) lab = ".";
@@ -558,10 +550,10 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
   TaskPool fpool(pool.threads());   // (the flusher's: the main thread's pool parses the next batch meanwhile)
   auto process = [&](BatchBuf& bb) {   // the flusher's work on one batch, in batch order
     std::vector<Pending*>& pend = bb.pend;
-    const pm_geno_call* calls = bb.calls;
+    const pm_vcf_call* calls = bb.calls;
     int rows = 0;
     double t0 = now();
-    if (bb.nb > 0) eval.run(bb.nb, bb.pl, dm.data(), bb.ref.data(), bb.res.data(), bb.calls, &rows);
+    if (bb.nb > 0) eval.run_vcf(bb.nb, np, bb.pl, bb.ref.data(), bb.res.data(), bb.calls, &rows);
     double t1 = now();
     tm[3] += t1 - t0;
     // the state each record prints with (sequential: a record without data takes the last computed one's)
@@ -875,7 +867,7 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
   fclose(out);
   if (lead) {   // this rank's leading no-data records, with the state of the nearest earlier rank that computed one
     State carried;
-    carried.calls.assign(np, pm_geno_call{0.0, 0, 0, PM_LBL_VCF_DIPLOID, {0, 0, 0}});
+    carried.calls.assign(np, pm_vcf_call{0, 0, PM_LBL_VCF_DIPLOID, 0});
     for (int q = R - 1; q >= 0; q--) {
       const int64_t* v = recv.data() + (size_t)q * K;
       if (!v[0]) continue;

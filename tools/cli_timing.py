@@ -58,8 +58,8 @@ def timing_fields(stderr):
     return out
 
 
-def run_cli(args, cwd, timeout=1200):
-    env = dict(os.environ, PM_TIMING="1")
+def run_cli(args, cwd, timeout=1200, extra_env=None):
+    env = dict(os.environ, PM_TIMING="1", **(extra_env or {}))
     t0 = time.perf_counter()
     r = subprocess.run(args, cwd=cwd, capture_output=True, text=True, timeout=timeout, env=env)
     dt = time.perf_counter() - t0
@@ -121,6 +121,8 @@ def main():
     ap.add_argument("--keep", default=None, help="work directory to keep (default: a temporary one, removed)")
     ap.add_argument("--glf", action="store_true", help="also time the CLI on the GLF files themselves (the reference's input)")
     ap.add_argument("--vcf-only", action="store_true", help="only the --in_vcf timing (no GLF / block runs)")
+    ap.add_argument("--no-blocks", action="store_true", help="skip the --in_blocks runs (with --glf: GLF runs only)")
+    ap.add_argument("--glf-env", nargs="+", default=[""], help="GLF runs under each of these env settings (K=V,K2=V2)")
     ap.add_argument("--vcf-small", type=int, default=2000, help="--in_vcf start-up run: records (subtracted for the steady rate)")
     a = ap.parse_args()
     tmp = a.keep or tempfile.mkdtemp(prefix="pm_cli_", dir=os.environ.get("TMPDIR", "/tmp"))
@@ -133,13 +135,15 @@ def main():
             t0 = time.perf_counter()
             pm.synth_write_dataset(tmp, "quad", a.families, a.sites, 7)
             out["seconds_synth_glf"] = time.perf_counter() - t0
-            out["seconds_glf2blocks"], _ = run_cli(base + ["-g", "test.gif", "--glf2blocks", "in.pmb"], tmp)
-            out["pmb_bytes"] = os.path.getsize(os.path.join(tmp, "in.pmb"))
+            if not a.no_blocks:
+                out["seconds_glf2blocks"], _ = run_cli(base + ["-g", "test.gif", "--glf2blocks", "in.pmb"], tmp)
+                out["pmb_bytes"] = os.path.getsize(os.path.join(tmp, "in.pmb"))
             small = os.path.join(tmp, "small")
             pm.synth_write_dataset(small, "quad", a.families, 64, 7)
-            run_cli(base + ["-g", "test.gif", "--glf2blocks", "small.pmb"], small)
+            if not a.no_blocks:
+                run_cli(base + ["-g", "test.gif", "--glf2blocks", "small.pmb"], small)
             ref_body = None
-            for e in a.engines:
+            for e in ([] if a.no_blocks else a.engines):
                 for b in a.batch:
                     # start-up (a 64-site run) and the full run, each the best of 3: single start-up samples varied
                     # 0.48-0.85 s on one box, which made their difference meaningless
@@ -158,13 +162,15 @@ def main():
                     out["runs"].append(rec)
                     print(json.dumps(rec), file=sys.stderr, flush=True)
             if a.glf:   # the drop-in on GLF: decode, merge and fill in the ingest thread; start-up from the 64-site GLF set
-                for e in a.engines:
-                    t_small = min(run_cli(base + ["-g", "test.gif", "--out_vcf", "s.vcf", "--engines", str(e)] + extra, small)[0]
+                for e, genv in [(e, g) for e in a.engines for g in a.glf_env]:
+                    xe = dict(kv.split("=", 1) for kv in genv.split(",") if kv)
+                    t_small = min(run_cli(base + ["-g", "test.gif", "--out_vcf", "s.vcf", "--engines", str(e)] + extra, small, extra_env=xe)[0]
                                   for _ in range(3))
-                    runs = [run_cli(base + ["-g", "test.gif", "--out_vcf", "g.vcf", "--engines", str(e)] + extra, tmp) for _ in range(3)]
+                    runs = [run_cli(base + ["-g", "test.gif", "--out_vcf", "g.vcf", "--engines", str(e)] + extra, tmp, extra_env=xe)
+                            for _ in range(3)]
                     dt, r = min(runs, key=lambda x: x[0])
                     bd = body(os.path.join(tmp, "g.vcf"))
-                    rec = {"input": "glf", "engines": e, "seconds": dt, "startup_seconds": t_small, "sites_per_s": a.sites / dt,
+                    rec = {"input": "glf", "env": genv, "engines": e, "seconds": dt, "startup_seconds": t_small, "sites_per_s": a.sites / dt,
                            "sites_per_s_past_startup": a.sites / max(1e-9, dt - t_small), "records": len(bd) - 1,
                            "vcf_identical_to_blocks": ref_body is None or bd == ref_body}
                     rec.update(timing_fields(r.stderr))
@@ -174,8 +180,9 @@ def main():
                     out.setdefault("glf_runs", []).append(rec)
                     print(json.dumps(rec), file=sys.stderr, flush=True)
                 out["glf_best"] = max(out["glf_runs"], key=lambda x: x["sites_per_s_past_startup"])
-            best = max(out["runs"], key=lambda x: x["sites_per_s_past_startup"])
-            out["best"] = {k: best[k] for k in ("engines", "batch", "sites_per_s", "sites_per_s_past_startup")}
+            if out["runs"]:
+                best = max(out["runs"], key=lambda x: x["sites_per_s_past_startup"])
+                out["best"] = {k: best[k] for k in ("engines", "batch", "sites_per_s", "sites_per_s_past_startup")}
             out["all_vcf_identical"] = all(x["vcf_identical_to_first"] for x in out["runs"])
         if a.vcf_records:
             vd = os.path.join(tmp, "vcf")
