@@ -478,7 +478,9 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, c
   } else {   // PedigreeGLF with parallel decode (ingest.h)
     auto* g = new ParallelSiteSource;
     srcp.reset(g);
-    g->open(ped, opt.glfListFile, default_io_threads(opt));
+    // sites per merge window (PM_GLF_WINDOW): 4096 measured best of 512-16384 (profiles/r05v_glf_window.json)
+    const char* ew = getenv("PM_GLF_WINDOW");
+    g->open(ped, opt.glfListFile, default_io_threads(opt), ew ? std::max(64, atoi(ew)) : 4096);
   }
   SiteStream& src = *srcp;
   if (getenv("PM_TIMING")) fprintf(stderr, "PM_TIMING open inputs %.3f s\n", now_s() - t_open0);

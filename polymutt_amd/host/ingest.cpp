@@ -373,9 +373,14 @@ void ParallelSiteSource::fill(const int* rowOf, uint8_t* pl, uint32_t* dm) {
   // the merge's advance rule replayed per person, for a chunk of up to 64 persons at a time with the sites outer, so each
   // site row receives the chunk's contiguous 640 PL bytes (columns of a row) rather than one 10-byte piece per row
   const int na = (int)active_.size();
-  const int nch = (na + 63) / 64;
+  static const int kFillChunk = [] {   // persons per chunk (PM_FILL_CHUNK, 1-64): the queues a thread streams at once
+    const char* e = getenv("PM_FILL_CHUNK");
+    return e ? std::max(1, std::min(64, atoi(e))) : 64;
+  }();
+  const int FC = kFillChunk;
+  const int nch = (na + FC - 1) / FC;
   pool_->run(nch, [&](int c) {
-    const int i0 = c * 64, i1 = std::min(na, i0 + 64), m = i1 - i0;
+    const int i0 = c * FC, i1 = std::min(na, i0 + FC), m = i1 - i0;
     // per person of the chunk: its column, queue base and last index (the section-start placeholder only
     // as the first head: handled by state() before the site loop)
     int k[64], col[64], last[64];

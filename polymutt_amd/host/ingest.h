@@ -85,7 +85,7 @@ class ParallelSiteSource : public SiteStream {
   ParallelSiteSource& operator=(const ParallelSiteSource&) = delete;
   ~ParallelSiteSource();
   // threads: decode/fill workers (the caller counts as one).  window: sites merged per nextSites call at most.
-  void open(const Pedigree& ped, const std::string& glfIndexFile, int threads, int window = 1024);
+  void open(const Pedigree& ped, const std::string& glfIndexFile, int threads, int window = 4096);
   bool nextSection() override;   // PedigreeGLF::Move2NextSection (the files skip to their next section in parallel)
   const std::string& label() const override { return files_[nonNull_].label; }
   int maxPosition() const override { return files_[nonNull_].maxPosition; }
@@ -123,7 +123,7 @@ class ParallelSiteSource : public SiteStream {
   std::vector<char> has_;
   std::vector<std::string> pids_;
   int nonNull_ = -1;
-  int window_ = 1024;
+  int window_ = 4096;
   TaskPool* pool_ = nullptr;
   GlfState virtual_{};
   int currentPos_ = 0;

@@ -164,16 +164,19 @@ def main():
             if a.glf:   # the drop-in on GLF: decode, merge and fill in the ingest thread; start-up from the 64-site GLF set
                 for e, genv in [(e, g) for e in a.engines for g in a.glf_env]:
                     xe = dict(kv.split("=", 1) for kv in genv.split(",") if kv)
+                    # (best of 5: the 64-site start-up runs varied 1.28-1.65 s between calls on one box)
                     t_small = min(run_cli(base + ["-g", "test.gif", "--out_vcf", "s.vcf", "--engines", str(e)] + extra, small, extra_env=xe)[0]
-                                  for _ in range(3))
+                                  for _ in range(5))
                     runs = [run_cli(base + ["-g", "test.gif", "--out_vcf", "g.vcf", "--engines", str(e)] + extra, tmp, extra_env=xe)
-                            for _ in range(3)]
+                            for _ in range(5)]
                     dt, r = min(runs, key=lambda x: x[0])
                     bd = body(os.path.join(tmp, "g.vcf"))
                     rec = {"input": "glf", "env": genv, "engines": e, "seconds": dt, "startup_seconds": t_small, "sites_per_s": a.sites / dt,
                            "sites_per_s_past_startup": a.sites / max(1e-9, dt - t_small), "records": len(bd) - 1,
                            "vcf_identical_to_blocks": ref_body is None or bd == ref_body}
                     rec.update(timing_fields(r.stderr))
+                    if "wall_end_s" in rec:   # in the pipeline: the sites after the first batch over the wall time after it
+                        rec["sites_per_s_pipeline"] = (a.sites - 4096) / max(1e-9, rec["wall_end_s"] - rec["wall_first_batch_s"])
                     m = re.search(r"PM_TIMING glf ingest: decode ([\d.]+) s, merge ([\d.]+) s, fill ([\d.]+) s", r.stderr)
                     if m:
                         rec.update({"glf_decode_s": float(m.group(1)), "glf_merge_s": float(m.group(2)), "glf_fill_s": float(m.group(3))})
