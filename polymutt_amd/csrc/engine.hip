@@ -88,7 +88,7 @@ struct pm_engine {
   int Tq = 0, Sq = 0, grid_q = 0;
   int quad_bpc16 = 0, quad_bpc8 = 0;   // QUAD k_brent blocks resident per CU (occupancy query, first launch)
   bool units_empty = false, units1_empty = false;   // a lane plan with no nuclear or founder unit (every family peeled)
-  int ep_bpc[2] = {0, 0};   // EP one-wave k_brent blocks resident per CU (bi-allelic / --denovo instantiation)
+  std::vector<std::pair<const void*, int>> ep_bpc;   // EP one-wave k_brent blocks resident per CU, per instantiation
   bool all_trio = false;   // every unit of the lane plan is a 3-person nuclear family (or empty): k_brent's NF = 3
   int4* d_units_q = nullptr;
   int* d_items[N_LISTS] = {nullptr, nullptr, nullptr};
@@ -776,8 +776,16 @@ static DevArgs make_args(pm_engine* E, int n, const uint8_t* pl, const uint32_t*
 typedef void (*BrentFn)(DevArgs, int);
 // numerics: PM_NUM_PRODUCT / PM_NUM_EXACT for every flavour; PM_NUM_POLY only for the lean kernel
 // (the generic and ES flavours fall back to PRODUCT numerics).
-static BrentFn brent_kernel(int T, int S, int num, bool gen, bool es, bool dn = false, bool pf = false, bool ep = false, bool trio = false) {
+static BrentFn brent_kernel(int T, int S, int num, bool gen, bool es, bool dn = false, bool pf = false, bool ep = false, bool trio = false,
+                            bool epo = false) {
   const int n = (num == PM_NUM_POLY && gen) ? PM_NUM_PRODUCT : num;
+  if (es && ep && epo && T == 64 && (S == 1 || S == 2 || S == 4)) {   // ep_only plans: the nuclear machinery compiled out
+#define PMKEO(s) \
+  if (S == s) return dn ? k_brent<64, s, PM_NUM_PRODUCT, true, true, true, false, true, false, 1> \
+                        : k_brent<64, s, PM_NUM_PRODUCT, true, true, false, false, true, false, 1>;
+    PMKEO(1) PMKEO(2) PMKEO(4)
+#undef PMKEO
+  }
   if (es && ep) {   // extended families in polynomial form (PM_NUM_POLY); DN: with the 10-state (--denovo) hoisting
 #define PMKEP(t, s) \
   if (T == t && S == s) return dn ? k_brent<t, s, PM_NUM_PRODUCT, true, true, true, false, true> : k_brent<t, s, PM_NUM_PRODUCT, true, true, false, false, true>;
@@ -918,9 +926,10 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
     shmem = (size_t)(T / 64) * 2 * DN_PF_BUF;
   }
   const bool ep = !unrelated && n_ext > 0 && E->es_poly && E->par.numerics == PM_NUM_POLY;
+  const bool ep_only = ep && (E->use_plan1 ? E->units1_empty : E->units_empty) && !getenv("PM_NO_EP_ONLY");
   BrentFn fn = quad ? qfn
                    : brent_kernel(T, S, E->par.numerics, gen, !unrelated && n_ext > 0, A.denovo != 0, A.pf_npad > 0 || A.dn_pf, ep,
-                                  E->all_trio && !unrelated && !getenv("PM_NO_TRIO"));
+                                  E->all_trio && !unrelated && !getenv("PM_NO_TRIO"), ep_only && !getenv("PM_NO_EPO"));
   if (!fn) { pm_set_last_error("launch_brent: no kernel variant for the lane plan"); return PM_EINVAL; }
   // multi-wave de novo plans (T = 512 / 1024: more than 1024 families) stage 2 buffers per wave: above the
   // default 64 KB dynamic-LDS limit the kernel must opt in, and the block (plus its static LDS: lane plan,
@@ -937,7 +946,7 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
   A.ws_lds = 0;
   if (ep) {   // polynomial-form peels: coefficients from k_es_hoist, no workspace in k_brent
     A.es_poly = 1;
-    A.ep_only = (E->use_plan1 ? E->units1_empty : E->units_empty) && !getenv("PM_NO_EP_ONLY");
+    A.ep_only = ep_only;
   } else if (!unrelated && n_ext > 0 && !E->par.denovo) {   // BA peels (the 10-state one is too big)
     const size_t need = (size_t)E->ws_per_lane * T * sizeof(double);
     if (need > 0 && need <= 150 * 1024) {
@@ -949,7 +958,9 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
     }
   }
   if (ep && T == 64) {   // EP one-wave plans: a persistent grid of exactly the resident blocks (no partial second round)
-    int& bpc = E->ep_bpc[fn == brent_kernel(64, S, E->par.numerics, true, true, true, false, true) ? 1 : 0];
+    int bpc = 0;
+    for (auto& c : E->ep_bpc)
+      if (c.first == (const void*)fn) bpc = c.second;
     if (bpc == 0) {
       int n = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)fn, T, shmem) != hipSuccess || n <= 0) {
@@ -957,6 +968,7 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
         n = 1024 / T;
       }
       bpc = n;
+      E->ep_bpc.push_back({(const void*)fn, n});
     }
     grid = std::min(grid, E->n_cu * bpc);
     grid -= grid % 8;

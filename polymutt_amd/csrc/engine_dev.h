@@ -45,6 +45,9 @@
 #ifndef PM_QD_WAVES
 #define PM_QD_WAVES 2   // QUAD plans: waves per SIMD the k_brent instantiation is compiled for (launch bounds, grid)
 #endif
+#ifndef PM_EPO_WAVES
+#define PM_EPO_WAVES 3   // the ep_only EP kernels (NF = 1): 167 VGPRs fit 3 waves per SIMD
+#endif
 #ifndef PM_EP_WAVES
 #define PM_EP_WAVES 2   // EP (polynomial-form extended families) k_brent: waves per SIMD of the launch bounds
 #endif
@@ -522,7 +525,9 @@ __device__ __forceinline__ double es_poly_eval(const double* c, size_t st, int D
 
 // es_poly_eval on register-resident coefficients (c[a] = 0 above D <= PDM): the leading zeros leave the Horner
 // sum's bits unchanged (0 * t + c = c)
+#ifndef PM_EPE
 #define PM_EPE 4   // extended families per lane whose coefficients stay in registers through an item's evaluations
+#endif
 __device__ __forceinline__ double es_poly_eval_r(const double* c, int D, double x) {
   const double g = 1 - x;
   double acc = 0.0, base;
@@ -1743,8 +1748,13 @@ constexpr int brent_waves() { return (NUM == PM_NUM_POLY && !GEN && (T == 64 || 
 // reference-order peel (d_es_lk) is compiled out, and the block asks for 2 waves per SIMD.
 // QD: lean --denovo kernel on a QUAD plan (hoist_quad: coalesced dword loads, prefetched across items).
 // NF: 3 = every nuclear family of the plan is a trio (the lean PF kernel's hoisting drops the second kid), 0 = any.
+// NF: the lean PF kernel's persons per family when every unit is one size (3: trio plans); on EP kernels NF = 1 marks
+// the ep_only plans (every family peeled: no nuclear or founder unit), whose unit loads, nuclear hoisting and lane
+// products are compiled out -- fewer live registers (PM_EPO_WAVES per SIMD)
 template <int T, int S, int NUM, bool GEN, bool ES, bool DN = false, bool PF = false, bool EP = false, bool QD = false, int NF = 0>
-__global__ void __launch_bounds__(T, (EP ? PM_EP_WAVES : QD ? PM_QD_WAVES : brent_waves<T, S, NUM, GEN>())) k_brent(DevArgs A, int list) {
+__global__ void __launch_bounds__(T, (EP ? (NF == 1 ? PM_EPO_WAVES : PM_EP_WAVES) : QD ? PM_QD_WAVES : brent_waves<T, S, NUM, GEN>()))
+k_brent(DevArgs A, int list) {
+  constexpr bool EPO = EP && NF == 1;
   constexpr bool PROD = NUM != PM_NUM_EXACT;
   constexpr bool POLYK = NUM == PM_NUM_POLY && !GEN;
   __shared__ double s_lk[256];
@@ -1762,7 +1772,7 @@ __global__ void __launch_bounds__(T, (EP ? PM_EP_WAVES : QD ? PM_QD_WAVES : bren
   int4 unit[S];
   if constexpr (!POLYK) {
 #pragma unroll
-    for (int s = 0; s < S; s++) unit[s] = A.units[s * T + threadIdx.x];
+    for (int s = 0; s < S; s++) unit[s] = EPO ? make_int4(0, 0, 0, 0) : A.units[s * T + threadIdx.x];
   }
   const int nItems = A.counts[list];
   const int* items = A.items[list];
@@ -1901,7 +1911,7 @@ __global__ void __launch_bounds__(T, (EP ? PM_EP_WAVES : QD ? PM_QD_WAVES : bren
 #pragma unroll
     for (int s = 0; s < S; s++) {
       fl[s] = 0;
-      if constexpr (QD) continue;
+      if constexpr (QD || EPO) continue;
       if (PFK || DNPF_ONLY || hoisted) continue;
       if constexpr (POLY) {
         const int4 u = A.units[s * T + threadIdx.x];   // L1/L2-resident; not kept in registers
@@ -1975,7 +1985,8 @@ __global__ void __launch_bounds__(T, (EP ? PM_EP_WAVES : QD ? PM_QD_WAVES : bren
         }
       } else if (PROD) {
         double m = 1.0; int e = 0;
-        if (!(ES && EP && A.ep_only)) lane_prod<S, GEN>(x, unit, (const double(*)[9])cond, fl, pmode, m, e);
+        if constexpr (!EPO)
+          if (!(ES && EP && A.ep_only)) lane_prod<S, GEN>(x, unit, (const double(*)[9])cond, fl, pmode, m, e);
         if constexpr (ES && EP && EPE > 0) {   // register-resident coefficients first (independent Horner chains)
           const double g = 1 - x;
           if (__builtin_amdgcn_readfirstlane((int)(g > 0.0))) {

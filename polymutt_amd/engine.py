@@ -86,6 +86,7 @@ SITE_DTYPE = np.dtype([
     ("af", "<f8"), ("ab", "<f8"), ("denovo_lr", "<f8"), ("evals", "<i4", (7,)), ("allele1", "<i4"),
     ("allele2", "<i4"), ("is_mono", "<i4"), ("denovo_mono", "<i4"), ("call_row", "<i4")])
 CALL_DTYPE = np.dtype([("dosage", "<f8"), ("best", "<i2"), ("gq", "<i2"), ("label", "i1"), ("_pad", "i1", (3,))])
+VCF_CALL_DTYPE = np.dtype([("best", "i1"), ("gq", "i1"), ("label", "i1"), ("pad", "i1")])   # pm_vcf_call
 assert SITE_DTYPE.itemsize == C.sizeof(SiteResult) == 240, SITE_DTYPE.itemsize
 assert CALL_DTYPE.itemsize == C.sizeof(GenoCall) == 16
 
@@ -257,6 +258,17 @@ class Engine:
         rows = i32(0)
         self._check(self.lib.pm_engine_run(self.h, n, _ptr(pl), _ptr(dm), _ptr(ref), 0, _ptr(res), _ptr(calls),
                                            C.byref(rows)))
+        return res, calls[: rows.value]
+
+    def run_vcf(self, pl, ref):
+        """pm_engine_run_vcf (vcf_mode engines): (results[n], calls[rows, n_person] of VCF_CALL_DTYPE, 4 B each)."""
+        n = len(ref)
+        pl = np.ascontiguousarray(pl, dtype=np.uint8).reshape(n, self.n_person, 10)
+        ref = np.ascontiguousarray(ref, dtype=np.uint8)
+        res = np.zeros(n, dtype=SITE_DTYPE)
+        calls = np.zeros((n, self.n_person), dtype=VCF_CALL_DTYPE)
+        rows = i32(0)
+        self._check(self.lib.pm_engine_run_vcf(self.h, n, _ptr(pl), _ptr(ref), _ptr(res), _ptr(calls), C.byref(rows)))
         return res, calls[: rows.value]
 
     def submit(self, pl, dm, ref):

@@ -78,6 +78,25 @@ def test_engine_vcf_mode_config5_geometry(built, tmp_path, numerics):
     eng.close()
 
 
+def test_engine_run_vcf_matches_run(built, tmp_path):
+    """pm_engine_run_vcf (the --in_vcf driver's entry: rows in the device's 4-byte form) returns pm_engine_run's
+    results and its rows narrowed to (best, GQ, label), on 2000 mixed families (config 5's shape)."""
+    pm.synth_write_dataset(str(tmp_path), "mixed", 2000, 512, 41)
+    ped, secs, _ = read_dataset(str(tmp_path))
+    (label, pos, ref, pl, dm), = secs
+    refalt = _vcf_block(pl, ref, 13)
+    eng = pm.Engine(ped.view, pm.Params.defaults(vcf_mode=1), max_batch=256)
+    zeros = np.zeros_like(dm)
+    for s in range(0, len(ref), 256):
+        sl = slice(s, s + 256)
+        r4, c4 = eng.run_vcf(pl[sl], refalt[sl])
+        r16, c16 = eng.run(pl[sl], zeros[sl], refalt[sl])
+        assert r4.tobytes() == r16.tobytes() and len(c4) == len(c16) == len(r4)
+        for f in ("best", "gq", "label"):
+            assert np.array_equal(c4[f].astype(np.int16), c16[f].astype(np.int16)), f
+    eng.close()
+
+
 def _vcf_block(pl, ref, seed):
     """Biallelic (ref, alt) per site: alt = transition, or a transversion on a third of the sites."""
     rng = np.random.default_rng(seed)
