@@ -2003,15 +2003,21 @@ k_brent(DevArgs A, int list) {
               pw = ((edl >> b) & 1) ? pw * gp : pw;
               gp = gp * gp;
             }
+            // each family's value split into mantissa and exponent first (independent), then one chain of products
+            // of mantissas in [0.5, 1) (no under- or overflow) and one renormalisation: bit for bit the mantissa of
+            // the renormalise-after-every-factor chain (scalings by 2^k are exact), with a shorter serial path
+            double mq[EPE];
 #pragma unroll
             for (int q = 0; q < EPE; q++) {
               double acc = ce[q][PDM];
 #pragma unroll
               for (int a = PDM - 1; a >= 0; a--) acc = fma(acc, t, ce[q][a]);
               int e1;
-              m = frexp(m * acc, &e1);   // (one factor per renormalisation: a peeled family's L can be ~1e-290)
+              mq[q] = frexp(acc, &e1);   // (a peeled family's L can be ~1e-290)
               e += e1;
             }
+#pragma unroll
+            for (int q = 0; q < EPE; q++) m = m * mq[q];
             int e2;
             m = frexp(m * pw, &e2);
             e += e2;
