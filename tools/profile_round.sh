@@ -13,8 +13,10 @@ mkdir -p "$OUT"
 echo "revision: $(cat "$R/REVISION" 2>/dev/null || echo unknown)" > "$OUT/revision.txt"
 cd /tmp && export TMPDIR=/tmp
 BENCH="python3 $R/bench.py --no-cpu-baseline --steps 40 --calib-steps 4"
+ONLY=${PR_ONLY:-}   # PR_ONLY="a b c": run only these steps (a round's passes split over several gpurun calls)
 step() {   # step NAME SECONDS CMD...
   local name=$1 secs=$2; shift 2
+  if [ -n "$ONLY" ] && [[ " $ONLY " != *" $name "* ]]; then return 0; fi
   echo "[$(date +%T)] $name" >&2
   timeout -k 10 "$secs" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
   local rc=$?
@@ -37,6 +39,11 @@ step pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_w
 step pmc_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_INSTS_VMEM_RD --output-format csv -d "$OUT/pmc_sq" -o run -- $BENCH --engines 1 --steps 4 --warmup 1 --calib-steps 0
 step pmc_sq2 400 rocprofv3 --pmc SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA SQ_INSTS_VMEM_WR SQ_INSTS_SMEM --output-format csv -d "$OUT/pmc_sq2" -o run -- $BENCH --engines 1 --steps 4 --warmup 1 --calib-steps 0
 step pmc_sq3 400 rocprofv3 --pmc SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_sq3" -o run -- $BENCH --engines 1 --steps 4 --warmup 1 --calib-steps 0
+# config 4 BA's EP k_brent and hoisting kernels: SQ and FETCH passes (one engine)
+E10="$BENCH --engines 1 --shape ext10 --families 200 --batch 16384 --no-denovo --steps 4 --warmup 1 --calib-steps 0"
+step pmc_ext10_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_INSTS_VMEM_RD --output-format csv -d "$OUT/pmc_ext10_sq" -o run -- $E10
+step pmc_ext10_sq2 400 rocprofv3 --pmc SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA SQ_INSTS_VMEM_WR SQ_INSTS_SMEM --output-format csv -d "$OUT/pmc_ext10_sq2" -o run -- $E10
+step pmc_ext10_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_ext10_fetch" -o run -- $E10
 # the other BASELINE configs' bench lines (default three engines)
 B="python3 $R/bench.py --no-cpu-baseline"
 step cfg2 300 $B --shape trio --families 1000 --no-denovo --steps 100

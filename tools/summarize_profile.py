@@ -25,6 +25,41 @@ def short(name):
     return n
 
 
+def pmc_summary(src, subs):
+    """Per kernel: dispatches and mean counters per dispatch over the PMC pass directories `subs`."""
+    acc = defaultdict(lambda: defaultdict(float))
+    disp = defaultdict(set)
+    src_of = {}   # counter -> the pass it was collected in
+    for sub in subs:
+        path = os.path.join(src, sub, "run_counter_collection.csv")
+        if not os.path.exists(path):
+            continue
+        for row in csv.DictReader(open(path)):
+            k = short(row["Kernel_Name"])
+            acc[k][row["Counter_Name"]] += float(row["Counter_Value"])
+            disp[(k, sub)].add(row["Dispatch_Id"])
+            src_of[row["Counter_Name"]] = sub
+    out = {}
+    for k, counters in acc.items():
+        d = {}
+        for c, v in counters.items():
+            sub = src_of[c]
+            n = max(1, len(disp[(k, sub)]))
+            d[c + "_per_dispatch"] = v / n
+            d["dispatches_" + sub] = n
+        if "SQ_WAVE_CYCLES_per_dispatch" in d:
+            for c in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS"):
+                if c + "_per_dispatch" in d:
+                    d[c + "_frac_of_wave_cycles"] = d[c + "_per_dispatch"] / d["SQ_WAVE_CYCLES_per_dispatch"]
+        if "FETCH_SIZE_per_dispatch" in d:
+            # FETCH_SIZE / WRITE_SIZE are reported in KiB
+            d["hbm_read_bytes_per_dispatch"] = 2 * d["FETCH_SIZE_per_dispatch"] * 1024
+        if "WRITE_SIZE_per_dispatch" in d:
+            d["hbm_write_bytes_per_dispatch"] = d["WRITE_SIZE_per_dispatch"] * 1024
+        out[k] = d
+    return out
+
+
 def main():
     rnd = sys.argv[1] if len(sys.argv) > 1 else "r01"
     src = os.path.join(ROOT, "gpurun_out", f"prof_{rnd}")
@@ -60,36 +95,7 @@ def main():
     if peak:
         with open(os.path.join(dst, f"{rnd}_fp64_peak.json"), "w") as fh:
             fh.write(peak[-1] + "\n")
-    acc = defaultdict(lambda: defaultdict(float))
-    disp = defaultdict(set)
-    src_of = {}   # counter -> the pass it was collected in
-    for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sq2", "pmc_sq3"):
-        path = os.path.join(src, sub, "run_counter_collection.csv")
-        if not os.path.exists(path):
-            continue
-        for row in csv.DictReader(open(path)):
-            k = short(row["Kernel_Name"])
-            acc[k][row["Counter_Name"]] += float(row["Counter_Value"])
-            disp[(k, sub)].add(row["Dispatch_Id"])
-            src_of[row["Counter_Name"]] = sub
-    out = {}
-    for k, counters in acc.items():
-        d = {}
-        for c, v in counters.items():
-            sub = src_of[c]
-            n = max(1, len(disp[(k, sub)]))
-            d[c + "_per_dispatch"] = v / n
-            d["dispatches_" + sub] = n
-        if "SQ_WAVE_CYCLES_per_dispatch" in d:
-            for c in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS"):
-                if c + "_per_dispatch" in d:
-                    d[c + "_frac_of_wave_cycles"] = d[c + "_per_dispatch"] / d["SQ_WAVE_CYCLES_per_dispatch"]
-        if "FETCH_SIZE_per_dispatch" in d:
-            # FETCH_SIZE / WRITE_SIZE are reported in KiB
-            d["hbm_read_bytes_per_dispatch"] = 2 * d["FETCH_SIZE_per_dispatch"] * 1024
-        if "WRITE_SIZE_per_dispatch" in d:
-            d["hbm_write_bytes_per_dispatch"] = d["WRITE_SIZE_per_dispatch"] * 1024
-        out[k] = d
+    out = pmc_summary(src, ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sq2", "pmc_sq3"))
     # the tree the passes ran on (profile_round.sh writes revision.txt from REVISION): bench.py stamps
     # roofline.traffic_source with it
     rev = "unknown"
@@ -100,6 +106,11 @@ def main():
     out["revision"] = rev
     with open(os.path.join(dst, f"{rnd}_pmc.json"), "w") as fh:
         json.dump(out, fh, indent=1, sort_keys=True)
+    e10 = pmc_summary(src, ("pmc_ext10_fetch", "pmc_ext10_sq", "pmc_ext10_sq2"))   # config 4 BA: EP k_brent + hoisting
+    if e10:
+        e10["revision"] = rev
+        with open(os.path.join(dst, f"{rnd}_pmc_ext10.json"), "w") as fh:
+            json.dump(e10, fh, indent=1, sort_keys=True)
     print(json.dumps({k: ({kk: round(vv, 1) for kk, vv in v.items()} if isinstance(v, dict) else v) for k, v in out.items()}, indent=1))
 
 
