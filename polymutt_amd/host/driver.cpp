@@ -535,14 +535,17 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, c
     std::atomic<bool> abort{false};
     std::exception_ptr perr, eerr, werr;
     // PM_TIMING: wall clock of the pipeline (since the inputs were opened): first batch handed on, ingest done, end
-    double w_first = 0, w_ingest = 0;
+    double w_first = 0, w_ingest = 0, w_sec = 0, w_sites1 = 0, w_fill1 = 0;
     struct WallReport {
       double t0, &first, &ingest;
       ~WallReport() {
         if (getenv("PM_TIMING"))
           fprintf(stderr, "PM_TIMING wall: first batch %.3f s, ingest done %.3f s, end %.3f s\n", first - t0, ingest - t0, now_s() - t0);
+        if (getenv("PM_TIMING") && sec > 0)
+          fprintf(stderr, "PM_TIMING first window: section %.3f s, sites %.3f s, fill %.3f s\n", sec - t0, sites1 - t0, fill1 - t0);
       }
-    } wall_report{t_open0, w_first, w_ingest};
+      double &sec, &sites1, &fill1;
+    } wall_report{t_open0, w_first, w_ingest, w_sec, w_sites1, w_fill1};
     std::thread producer([&] {
       try {
         size_t done = 0;
@@ -553,6 +556,7 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, c
           const std::string label = src.label();
           if (!chrSel.empty() && chrSel[label] < 1) continue;   // the next section's skip consumes this one
           const int chrom = chrom_of(label);
+          if (w_sec == 0) w_sec = now_s();
           done++;
           toEngine.push({M_SECTION, nullptr, label, chrom, 0, {}});
           int entries = 0;
@@ -562,6 +566,7 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, c
             const double ti = now_s();
             const int want = std::min(src.window(), b->cap - b->n);
             const int got = src.nextSites(want, wpos.data(), wref.data());
+            if (w_sites1 == 0) w_sites1 = now_s();
             if (got > 0 && entries == 0) entries = src.maxPosition();
             for (int k = 0; k < got; k++) {
               const int i = b->n++;
@@ -570,6 +575,7 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, c
               rowOf[k] = i;
             }
             src.fill(rowOf.data(), b->pl, b->dm);
+            if (w_fill1 == 0) w_fill1 = now_s();
             t_ingest += now_s() - ti;
             if (b->n == b->cap) {
               if (w_first == 0) w_first = now_s();
@@ -579,8 +585,10 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, c
             }
             if (src.ended()) break;
           }
-          if (b->n > 0) toEngine.push({M_BATCH, b, label, chrom, 0, {}});
-          else freeq.push(b);
+          if (b->n > 0) {
+            if (w_first == 0) w_first = now_s();
+            toEngine.push({M_BATCH, b, label, chrom, 0, {}});
+          } else freeq.push(b);
           toEngine.push({M_END, nullptr, label, chrom, entries, {}});
         }
       } catch (...) {

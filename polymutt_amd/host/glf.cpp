@@ -15,19 +15,22 @@ GlfFile::~GlfFile() {
 }
 
 bool GlfFile::open(const std::string& path) {
-  fh_ = gzopen(path.c_str(), "rb");
-  if (!fh_) return false;
-  gzbuffer(fh_, 1 << 16);
-  buf_.resize(1 << 16);
-  if (gzdirect(fh_)) {   // not gzip: plain reads of the file (same bytes, one copy fewer)
-    const int fd = ::open(path.c_str(), O_RDONLY);
-    if (fd >= 0) {
-      posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);
-      fd_ = fd;
-      gzclose(fh_);   // (one descriptor per person, as before)
-      fh_ = nullptr;
-    }
+  // gzip (magic 1f 8b) through zlib; anything else is read as it is, as zlib's transparent mode would (gzdirect),
+  // with plain read() calls -- decided from two bytes, so opening a plain file reads nothing more
+  const int fd = ::open(path.c_str(), O_RDONLY);
+  if (fd < 0) return false;
+  uint8_t mg[2] = {0, 0};
+  const bool gz = ::pread(fd, mg, 2, 0) == 2 && mg[0] == 0x1f && mg[1] == 0x8b;
+  if (gz) {
+    ::close(fd);
+    fh_ = gzopen(path.c_str(), "rb");
+    if (!fh_) return false;
+    gzbuffer(fh_, 1 << 16);
+  } else {
+    posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);
+    fd_ = fd;
   }
+  buf_.resize(1 << 16);
   pos_ = len_ = 0;
   zeof_ = false;
   // glfHandler::ReadHeader (:87-134): "GLF\3", u32 header length, header text

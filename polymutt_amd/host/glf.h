@@ -12,6 +12,7 @@
 #pragma once
 #include <cstdint>
 #include <map>
+#include <memory>
 #include <string>
 #include <vector>
 #include <zlib.h>
@@ -42,7 +43,15 @@ class GlfFile {
   bool eof();
   gzFile fh_ = nullptr;
   int fd_ = -1;   // an uncompressed file: read() straight into buf_ (gzread's transparent mode copies once more)
-  std::vector<uint8_t> buf_;
+  struct RawBuf {   // (a read buffer that is not zero-filled: 4000 persons' 64 KB buffers are written by read() first)
+    std::unique_ptr<uint8_t[]> p;
+    size_t n = 0;
+    uint8_t* data() { return p.get(); }
+    const uint8_t* data() const { return p.get(); }
+    size_t size() const { return n; }
+    uint8_t operator[](size_t i) const { return p[i]; }
+    void resize(size_t k) { p.reset(new uint8_t[k]); n = k; }
+  } buf_;
   size_t pos_ = 0, len_ = 0;
   bool zeof_ = false;
 };

@@ -49,6 +49,9 @@ def timing_fields(stderr):
     m = re.search(r"PM_TIMING wall: first batch ([\d.]+) s, ingest done ([\d.]+) s, end ([\d.]+) s", stderr)
     if m:
         out.update({"wall_first_batch_s": float(m.group(1)), "wall_ingest_done_s": float(m.group(2)), "wall_end_s": float(m.group(3))})
+    m = re.search(r"PM_TIMING first window: section ([\d.]+) s, sites ([\d.]+) s, fill ([\d.]+) s", stderr)
+    if m:
+        out.update({"wall_section_s": float(m.group(1)), "wall_first_sites_s": float(m.group(2)), "wall_first_fill_s": float(m.group(3))})
     m = re.search(r"PM_TIMING glf ingest: .*decode ahead ([\d.]+) s", stderr)
     if m:
         out["glf_decode_ahead_s"] = float(m.group(1))
@@ -165,8 +168,9 @@ def main():
                 for e, genv in [(e, g) for e in a.engines for g in a.glf_env]:
                     xe = dict(kv.split("=", 1) for kv in genv.split(",") if kv)
                     # (best of 5: the 64-site start-up runs varied 1.28-1.65 s between calls on one box)
-                    t_small = min(run_cli(base + ["-g", "test.gif", "--out_vcf", "s.vcf", "--engines", str(e)] + extra, small, extra_env=xe)[0]
-                                  for _ in range(5))
+                    small_best = min((run_cli(base + ["-g", "test.gif", "--out_vcf", "s.vcf", "--engines", str(e)] + extra, small,
+                                              extra_env=xe) for _ in range(5)), key=lambda x: x[0])
+                    t_small = small_best[0]
                     runs = [run_cli(base + ["-g", "test.gif", "--out_vcf", "g.vcf", "--engines", str(e)] + extra, tmp, extra_env=xe)
                             for _ in range(5)]
                     dt, r = min(runs, key=lambda x: x[0])
@@ -175,6 +179,7 @@ def main():
                            "sites_per_s_past_startup": a.sites / max(1e-9, dt - t_small), "records": len(bd) - 1,
                            "vcf_identical_to_blocks": ref_body is None or bd == ref_body}
                     rec.update(timing_fields(r.stderr))
+                    rec["small_timing"] = timing_fields(small_best[1].stderr)
                     if "wall_end_s" in rec:   # in the pipeline: the sites after the first batch over the wall time after it
                         rec["sites_per_s_pipeline"] = (a.sites - 4096) / max(1e-9, rec["wall_end_s"] - rec["wall_first_batch_s"])
                     m = re.search(r"PM_TIMING glf ingest: decode ([\d.]+) s, merge ([\d.]+) s, fill ([\d.]+) s", r.stderr)
