@@ -94,7 +94,9 @@ void ParallelSiteSource::joinAhead() {
 }
 
 void ParallelSiteSource::open(const Pedigree& ped, const std::string& glfIndexFile, int threads, int window) {
+  const double to0 = ing_now();
   auto index = read_glf_index(glfIndexFile);
+  const double to1 = ing_now();
   const int n = (int)ped.column_pid.size();
   files_ = std::vector<GlfFile>(n);
   qs_ = std::vector<Queue>(n);
@@ -114,10 +116,14 @@ void ParallelSiteSource::open(const Pedigree& ped, const std::string& glfIndexFi
     else path[j] = it->second;
   }
   std::vector<char> ok(n, 0);
+  const double to2 = ing_now();
   pool_->run((n + 31) / 32, [&](int c) {
     for (int j = c * 32; j < std::min(n, (c + 1) * 32); j++)
       if (!path[j].empty()) ok[j] = files_[j].open(path[j]);
   });
+  if (getenv("PM_TIMING"))
+    fprintf(stderr, "PM_TIMING glf open: index %.3f s, setup %.3f s, file opens %.3f s (%d threads)\n", to1 - to0, to2 - to1,
+            ing_now() - to2, pool_->threads());
   for (size_t f = 0; f < ped.families.size(); f++) {
     int valid = 0;
     for (int j = ped.fam_start[f]; j < ped.fam_start[f + 1]; j++) {
