@@ -45,6 +45,9 @@
 #ifndef PM_QD_WAVES
 #define PM_QD_WAVES 2   // QUAD plans: waves per SIMD the k_brent instantiation is compiled for (launch bounds, grid)
 #endif
+#ifndef PM_G4_LATE
+#define PM_G4_LATE 1   // lane_poly_r: the per-family g^4 factor applied once per lane as (g^4)^S
+#endif
 #ifndef PM_EPO_WAVES
 #define PM_EPO_WAVES 3   // the ep_only EP kernels (NF = 1): 167 VGPRs fit 3 waves per SIMD
 #endif
@@ -1326,8 +1329,10 @@ __device__ __forceinline__ void lane_poly_r(double r, double g4, const double (*
   am[0] = m0; ae[0] = e0;
 #pragma unroll
   for (int s = 0; s < S; s++) {
-    const double h = (NC == 4 ? fma(r, fma(r, fma(r, fma(r, a[s][0], a[s][1]), a[s][2]), a[s][3]), 1.0)
-                              : fma(r, fma(r, fma(r, fma(r, a[s][0], a[s][1]), a[s][2]), a[s][3]), a[s][NC - 1])) * g4;
+    // (PM_G4_LATE: the families' common factor g^4 applied once, as (g^4)^S after the product, instead of per family)
+    const double h0 = NC == 4 ? fma(r, fma(r, fma(r, fma(r, a[s][0], a[s][1]), a[s][2]), a[s][3]), 1.0)
+                              : fma(r, fma(r, fma(r, fma(r, a[s][0], a[s][1]), a[s][2]), a[s][3]), a[s][NC - 1]);
+    const double h = PM_G4_LATE ? h0 : h0 * g4;
     am[s % NA] = am[s % NA] * h;
     // renormalise after every second factor of an accumulator (and after the last): a nuclear family's
     // likelihood is >= ~1e-118 (PL <= 255 per person, HWE prior >= 1e-16), so two factors on a mantissa in
@@ -1347,6 +1352,17 @@ __device__ __forceinline__ void lane_poly_r(double r, double g4, const double (*
     }
   m = am[0];
   e = ae[0];
+  if constexpr (PM_G4_LATE) {   // (g^4)^S by squaring (g >= 1e-4 on Brent's bracket: >= 1e-256), one renormalisation
+    double p = 1.0, q = g4;
+#pragma unroll
+    for (int b = 1; b <= S; b <<= 1) {
+      if (S & b) p = p * q;
+      q = q * q;
+    }
+    int x;
+    m = frexp(m * p, &x);
+    e += x;
+  }
 }
 
 
