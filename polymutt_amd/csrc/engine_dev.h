@@ -1093,8 +1093,27 @@ __device__ __forceinline__ void hoist_poly4_dn_pf(const DevArgs& A, const int* s
 // first QD_AHEAD slots are fetched while this item's Brent runs.  A slot is then 13 conflict-free ds_read_b32
 // and 26 table lookups -- no per-byte address arithmetic, no per-family selects (only the partial last slot row
 // needs the phantom family).
-#define QB 3
-#define QD_AHEAD 2
+#ifndef QB
+#define QB 3          // slot buffers in the ring
+#endif
+#ifndef QD_AHEAD
+#define QD_AHEAD 2    // slots in flight ahead of the hoisting (< QB)
+#endif
+static_assert(QD_AHEAD >= 1 && QD_AHEAD < QB && QD_AHEAD <= 6, "QUAD ring geometry");
+// s_waitcnt immediate for vmcnt(n) alone (expcnt and lgkmcnt at their no-wait maxima; vmcnt's two high bits at 15:14)
+#define PM_VMCNT(n) (0x0F70 | ((n) & 0xF) | (((n) >> 4) << 14))
+template <int N> __device__ __forceinline__ void vm_wait() { __builtin_amdgcn_s_waitcnt(PM_VMCNT(N)); }
+// wait until at most j slots' DMA (3 instructions each) are outstanding (j folds to a constant in unrolled loops)
+__device__ __forceinline__ void vm_wait_slots(int j) {
+  switch (j) {
+    case 0: vm_wait<0>(); break;
+    case 1: vm_wait<3>(); break;
+    case 2: vm_wait<6>(); break;
+    case 3: vm_wait<9>(); break;
+    case 4: vm_wait<12>(); break;
+    default: vm_wait<15>(); break;
+  }
+}
 #define QSLOT 3072   // 10 planes x 256 B + the third DMA instruction's tail
 #define QWAVE (QB * QSLOT)
 
@@ -1186,8 +1205,8 @@ __device__ __forceinline__ void hoist_quad_t(const DevArgs& A, const ItemCtx& I,
   asm volatile("" : "+s"(qfull), "+s"(nfam), "+s"(npo));
 #pragma unroll
   for (int s = 0; s < S; s++) {
-    if (s + 1 < S) __builtin_amdgcn_s_waitcnt(0x0F70 | 3);   // vmcnt(3): slot s has landed
-    else __builtin_amdgcn_s_waitcnt(0x0F70);                   // vmcnt(0)
+    // slot s has landed: only the later slots' DMA (3 instructions each, at most QD_AHEAD - 1 of them) may be outstanding
+    vm_wait_slots(QD_AHEAD - 1 < S - 1 - s ? QD_AHEAD - 1 : S - 1 - s);
     __builtin_amdgcn_sched_barrier(0);
     const uint32_t* b = rw + (s % QB) * (QSLOT / 4);
     // byte j of a plane dword: person j of the family (0 father, 1 mother, 2 / 3 kids)
@@ -1837,7 +1856,7 @@ k_brent(DevArgs A, int list) {
     const int site = item >> 3, cfg = item & 7;
     int r;
     if constexpr (QD) {
-      __builtin_amdgcn_s_waitcnt(0x0F70 | 6);   // vmcnt(6): the ref dword has landed (slots 0, 1 and the next index may not)
+      __builtin_amdgcn_s_waitcnt(PM_VMCNT(3 * QD_AHEAD));   // the ref dword has landed (the item's first slots and the next index may not)
       __builtin_amdgcn_sched_barrier(0);
       r = __builtin_amdgcn_readfirstlane(((const volatile __attribute__((address_space(3))) uint8_t*)s_qaux)[site & 3]);
     } else r = A.ref[site];
