@@ -718,8 +718,33 @@ __device__ __forceinline__ void load_units(const int* su, int* uu) {
 // per region) are generated; the arithmetic and its order are hoist_nuc's.
 // NF = 3: the plan's every nuclear family is a trio (or the slot is empty): one kid, no second-kid loads or selects (an
 // empty slot's kid terms multiply lF = 0 and are then replaced by the phantom family)
+// PM_FAM_FACTORED (default): the quartic from quad_poly4's factored sums (the QUAD plan's form: equal to fold_poly(c9)
+// in real arithmetic, about half the operations) instead of hoist_nuc's nine products
+#ifndef PM_FAM_FACTORED
+#define PM_FAM_FACTORED 1
+#endif
+__device__ __forceinline__ void quad_poly4(const double (*D)[3], const double* lF, const double* lM, double* a);
 template <int NF = 0>
 __device__ __forceinline__ void fam_poly4(const uint32_t* by, int nn, const double* lk, double* a) {
+  if constexpr (PM_FAM_FACTORED) {
+    // kid q's (l11, l12, l22); a missing kid is (1, 1, 1): its likelihoodONEKid terms are then exactly 1 (the factors
+    // 2 and 4 of quad_poly4's sums are undone by its exact 0.5 / 0.25 scalings)
+    double D[2][3];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      const bool kid = NF == 3 ? q == 0 : 2 + q < nn;
+#pragma unroll
+      for (int k = 0; k < 3; k++) D[q][k] = kid ? lk[by[3 * (2 + q) + k]] : 1.0;
+    }
+    const bool fam = nn >= 2;   // (no parents: lF = 0, every coefficient +0, then the phantom family)
+    const double lF[3] = {fam ? lk[by[0]] : 0.0, fam ? lk[by[1]] : 0.0, fam ? lk[by[2]] : 0.0};
+    const double lM[3] = {lk[by[3]], lk[by[4]], lk[by[5]]};
+    quad_poly4(D, lF, lM, a);
+    if (nn == 0) {
+      a[0] = 1.0; a[1] = 4.0; a[2] = 6.0; a[3] = 4.0; a[4] = 1.0;
+    }
+    return;
+  }
   double kids[9];
 #pragma unroll
   for (int k = 0; k < 9; k++) kids[k] = 1.0;
