@@ -1036,7 +1036,9 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
         if (K->wave)
           HIP_TRY(hipModuleLaunchKernel(K->fn, E->n_cu * (K->blocks_per_cu > 0 ? K->blocks_per_cu : std::max(1, 16 / K->wpb)), 1, 1,
                                         64 * K->wpb, 1, 1, 0, E->stream, params, nullptr));
-        else HIP_TRY(hipModuleLaunchKernel(K->fn, E->n_cu * 8, 1, 1, 256, 1, 1, 0, E->stream, params, nullptr));
+        else   // (a persistent grid of the resident blocks: each thread loads its next unit's PL bytes ahead)
+          HIP_TRY(hipModuleLaunchKernel(K->fn, E->n_cu * (K->blocks_per_cu > 0 ? std::min(8, K->blocks_per_cu) : 8), 1, 1, 256, 1, 1, 0,
+                                        E->stream, params, nullptr));
       } else hipLaunchKernelGGL(hoist, dim3(hgrid), dim3(64 * E->hoist_waves), hlds, E->stream, A, list);
       HIP_TRY(hipGetLastError());
       if ((mrc = mark(E->es_events, false))) return mrc;

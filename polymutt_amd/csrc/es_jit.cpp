@@ -99,6 +99,9 @@ std::string shape_key(const Family& F) {
   return k;
 }
 
+int g_bapf = 0;           // es_hoist_jit: PL bytes of the thread's next (item, family) loaded ahead, 3 per person of the
+                          // largest family (0: off, the default -- PM_ES_BAPF=1 turns it on for families of <= 12)
+
 // One family shape's hoisting as a device function: the polynomial of FamilyLikelihoodES' BA peel in (f, g).
 std::string gen_family(const Family& F, int chrom, const double (*T)[27], const std::string& name, double* ops) {
   Gen G;
@@ -110,7 +113,8 @@ std::string gen_family(const Family& F, int chrom, const double (*T)[27], const 
     auto it = pen.find(key);
     if (it != pen.end()) return it->second;
     static const char* plane[3] = {"P11", "P12", "P22"};
-    std::string v = G.def(std::string("lk[") + plane[j] + "[p0 + " + std::to_string(i) + "]]");
+    std::string v = g_bapf ? G.def("lk[b[" + std::to_string(3 * i + j) + "]]")
+                           : G.def(std::string("lk[") + plane[j] + "[p0 + " + std::to_string(i) + "]]");
     pen[key] = v;
     return v;
   };
@@ -178,10 +182,13 @@ std::string gen_family(const Family& F, int chrom, const double (*T)[27], const 
   }
   // CalculateLikelihood_BA (:1013-1032): the final person's partials summed
   Poly L = G.add(G.add(P[fin][0], P[fin][1]), P[fin][2]);
-  std::string out = "__device__ __attribute__((noinline)) void " + name +
-                    "(const unsigned char* __restrict__ P11, const unsigned char* __restrict__ P12, "
-                    "const unsigned char* __restrict__ P22, int p0, const double* __restrict__ lk, double* __restrict__ out, "
-                    "int os, int dcap) {\n" + G.code;
+  std::string out = g_bapf ? "__device__ __forceinline__ void " + name +   // (inlined: b stays in registers)
+                                 "(const unsigned int* b, const double* __restrict__ lk, double* __restrict__ out, int os, int dcap) {\n" +
+                                 G.code
+                           : "__device__ __attribute__((noinline)) void " + name +
+                                 "(const unsigned char* __restrict__ P11, const unsigned char* __restrict__ P12, "
+                                 "const unsigned char* __restrict__ P22, int p0, const double* __restrict__ lk, double* __restrict__ out, "
+                                 "int os, int dcap) {\n" + G.code;
   for (int a = 0; a <= L.d; a++) out += "  out[" + std::to_string(a) + " * os] = " + (L.c[a].empty() ? "0.0" : L.c[a]) + ";\n";
   out += "  out[(dcap - 1) * os] = " + std::to_string(L.d) + ".0;\n}\n";
   *ops = (double)G.ops;
@@ -214,6 +221,56 @@ __device__ __forceinline__ void cfg_alleles(int cfg, int r, int* a1, int* a2) { 
 )";
 
 std::string gen_kernel(const std::vector<std::string>& shapes) {
+  if (g_bapf) {   // the next unit's PL bytes are loaded before this unit is computed (one HBM round trip hidden per unit)
+    std::string s = R"(
+extern "C" __global__ void __launch_bounds__(256) es_hoist_jit(Args A) {
+  __shared__ double lk[256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) lk[i] = A.lktab[i];
+  __syncthreads();
+  const int nItems = min(A.counts[A.list], A.it1);
+  if (nItems <= A.it0) return;
+  const long long units = (long long)(nItems - A.it0) * A.nslots;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  unsigned int bn[NB];
+  // unit uu's bytes b[3 i + j] = plane j (g11, g12, g22) of the family's person i (persons past the family: clamped reads
+  // inside the site's block, never used)
+  auto load = [&](long long uu) {
+    const int uq = (int)(uu / A.nslots), k = (int)(uu - (long long)uq * A.nslots);
+    const int item = A.items[A.it0 + uq];
+    const int site = item >> 3, cfg = item & 7, r = A.ref[site];
+    int a1, a2;
+    if (A.vcf) { a1 = r & 15; a2 = r >> 4; }
+    else if (cfg == 7) { a1 = A.res[(size_t)site * A.res_words + A.res_a1]; a2 = A.res[(size_t)site * A.res_words + A.res_a2]; }
+    else cfg_alleles(cfg, r, &a1, &a2);
+    const uint8_t* pl = A.pl + (size_t)site * A.np * 10;
+    const uint8_t* P[3] = {pl + (size_t)gi(a1, a1) * A.np, pl + (size_t)gi(a1, a2) * A.np, pl + (size_t)gi(a2, a2) * A.np};
+    const int p0 = A.slot_p0[k];
+#pragma unroll
+    for (int i = 0; i < NB / 3; i++) {
+      const int pi = min(p0 + i, A.np - 1);
+#pragma unroll
+      for (int j = 0; j < 3; j++) bn[3 * i + j] = P[j][pi];
+    }
+  };
+  long long u = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u < units) load(u);
+  for (; u < units; u += stride) {
+    unsigned int b[NB];
+#pragma unroll
+    for (int i = 0; i < NB; i++) b[i] = bn[i];
+    const int uq = (int)(u / A.nslots), k = (int)(u - (long long)uq * A.nslots);
+    const int e = A.slot_e[k], q = e / A.T;
+    double* out = A.coef + ((size_t)uq * A.max_ext + q) * A.dcap * A.T + (e - q * A.T);
+    const int sig = A.slot_sig[k];
+    if (u + stride < units) load(u + stride);
+    switch (sig) {
+)";
+    for (size_t i = 0; i < shapes.size(); i++)
+      s += "      case " + std::to_string(i) + ": " + shapes[i] + "(b, lk, out, A.T, A.dcap); break;\n";
+    s += "    }\n  }\n}\n";
+    for (size_t at; (at = s.find("NB")) != std::string::npos;) s.replace(at, 2, std::to_string(g_bapf));
+    return s;
+  }
   std::string s = R"(
 extern "C" __global__ void __launch_bounds__(256) es_hoist_jit(Args A) {
   __shared__ double lk[256];
@@ -1419,6 +1476,14 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
   const char* exd = getenv("PM_ES_XCD");
   g_xcd = !(exd && exd[0] == '0');
   if (g_pair) { g_regp = 0; g_regf = false; g_tr_regs = false; }   // (cross-lane reads by LDS only in pair mode)
+  {
+    int nmax = 0;
+    for (const Family& F : fams) nmax = std::max(nmax, F.n);
+    const char* ebp = getenv("PM_ES_BAPF");
+    // (opt-in, PM_ES_BAPF=1: measured slower, 0.105 vs 0.079 ms per config-4 launch -- 132 VGPRs, 3 waves per SIMD
+    // instead of 4, r05bp)
+    g_bapf = (!denovo && nmax <= 12 && ebp && ebp[0] == '1') ? 3 * nmax : 0;
+  }
   int ws = 1;
   std::vector<std::pair<int, int>> order;   // (shape, index into fams)
   for (size_t i = 0; i < fams.size(); i++) {
@@ -1568,9 +1633,9 @@ bool build(int device, int chrom, const std::vector<Family>& fams, const double 
     *err = "hipModuleGetFunction of the generated kernels failed";
     return false;
   }
-  if (denovo) {   // resident blocks per CU (VGPRs and LDS): the launch's grid
+  if (denovo || g_bapf) {   // resident blocks per CU (VGPRs and LDS): the launch's grid
     int nb = 0;
-    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, out->fn, 64 * out->wpb, 0) != hipSuccess) nb = 0;
+    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, out->fn, denovo ? 64 * out->wpb : 256, 0) != hipSuccess) nb = 0;
     out->blocks_per_cu = nb;
     if (getenv("PM_JIT_LAYOUT")) fprintf(stderr, "es_hoist_wave: wpb %d ws %d blocks/CU %d\n", out->wpb, out->ws, nb);
   }
