@@ -3032,8 +3032,16 @@ __device__ __forceinline__ void lean_row(const DevArgs& A, int row, LeanRow& r) 
   r.mono = R->maxidx == 0 ? 1 : 0;
   r.freq = r.mono ? 1 - A.theta : R->af;   // main.cpp:576-587
 }
+#ifndef PM_POST_WAVES
+#define PM_POST_WAVES 0   // k_posterior_lean: minimum waves per SIMD the register allocation must allow (0: the compiler's)
+#endif
+#if PM_POST_WAVES > 0
+#define PM_POST_WPE __attribute__((amdgpu_waves_per_eu(PM_POST_WAVES)))
+#else
+#define PM_POST_WPE
+#endif
 template <bool VCF>
-__global__ void __launch_bounds__(256) k_posterior_lean(DevArgs A) {
+__global__ void __launch_bounds__(256) PM_POST_WPE k_posterior_lean(DevArgs A) {
   __shared__ double s_lk[256];
   __shared__ double s_gq[101];
   extern __shared__ uint32_t s_fam[];   // [n_fam]
