@@ -86,16 +86,19 @@ def test_cpu_driver_reproduces_vcf_input_golden(cpu_driver, tmp_path):
 INGEST = os.path.join(os.path.dirname(EXAMPLE), "ingest")
 
 
-@pytest.mark.parametrize("io_threads,serial", [(1, False), (4, False), (4, True)])
-def test_cpu_driver_ragged_glf_matches_reference(cpu_driver, tmp_path, io_threads, serial):
+@pytest.mark.parametrize("io_threads,serial,env", [(1, False, {}), (4, False, {}), (4, True, {}),
+                                                   (4, False, {"PM_GLF_WINDOW": "64"}),
+                                                   (6, False, {"PM_GLF_WINDOW": "64", "PM_NO_DECODE_AHEAD": "1"}),
+                                                   (3, False, {"PM_GLF_WINDOW": "97", "PM_FILL_CHUNK": "5"})])
+def test_cpu_driver_ragged_glf_matches_reference(cpu_driver, tmp_path, io_threads, serial, env):
     """Parallel GLF ingest (host/ingest.cpp), pipelined or serial driver loop, on ragged GLFs -- per-person position sets, offset-0 repeats,
     indel records, an early section end, a person without a GLF key, two sections -- reproduces the VCF the
     reference wrote for the same files (tests/golden/ingest, tools/make_ingest_golden.py), for any thread
-    count."""
+    count, merge window (many windows, each merged and decoded ahead of the previous one's fill) and fill chunk."""
     out = tmp_path / "out.vcf"
     r = subprocess.run([cpu_driver, "-p", "test.ped", "-d", "test.dat", "-g", "test.gif", "--all_sites",
                         "--io_threads", str(io_threads), "--out_vcf", str(out)], cwd=INGEST, capture_output=True,
-                       text=True, timeout=300, env=dict(os.environ, **({"PM_SERIAL": "1"} if serial else {})))
+                       text=True, timeout=300, env=dict(os.environ, **({"PM_SERIAL": "1"} if serial else {}), **env))
     assert r.returncode == 0, r.stdout[-2000:]
     exp = [l for l in gzip.open(os.path.join(INGEST, "ref.vcf.body.gz"), "rt").read().splitlines() if l]
     assert _body(out) == exp
