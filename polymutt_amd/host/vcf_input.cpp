@@ -87,6 +87,7 @@ struct BlockReader {
   bool zeof = false;
   struct Line { const char* p; size_t n; int64_t off; };
   BlockReader(LineReader& lr, TaskPool* tp) : fh(lr.fh), pool(tp), base(lr.tell()) {
+    if (const char* eb = getenv("PM_VCF_BLOCK")) buf.resize(std::max<size_t>(64, strtoull(eb, nullptr, 10)));   // (tests: refills)
     if (gzdirect(fh) && !getenv("PM_VCF_GZREAD")) {
       fd = ::open(lr.path.c_str(), O_RDONLY);
       if (fd >= 0) posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);

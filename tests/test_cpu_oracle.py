@@ -104,6 +104,25 @@ def test_cpu_driver_ragged_glf_matches_reference(cpu_driver, tmp_path, io_thread
     assert _body(out) == exp
 
 
+@pytest.mark.parametrize("block,batch", [("512", "7"), ("4096", "64"), ("100000", "4096")])
+def test_cpu_driver_vcf_input_blocks_and_batches(cpu_driver, tmp_path, block, batch):
+    """--in_vcf (host/vcf_input.cpp) with small read blocks -- lines longer than the block (the buffer grows), partial
+    lines carried over a refill -- and small batches (the flusher's two batch buffers and the writer thread alternate
+    many times) reproduces the reference's example/testvcf.out.vcf body byte for byte, from the gzip input and from
+    the same text uncompressed (read by pread pieces)."""
+    src_gz = os.path.join(EXAMPLE, "testvcf.in.vcf.gz")
+    plain = tmp_path / "in.vcf"
+    plain.write_bytes(gzip.open(src_gz, "rb").read())
+    exp = [l for l in gzip.open(os.path.join(EXAMPLE, "testvcf.out.vcf.body.gz"), "rt").read().splitlines()]
+    for src in (src_gz, str(plain)):
+        out = tmp_path / "out.vcf"
+        r = subprocess.run([cpu_driver, "-p", "test.ped", "-d", "test.dat", "--in_vcf", src, "--out_vcf", str(out), "--batch", batch],
+                           cwd=EXAMPLE, capture_output=True, text=True, timeout=300, env=dict(os.environ, PM_VCF_BLOCK=block))
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        got = [l for l in out.read_text().splitlines() if not l.startswith("##")]
+        assert got == exp, src
+
+
 def test_vcf_fixed_point_formatting_matches_printf(tmp_path):
     """host/vcf_fmt.h (the allocation-free DS/GQ/DP/PL column formatter) prints exactly what glibc's printf
     prints: random dosages, exact decimal ties and their neighbours, signed zeros, subnormals."""
