@@ -820,6 +820,8 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
   int fin = -1;
   double nops = 0;
   std::vector<char> done(nst, 0);
+  double lane_slots = 0, step_ops = 0, step_eff = 1;
+  std::vector<double> eff2(nst, 0.0);   // packed type-2 runs: the run's lane occupancy (10 r of WL lanes)
   std::vector<double> frac1(nst, 1.0);   // type-1 steps: the fraction of the 100 pairs computed (founder-sparse rows)
   // persons whose partial the previous phase (a type-2 phase, lanes over states) left in registers: person -> (the
   // registers' name, the first lane); a following type-1 phase takes its coefficients by v_readlane instead of
@@ -831,18 +833,32 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
     fin = (St.x >> 24) & 255;
     if ((part == 1 && !leaf[kstep]) || (part == 2 && leaf[kstep])) continue;
     const bool emitted = done[kstep];   // (in a fused run of type-1 steps: counted here, emitted with the run's first)
-    {   // this step's FP64 operations (per item)
+    {   // this step's FP64 operations (per item), and the lane slots they occupy (PM_JIT_LAYOUT: the static lane
+        // occupancy -- a phase over E elements on a family's WL lanes runs ceil(E / WL) passes of WL lanes; a packed
+        // run of r type-2 steps fills 10 r of the WL lanes; PM_JIT_STEPS: per step)
       const int type = St.x & 255, slot = (St.y >> 8) & 255, create = (St.y >> 16) & 1;
-      const double ns = NS;
-      if (type == 1) nops += frac1[kstep] * ns * ns * ((g.a + 1) * ns + (create ? 0 : (g.a + 1) * (g.b + 1)));
-      else if (type == 2) {
+      const double ns = NS, before = nops;
+      auto occ = [&](double E, double lanes) { return E / (std::ceil(E / lanes) * lanes); };
+      double eff = 1.0;
+      if (type == 1) {
+        nops += frac1[kstep] * ns * ns * ((g.a + 1) * ns + (create ? 0 : (g.a + 1) * (g.b + 1)));
+        eff = occ(frac1[kstep] * ns * ns, g_wl);
+      } else if (type == 2) {
         const int ds = g.a + g.b;
         if (pristine[kstep]) nops += ns * ((double)pterms((St.x >> 8) & 255).size() * (slot == 255 ? 1 : (g.b + 1)) + (g.c + 1) * (ds + 1));
         else nops += ns * ((slot == 255 ? (ds + 1) * ns : ns * (g.a + 1) * (g.b + 1)) + (g.c + 1) * (ds + 1));
+        eff = eff2[kstep] > 0 ? eff2[kstep] : occ(mc ? M * ns : ns, g_wl);   // (a packed run's first step: corrected below)
       } else {
         const int dw = g.a + g.b + g.c;
-        nops += ns * ns * (g.a + 1) * (g.b + 1) * (g.c + 1) * (slot == 255 ? 1 : 2) + ns * (ns * ns * (dw + 1) + (g.e + 1) * (dw + 1));
+        const double o1 = ns * ns * (g.a + 1) * (g.b + 1) * (g.c + 1) * (slot == 255 ? 1 : 2), o2 = ns * (ns * ns * (dw + 1) + (g.e + 1) * (dw + 1));
+        nops += o1 + o2;
+        eff = (o1 + o2) / (o1 / occ(ns * ns, g_wl) + o2 / occ(mc ? M * ns : ns, g_wl));
       }
+      lane_slots += (nops - before) / eff;
+      step_ops = nops - before;
+      step_eff = eff;
+      if (getenv("PM_JIT_STEPS"))
+        fprintf(stderr, "  step %s part %d M %d k %d type %d ops %.0f eff %.3f\n", name.c_str(), part, M, kstep, type, step_ops, eff);
     }
     const int type = St.x & 255, from0 = (St.x >> 8) & 255, from1 = (St.x >> 16) & 255, to0 = (St.x >> 24) & 255;
     const int slot = (St.y >> 8) & 255, create = (St.y >> 16) & 1, fa2mo = (St.y >> 17) & 1;
@@ -1011,6 +1027,10 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
           if (!indep) break;
           run.push_back(k2);
         }
+      }
+      if (run.size() > 1) {
+        for (int k2 : run) eff2[k2] = (double)NS * run.size() / g_wl;
+        lane_slots += step_ops / eff2[kstep] - step_ops / step_eff;
       }
       std::string OF = PO(sf), OT = PO(stt), OM = slot == 255 ? "" : MOf(slot), pre;
       if (run.size() > 1) {
@@ -1188,6 +1208,9 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
   }
   const int D = dP[fin];
   *ops = M * (nops + (part == 1 ? 0.0 : (double)(D + 1) * NS));
+  if (getenv("PM_JIT_LAYOUT"))
+    fprintf(stderr, "occupancy %s part %d WL %d: %.0f FP64 ops / %.0f lane slots = %.3f\n", name.c_str(), part, g_wl, nops, lane_slots,
+            lane_slots > 0 ? nops / lane_slots : 0.0);
   if (part != 1) {
     code += lanes(D + 1, "a", "    double s = 0.0;\n#pragma unroll\n    for (int i = 0; i < " + nsS + "; i++) s += W[" + PO(fin) + " + i * " +
                                   S(capP[fin]) + " + a];\n    out[" + std::string(mc ? "c * ostr + " : "") + "(size_t)a * os] = s;\n");

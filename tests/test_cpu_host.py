@@ -362,8 +362,11 @@ def test_schedule_compiler_builds_every_class(tmp_path, shape):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "polymutt_amd"), "../tests/native/build/jit_check"], check=True)
     pm.synth_write_dataset(str(tmp_path), shape, 5, 1, 3)
     r = subprocess.run([exe, str(tmp_path / "test.dat"), str(tmp_path / "test.ped"), "--emit", str(tmp_path / "k.hip")],
-                       capture_output=True, text=True, timeout=300)
+                       capture_output=True, text=True, timeout=300, env=dict(os.environ, PM_JIT_LAYOUT="1"))
     assert r.returncode == 0, r.stdout + r.stderr
+    # the static lane occupancy per generated function (useful FP64 element-ops / issued lane slots), in (0, 1]
+    occ = [l.split() for l in r.stderr.splitlines() if l.startswith("occupancy")]
+    assert occ and all(0.0 < float(l[-1]) <= 1.0 for l in occ), r.stderr[-2000:]
     lines = [l.split() for l in r.stdout.splitlines() if l.startswith("class")]
     assert [int(l[1]) for l in lines] == [0, 1, 2, 3] * 3   # bi-allelic engines, --denovo (grouped tasks, then all)
     assert all(int(l[3]) == 1 and int(l[5]) == 5 and int(l[9]) > 0 for l in lines), r.stdout   # one shape, 5 families
