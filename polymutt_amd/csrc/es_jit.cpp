@@ -521,6 +521,11 @@ bool g_fence = true;      // PM_ES_FENCE=0: wave_sync without the wavefront-scop
 bool g_xcd = true;        // PM_ES_XCD=0: units dealt to the blocks in plain order
 bool g_no_penp = false;   // PM_ES_PENP=0: leaf offspring partials stored and read from the workspace
 int g_wl = 64;
+// PM_ES_FACT=1 (opt-in experiment): a dense 10-state type-1 run through T10dn = T10 * M (SetTransmissionMatrix_denovo
+// :787-810) -- P' = M P per offspring coefficient (lanes over (genotype, coefficient)), then per pair 0.25 x the sum
+// of P' at its four Mendelian children, instead of sum_k T10dn(e, k) P(k): the same value in real arithmetic, a
+// different rounding order (not the reference's), ~3x fewer operations and no per-lane transmission-row loads
+bool g_fact = false;
 
 struct WaveGen {
   std::string code;
@@ -677,6 +682,14 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
       if (sp.compact) crows[(F.steps[k].y >> 8) & 255] = 10 * (int)sp.terms.size();
     }
   const int M = part == 2 ? std::max(1, multi) : 1;
+  if (g_fact && NS == 10 && M == 1)   // (PM_ES_FACT: the P' rows of a dense type-1 run in the temporaries' region)
+    for (int k = 0; k < nst; k++) {
+      if (!inpart(k) || (F.steps[k].x & 255) != 1) continue;
+      const std::vector<int> run = run_of(k);
+      int sz = 0;
+      for (int k2 : run) sz += 10 * (sd[k2].a + 1);
+      tmp = std::max(tmp, sz);
+    }
   std::map<int, int> leafs;   // the marriage slots the leaf steps write
   for (int k = 0; k < nst; k++)
     if (leaf[k]) leafs[(F.steps[k].y >> 8) & 255] = 1;
@@ -908,6 +921,24 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
           for (int k2 : run) frac1[k2] = fr;
         }
         const int npair = sparse ? 1 : (100 + g_wl - 1) / g_wl;
+        bool fact = g_fact && !sparse;
+        for (int k2 : run)
+          if (regp.count((F.steps[k2].x >> 8) & 255)) fact = false;
+        std::vector<int> pfo(run.size(), 0);   // PM_ES_FACT: each step's P' rows at TB + pfo[q]
+        if (fact) {   // P'(m, a) = sum_k M(m, k) P(k, a); M's row m is T10dn's row of the parent pair (x x, y y), m = {x, y}
+          int at = 0;
+          for (size_t q = 0; q < run.size(); q++) {
+            const int offq = (F.steps[run[q]].x >> 8) & 255, ga = sd[run[q]].a, na = ga + 1;
+            pfo[q] = at;
+            const std::string P = penp[offq] ? "PEN[k * " + S(n) + " + " + S(offq) + "]"
+                                             : "W[" + PO(offq) + " + k * " + S(capP[offq]) + " + a]";
+            code += lanes(10 * na, "x", "    const int m = x / " + S(na) + ", a = x - m * " + S(na) + ";\n    (void)a;\n"
+                          "    const double* Mr = t10dn + kMrow[m] * 10;\n    double s = 0.0;\n#pragma unroll\n"
+                          "    for (int k = 0; k < 10; k++) s = fma(Mr[k], " + P + ", s);\n    W[" + TBs + " + " + S(at) + " + x] = s;\n");
+            at += 10 * na;
+          }
+          code += "  wave_sync();\n";
+        }
         std::string c1 = "  {\n";
         if (sparse) {
           const std::string gq[3] = {"g11", "g12", "g22"};
@@ -925,8 +956,21 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
             for (int a = 0; a <= ga; a++) c1 += "    s" + S(pr) + "_" + S(q) + "[" + S(a) + "] = 0.0;\n";
           }
         }
+        if (fact) {   // per pair: 0.25 x the P' values at its four Mendelian children (packed bytes, kMend)
+          for (int pr = 0; pr < npair; pr++)
+            c1 += "    const unsigned cm" + S(pr) + " = kMend[" + (pr ? "e" + S(pr) + "c" : std::string("lane")) + "];\n";
+          for (size_t q = 0; q < run.size(); q++) {
+            const int ga = sd[run[q]].a, na = ga + 1;
+            for (int pr = 0; pr < npair; pr++)
+              for (int a = 0; a <= ga; a++) {
+                auto pf = [&](int t) { return "W[" + TBs + " + " + S(pfo[q] + a) + " + " + S(na) + " * ((cm" + S(pr) + " >> " + S(8 * t) + ") & 255)]"; };
+                c1 += "    s" + S(pr) + "_" + S(q) + "[" + S(a) + "] = 0.25 * (((" + pf(0) + " + " + pf(1) + ") + " + pf(2) + ") + " + pf(3) + ");\n";
+              }
+          }
+        }
         // (k unrolled by 2 only: fully unrolled, the scheduler hoists every offspring coefficient's LDS read and
         // spills)
+        if (!fact) {
         c1 += "#pragma unroll 2\n    for (int k = 0; k < 10; k++) {\n";
         if (sparse) c1 += "      const double t0 = t10dn[e * 10 + k];\n";
         else if (npair > 2) {   // (pair mode: the rows of this lane's four pairs)
@@ -955,6 +999,7 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
           }
         }
         c1 += "    }\n";
+        }
         // per pair: each marriage partial chained through its steps in registers, one write
         for (int pr = 0; pr < npair; pr++) {
           const std::string sp = "s" + S(pr) + "_", e = spi.compact ? "lane" : sparse ? "e" : pr ? "e" + S(pr) : "lane";
@@ -1253,6 +1298,23 @@ __device__ __forceinline__ void wave_sync() {
   asm volatile("" ::: "memory");
 }
 )";
+  if (g_fact) {   // PM_ES_FACT: the four Mendelian children of parent pair e = i * 10 + j (bytes), and the pair (x x, y y)
+                  // whose only child is genotype m (its T10dn row is M's row m)
+    auto gi = [](int b1, int b2) { return b1 < b2 ? (b1 - 1) * (10 - b1) / 2 + (b2 - b1) : (b2 - 1) * (10 - b2) / 2 + (b1 - b2); };
+    int al[10][2], at = 0;
+    for (int x = 1; x <= 4; x++)
+      for (int y = x; y <= 4; y++) { al[gi(x, y)][0] = x; al[gi(x, y)][1] = y; at++; }
+    s += "__device__ const unsigned kMend[100] = {";
+    for (int i = 0; i < 10; i++)
+      for (int j = 0; j < 10; j++) {
+        const int c[4] = {gi(al[i][0], al[j][0]), gi(al[i][0], al[j][1]), gi(al[i][1], al[j][0]), gi(al[i][1], al[j][1])};
+        s += std::to_string((unsigned)c[0] | (unsigned)c[1] << 8 | (unsigned)c[2] << 16 | (unsigned)c[3] << 24) + "u,";
+      }
+    s += "};\n__device__ const int kMrow[10] = {";
+    for (int m = 0; m < 10; m++) s += std::to_string(gi(al[m][0], al[m][0]) * 10 + gi(al[m][1], al[m][1])) + ",";
+    s += "};\n";
+    (void)at;
+  }
   s += "__device__ __forceinline__ int shape_n(int sig) {\n  switch (sig) {\n";
   for (size_t i = 0; i < shape_ns.size(); i++) s += "    case " + std::to_string(i) + ": return " + std::to_string(shape_ns[i]) + ";\n";
   s += "  }\n  return 0;\n}\n";
@@ -1489,6 +1551,8 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
   g_regf = !(erf && erf[0] == '0');
   const char* eex = getenv("PM_ES_EXPT");
   g_expt = eex ? atoi(eex) : 0;
+  const char* efc = getenv("PM_ES_FACT");
+  g_fact = denovo != 0 && efc && efc[0] == '1';
   const char* epr = getenv("PM_ES_PAIR");
   g_pair = denovo != 0 && !(epr && epr[0] == '0') && pps == 3;
   g_wl = g_pair ? 32 : 64;
