@@ -756,7 +756,8 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
     if (L == 1) LSZ = off;
   }
   const int TB = off, NSZ = off + tmp - LSZ;
-  *ws_doubles = part == 1 ? LSZ : LSZ + M * NSZ;   // (the leaf prefix writes its own regions only)
+  // (the leaf prefix writes its own regions only -- and with PM_ES_FACT its P' rows in the temporaries' region)
+  *ws_doubles = part == 1 ? (g_fact && NS == 10 ? TB + tmp : LSZ) : LSZ + M * NSZ;
   if (getenv("PM_JIT_LAYOUT")) {
     fprintf(stderr, "layout %s NS %d part %d top %d: LSZ %d NSZ %d tmp %d ws %d |", name.c_str(), NS, part, (int)top, LSZ, NSZ, tmp, *ws_doubles);
     for (int i = 0; i < n; i++) fprintf(stderr, " p%d:%d%s", i, (!regf[i] && !regn[i]) ? NS * capP[i] : 0, leafp[i] ? "L" : "");
