@@ -1068,10 +1068,14 @@ static int run_pipeline(pm_engine* E, int n, const uint8_t* pl, const uint32_t* 
   {   // persons per lane of k_prep: vector loads when n_person allows; the reference's serial mono order in EXACT
     const int np = E->n_person;
     int vmax = 8;   // measured best on 1000 quads (16 and 4 within 1%)
-    void (*prep)(DevArgs) = E->par.numerics == PM_NUM_EXACT ? k_prep<1, true>
+    void (*prep)(DevArgs, int) = E->par.numerics == PM_NUM_EXACT ? k_prep<1, true>
                           : (np % 16 == 0 && vmax >= 16) ? k_prep<16, false> : (np % 8 == 0 && vmax >= 8) ? k_prep<8, false>
                           : (np % 4 == 0 && vmax >= 4) ? k_prep<4, false> : k_prep<1, false>;
-    hipLaunchKernelGGL(prep, dim3((n + 4 * PREP_SPW - 1) / (4 * PREP_SPW)), dim3(256), 0, E->stream, A);
+    // sites per wave: PREP_SPW (PM_PREP_SPW = 1..8 overrides it; fewer sites per wave on config 4's 16 384-site
+    // batches measured slower: 20.3 -> 19.7 M sites/s at 1, config 5 within noise, profiles/r05sp_ab_prep_spw.txt)
+    int spw = PREP_SPW;
+    if (const char* s = getenv("PM_PREP_SPW"); s && *s) spw = std::max(1, std::min(PREP_SPW, atoi(s)));
+    hipLaunchKernelGGL(prep, dim3((n + 4 * spw - 1) / (4 * spw)), dim3(256), 0, E->stream, A, spw);
   }
   HIP_TRY(hipGetLastError());
   int rc;

@@ -2218,13 +2218,14 @@ __device__ __forceinline__ void load_dwords(const uint32_t* p, uint32_t* out) {
 // (NucFamGenotypeLikelihood.cpp:502-546).  SERIAL (PM_NUM_EXACT): the mono sum -PL/10 is accumulated in
 // the reference's person order (VEC = 1, lanes ascending via ballot); otherwise it is -(Sum PL)/10 from
 // the exact integer sum -- correctly rounded, within ~1e-14 relative of the serial sum.
-// PREP_SPW sites per wave, one after the other (a block of 4 waves takes 4 x PREP_SPW consecutive sites), so the
+// spw (<= PREP_SPW) sites per wave, one after the other (a block of 4 waves takes 4 x spw consecutive sites), so the
 // block-level work -- one returning atomic that reserves the block's Brent items (the sites' items then go to
-// consecutive slots in site order) and at most 9 counter atomics -- is shared by 4 x PREP_SPW sites.  (One
-// same-address atomic per site serialised k_prep: 262 144 returning atomics on counts[0] per batch.)
+// consecutive slots in site order) and at most 9 counter atomics -- is shared by 4 x spw sites.  (One
+// same-address atomic per site serialised k_prep: 262 144 returning atomics on counts[0] per batch.)  spw is a
+// launch argument (engine.hip: PREP_SPW unless PM_PREP_SPW says otherwise).
 #define PREP_SPW 8
 template <int VEC, bool SERIAL>
-__global__ void __launch_bounds__(256) k_prep(DevArgs A) {
+__global__ void __launch_bounds__(256) k_prep(DevArgs A, int spw) {
   __shared__ unsigned long long s_c[9];
   __shared__ double s_lk[256];
   __shared__ double s_M[100];
@@ -2241,9 +2242,9 @@ __global__ void __launch_bounds__(256) k_prep(DevArgs A) {
   const int list = (A.vcf || !A.unrelated) ? 0 : 1;
   const int k0 = A.vcf ? 1 : A.unrelated ? 1 : (A.denovo && !A.mono_dn) ? 0 : 1;   // first cfg (cfg 0: de novo mono)
   const int nit_called = A.vcf ? 1 : A.unrelated ? 3 : 4 - k0;
-  const int site0 = blockIdx.x * 4 * PREP_SPW;
-  for (int j = 0; j < PREP_SPW; j++) {
-    const int sl = w * PREP_SPW + j, site = site0 + sl;
+  const int site0 = blockIdx.x * 4 * spw;
+  for (int j = 0; j < spw; j++) {
+    const int sl = w * spw + j, site = site0 + sl;
     bool valid = false;
     if (site < A.n) {
       const int rb = A.ref[site];
@@ -2375,14 +2376,14 @@ __global__ void __launch_bounds__(256) k_prep(DevArgs A) {
   __syncthreads();
   if (threadIdx.x == 0) {   // the block's items: one reservation, then consecutive slots in site order
     int t = 0;
-    for (int i = 0; i < 4 * PREP_SPW; i++) { s_pre[i] = t; t += s_nit[i]; }
+    for (int i = 0; i < 4 * spw; i++) { s_pre[i] = t; t += s_nit[i]; }
     s_base = t ? atomicAdd(&A.counts[list], t) : 0;
     for (int i = 0; i < 9; i++) if (s_c[i]) atomicAdd(&A.counters[i], s_c[i]);
   }
   __syncthreads();
   // lane i of wave w writes item i of each of its sites (at most 4 items per site)
-  for (int j = 0; j < PREP_SPW; j++) {
-    const int sl = w * PREP_SPW + j;
+  for (int j = 0; j < spw; j++) {
+    const int sl = w * spw + j;
     if (lane < s_nit[sl]) A.items[list][s_base + s_pre[sl] + lane] = ((site0 + sl) << 3) | (lane + k0);
   }
 }
