@@ -612,9 +612,15 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
       HIP_TRY(hipMemcpy(E->d_poly_start, poly_start.data(), sizeof(int) * poly_start.size(), hipMemcpyHostToDevice));
       if (!poly_lay.empty()) HIP_TRY(hipMemcpy(E->d_poly_lay, poly_lay.data(), sizeof(int) * poly_lay.size(), hipMemcpyHostToDevice));
       if (!poly_deg.empty()) HIP_TRY(hipMemcpy(E->d_poly_deg, poly_deg.data(), sizeof(int) * poly_deg.size(), hipMemcpyHostToDevice));
-      // hoisted coefficients of a chunk of items: <= 1 GiB, at most every item a batch can enqueue in one list (4 per site)
+      // hoisted coefficients of a chunk of items: every item a batch can enqueue in one list (4 per site, rounded up
+      // to whole 12-item groups), <= 4 GiB.  launch_brent runs hoisting + Brent once per chunk of the list's largest
+      // possible item count (4 per site), so a chunk even 4 items short of it costs an extra pair of launches per
+      // list over items that do not exist (config 4's 16 384-site batches: 65 532-item chunks for 65 536, two empty
+      // pairs per step).  PM_ES_CHUNK = items per chunk caps it (experiments).
       const size_t per_item = (size_t)std::max({E->max_ext * E->T, E->max_ext1 * std::max(1, E->T1), 1}) * E->poly_dcap * sizeof(double);
-      E->es_chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)4 * std::max(1, max_batch), ((size_t)1 << 30) / per_item));
+      const size_t want = ((size_t)4 * std::max(1, max_batch) + 11) / 12 * 12;
+      E->es_chunk = (int)std::max<size_t>(1, std::min<size_t>(want, ((size_t)1 << 32) / per_item));
+      if (const char* s = getenv("PM_ES_CHUNK"); s && atoi(s) > 0) E->es_chunk = std::min(E->es_chunk, atoi(s));
       if (E->es_chunk >= 12) E->es_chunk -= E->es_chunk % 12;   // whole sites of lists 0 and 1 per chunk (grouped tasks)
       DALLOC(E->d_es_coef, (size_t)E->es_chunk * per_item / sizeof(double));
     }
