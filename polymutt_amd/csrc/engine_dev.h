@@ -2703,6 +2703,9 @@ __device__ void d_kid_geno(int chrom, const uint8_t* pl, int np, const double* l
   out[0] = G11; out[1] = G12; out[2] = G22;
 }
 
+#ifndef PM_POST_ZINIT
+#define PM_POST_ZINIT 1   // lean_nuc_post's kid sums start from their first term (0: from 0.0, the former code)
+#endif
 // The 12 PL bytes of a nuclear family of <= 4 persons: (g11, g12, g22) of father, mother and the two kid slots
 // (a trio's second kid slot repeats its kid; every read stays inside the family)
 __device__ __forceinline__ void lean_fam_bytes(const uint8_t* pl, int np, int p0, int n, int g11, int g12, int g22, uint32_t* by) {
@@ -2773,6 +2776,9 @@ __device__ __forceinline__ void lean_nuc_post(const DevArgs& A, const double* s_
     const double m11 = kl[me][0], m12 = kl[me][1], m22 = kl[me][2];
     const double o11 = kl[other][0], o12 = kl[other][1], o22 = kl[other][2];
     double g[3] = {0.0, 0.0, 0.0};
+    // PM_POST_ZINIT: each sum starts from its first term instead of 0.0 + term (every term is +0 or positive, so
+    // 0.0 + v == v bit for bit; the compiler may not drop the add itself without no-signed-zeros)
+    bool h[3] = {!PM_POST_ZINIT, !PM_POST_ZINIT, !PM_POST_ZINIT};
 #pragma unroll
     for (int k = 0; k < 9; k++) {
       double lo, q11 = 0, q12 = 0, q22 = 0;   // the other kid's likelihood, this kid's genotype terms (d_kid_geno's switch)
@@ -2787,9 +2793,9 @@ __device__ __forceinline__ void lean_nuc_post(const DevArgs& A, const double* s_
       }
       const double w = wk[k];
       // kid order: (1.0 * f_kid2) * f_kid3 -- one product, whichever kid carries q
-      if (!z11) g[0] = g[0] + (two ? q11 * lo : q11) * w;
-      if (!z12) g[1] = g[1] + (two ? q12 * lo : q12) * w;
-      if (!z22) g[2] = g[2] + (two ? q22 * lo : q22) * w;
+      if (!z11) { const double v = (two ? q11 * lo : q11) * w; g[0] = h[0] ? g[0] + v : v; h[0] = true; }
+      if (!z12) { const double v = (two ? q12 * lo : q12) * w; g[1] = h[1] ? g[1] + v : v; h[1] = true; }
+      if (!z22) { const double v = (two ? q22 * lo : q22) * w; g[2] = h[2] ? g[2] + v : v; h[2] = true; }
     }
     const double sum = g[0] + g[1] + g[2];
     if constexpr (VCF) {
