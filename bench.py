@@ -70,9 +70,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--families", type=int, default=1000)
-    ap.add_argument("--shape", choices=["quad", "trio", "ext10", "mixed"], default="quad",
-                    help="quad/trio: BASELINE configs 2-3; ext10: config 4 (3-generation pedigrees, ES peeling); "
-                         "mixed: trios and quads (config 5 with --vcf)")
+    ap.add_argument("--shape", choices=["quad", "trio", "ext10", "extmix", "mixed"], default="quad",
+                    help="quad/trio: BASELINE configs 2-3; ext10: config 4 (3-generation pedigrees, ES peeling), one "
+                         "10-member shape; extmix: config 4 at its stated 8-12-member range (ext10, roof, roof2, ext12, "
+                         "ext11 round-robin); mixed: trios and quads (config 5 with --vcf)")
     ap.add_argument("--vcf", action="store_true", help="BASELINE config 5: the --in_vcf engine mode (one Brent per site)")
     ap.add_argument("--denovo", dest="denovo", action="store_true", default=True,
                     help="BASELINE config 3: --denovo MutationModel (default)")
@@ -331,7 +332,7 @@ def main():
     import polymutt_amd as pm
     from polymutt_amd.shard import allreduce_counters, max_over_ranks
 
-    kids = {"quad": 2, "trio": 1, "mixed": 2, "ext10": 2}[args.shape]
+    kids = {"quad": 2, "trio": 1, "mixed": 2, "ext10": 2, "extmix": 2}[args.shape]
     if args.shape in ("quad", "trio"):
         ped = nuclear_pedigree(pm, args.families, kids)
         ped_keep = None

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 6   /* 6: pm_engine_run_vcf (round 5); 5: submit / collect / host_alloc / host_free */
+#define PM_ABI_VERSION 7   /* 7: pm_engine_stuck_site, partial batches on PM_EBRENT; 6: pm_engine_run_vcf; 5: submit / collect */
 #define PM_NCFG 7           /* varllk slots: 0 mono, 1 ref/ts, 2 ref/tv1, 3 ref/tv2, 4 ts/tv1, 5 ts/tv2, 6 tv1/tv2 */
 
 typedef enum { PM_OK = 0, PM_EINVAL = -1, PM_EHIP = -2, PM_ENOMEM = -3, PM_EBRENT = -4, PM_EPED = -5 } pm_status;
@@ -209,16 +209,23 @@ int pm_engine_begin_section(pm_engine *eng, int32_t chrom);
  * Outputs are host pointers: res[n]; calls[n_rows * n_person] receives one row per written record
  * (emit == 1; row index = res[i].call_row, rows numbered in site order, -1 for every other site: a
  * suppressed de novo record, emit == 2, prints nothing and gets no row); *n_rows is set to the row count.
- * Counters accumulate into the section totals.  Synchronous. */
+ * Counters accumulate into the section totals.  Synchronous.
+ * PM_EBRENT: some site's Brent maximisation hit ITMAX (ScalarMinimizer::Brent's numerror, core/MathGold.cpp:98,175,
+ * where the reference's site loop ends the run).  res[] is still written for the whole batch, and the sites before the
+ * first stuck one -- pm_engine_stuck_site -- are complete: their genotype rows are the first *n_rows rows (*n_rows
+ * counts only their rows), as the reference had written their records (NucFamGenotypeLikelihood.cpp:1829, fflush per
+ * record) before exiting at the stuck site.  The section counters then include the whole batch. */
 int pm_engine_run(pm_engine *eng, int32_t n, const uint8_t *pl, const uint32_t *dm, const uint8_t *ref,
                   int32_t inputs_on_device, pm_site_result *res, pm_geno_call *calls, int32_t *n_rows);
 
 /* vcf_mode engines only: pm_engine_run on host inputs (no depth plane) with the genotype rows returned in the
  * compact pm_vcf_call form the device writes -- best / GQ / label, all FamilyLikelihoodSeq_VCF::OutputVCF
  * (src/FamilyLikelihoodSeq_VCF.cpp:412-521) prints -- instead of widened into pm_geno_call rows: a quarter of
- * the bytes, copied straight into `calls` (page-locked from pm_host_alloc: an asynchronous copy).  Replaces, for
- * the --in_vcf path, the per-record FamilyLikelihoodSeq_VCF::FillPenetrance -> CalcLikelihood -> OutputVCF calls of
- * PedVCF::VarCallFromVCF (src/PedVCF.cpp:103-160).  PM_EINVAL on an engine created without vcf_mode. */
+ * the bytes, copied straight into `calls` (one synchronous device-to-host copy; page-locked `calls` from
+ * pm_host_alloc copy at full PCIe rate).  Replaces, for the --in_vcf path, the per-record
+ * FamilyLikelihoodSeq_VCF::FillPenetrance -> CalcLikelihood -> OutputVCF calls of PedVCF::VarCallFromVCF
+ * (src/PedVCF.cpp:103-160).  PM_EINVAL on an engine created without vcf_mode, or while a pm_engine_submit batch
+ * has not been collected (that batch stays pending).  PM_EBRENT as for pm_engine_run. */
 int pm_engine_run_vcf(pm_engine *eng, int32_t n, const uint8_t *pl, const uint8_t *ref, pm_site_result *res,
                       pm_vcf_call *calls, int32_t *n_rows);
 
@@ -231,6 +238,12 @@ int pm_engine_run_vcf(pm_engine *eng, int32_t n, const uint8_t *pl, const uint8_
  * asynchrony itself.) */
 int pm_engine_submit(pm_engine *eng, int32_t n, const uint8_t *pl, const uint32_t *dm, const uint8_t *ref);
 int pm_engine_collect(pm_engine *eng, pm_site_result *res, pm_geno_call *calls, int32_t *n_rows);
+
+/* After a batch returned PM_EBRENT (pm_engine_run, _run_vcf, _collect or _sync): *site = the batch index of the first
+ * site whose Brent hit ITMAX, i.e. the number of leading sites whose results and rows are complete; -1 when the last
+ * finished batch had none.  (core/MathGold.cpp:98,175: the reference exits at that site, its earlier records
+ * written.)  The environment variable PM_TEST_ITMAX, read at pm_engine_create, lowers ITMAX (200) for tests. */
+int pm_engine_stuck_site(pm_engine *eng, int32_t *site);
 
 /* Page-locked host memory for pm_engine_submit's inputs and the result rows (H2D/D2H at full PCIe rate). */
 int pm_host_alloc(uint64_t bytes, void **h_ptr);

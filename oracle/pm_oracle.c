@@ -46,6 +46,7 @@ struct pmo_ctx {
   pm_peel_step *steps;
   pm_params par;
   int chrom, isX, isY, isMT;
+  int itmax;   /* ITMAX (200); PM_TEST_ITMAX lowers it, as for the engine (failure-path tests) */
   double prior;                /* GetPolyPrior() of the section */
   double lktab[256];           /* core/BaseQualityHelper.cpp:13 */
   double M[10][10];            /* GenotypeMutationModel::genoMutMatrix */
@@ -465,7 +466,7 @@ static int optimize(pmo_ctx *c, lkobj *o) {
   if (a > cc) { temp = a; a = cc; cc = temp; temp = fa; fa = fc; fc = temp; }
   double min = b, fmin = fb, w = b, v = b, fw = fb, fv = fb, delta = 0.0, u, fu, d = 0.0;
   (void)fa; (void)fc;
-  for (int iter = 1; iter <= ITMAX; iter++) {
+  for (int iter = 1; iter <= c->itmax; iter++) {
     double middle = 0.5 * (a + cc);
     double tol1 = tol * fabs(min) + ZEPS;
     double tol2 = 2.0 * tol1;
@@ -892,6 +893,9 @@ static int vcf_site(pmo_ctx *c, const uint8_t *pl, int32_t ref_alt, pm_site_resu
 pmo_ctx *pmo_create(const pm_pedigree *ped, const pm_params *par) {
   pmo_ctx *c = (pmo_ctx *)calloc(1, sizeof(pmo_ctx));
   c->ped = *ped; c->par = *par;
+  c->itmax = ITMAX;
+  const char *eit = getenv("PM_TEST_ITMAX");
+  if (eit && atoi(eit) > 0 && atoi(eit) < ITMAX) c->itmax = atoi(eit);
   int nf = ped->n_fam, np = ped->n_person, ns = ped->peel_start ? ped->peel_start[nf] : 0;
   c->fam_start = malloc(sizeof(int32_t) * (nf + 1)); memcpy(c->fam_start, ped->fam_start, sizeof(int32_t) * (nf + 1));
   c->fam_founders = malloc(sizeof(int32_t) * nf); memcpy(c->fam_founders, ped->fam_founders, sizeof(int32_t) * nf);

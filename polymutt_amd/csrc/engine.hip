@@ -63,6 +63,9 @@ struct pm_engine {
   // ES polynomial form (PM_NUM_POLY): per-family layouts and per-step degrees (poly_layout)
   bool es_poly = false;
   int poly_ws = 0, poly_coef = 0, poly_dcap = 0;
+  int ep_dmax[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+  int itmax = 200;          // ScalarMinimizer::Brent's ITMAX (core/MathGold.cpp:98); PM_TEST_ITMAX lowers it (tests)
+  int stuck_site = -1;      // the last finished batch's first site whose Brent hit ITMAX (pm_engine_stuck_site)   // [plan][class]: the largest polynomial degree of a peeled family
   int hoist_tmp = 0, hoist_waves = 4, es_chunk = 0;   // k_es_hoist: step temporaries per wave, waves per block, items per launch
   double* d_es_coef = nullptr;                        // [es_chunk][max_ext][poly_dcap][T] hoisted coefficients
   unsigned long long* d_es_prof = nullptr;            // PM_ES_PROF: es_hoist_wave cycles by part
@@ -139,6 +142,9 @@ static int dalloc(X** p, size_t count) {
   }
   return PM_OK;
 }
+// a persistent grid rounded down to whole rounds of the 8 XCDs (the kernels' XCD-aware item order needs gridDim % 8 == 0;
+// they fall back to plain order otherwise), never below one block
+static int xcd_grid(int g) { return g >= 8 ? g - g % 8 : std::max(g, 1); }
 #define DALLOC(p, n) do { int _r = dalloc(&(p), (n)); if (_r) { pm_engine_destroy(E); return _r; } } while (0)
 
 static const struct { int T, S; } kVariants[] = {{64, 1}, {64, 2}, {64, 4}, {128, 4}, {128, 16}, {256, 1}, {256, 4}, {512, 2}, {512, 4},
@@ -319,6 +325,7 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
   E->vcf = par->vcf_mode != 0;
   if (E->vcf) { E->par.denovo = 0; E->par.quick_call = 0; }   // the VCF path has neither (PedVCF.cpp)
   par = &E->par;
+  if (const char* s = getenv("PM_TEST_ITMAX"); s && atoi(s) > 0) E->itmax = std::min(200, atoi(s));
   E->n_fam = ped->n_fam;
   E->n_person = ped->n_person;
   E->max_batch = max_batch;
@@ -339,6 +346,70 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
   HIP_TRY(hipStreamCreateWithFlags(&E->stream, hipStreamNonBlocking));
   HIP_TRY(hipEventCreate(&E->ev0));
   HIP_TRY(hipEventCreate(&E->ev1));
+  // --- Elston-Stewart schedules and their polynomial-form layouts first: whether the polynomial form is usable
+  // (es_poly) decides how many extended families a lane of the plan may hold
+  const int ns = par->denovo ? 10 : 3;
+  std::vector<int> peel_start(ped->n_fam + 1, 0);
+  std::vector<int2> steps;
+  std::vector<int> founders(ped->fam_founders, ped->fam_founders + ped->n_fam);
+  int wsmax = 0;
+  E->plan1_ok = E->vcf;
+  for (int f = 0; f < ped->n_fam; f++) {
+    peel_start[f] = (int)steps.size();
+    const int kind = ped->fam_kind[f];
+    if (kind == PM_FAM_FOUNDERS || (kind == PM_FAM_NUCLEAR && !E->vcf)) continue;
+    const size_t mark = steps.size();
+    const int w = pack_steps(ped, f, ns, steps);
+    if (w < 0 && kind == PM_FAM_EXTENDED) {
+      pm_engine_destroy(E);
+      pm_set_last_error("pm_engine_create: extended family without a usable peeling schedule (or > 255 members)");
+      return PM_EPED;
+    }
+    if (w < 0) { steps.resize(mark); E->plan1_ok = false; continue; }   // nuclear without a schedule: no plan 1
+    wsmax = std::max(wsmax, w);
+  }
+  peel_start[ped->n_fam] = (int)steps.size();
+  E->ws_per_lane = wsmax;
+  // polynomial-form layouts (PM_NUM_POLY): every family with a schedule.  Under --denovo the 10-state layout
+  // also serves the BA (cfg-7) items: the degrees do not depend on the state count, the slots are larger.
+  std::vector<int> poly_start(ped->n_fam + 1, 0), poly_lay, poly_deg((size_t)steps.size() * 4, 0);
+  int poly_w = 0, poly_d = 0;
+  E->es_poly = par->numerics == PM_NUM_POLY && !steps.empty();
+  for (int f = 0; f < ped->n_fam && E->es_poly; f++) {
+    poly_start[f] = (int)poly_lay.size();
+    const int ns0 = peel_start[f], ns1 = peel_start[f + 1];
+    if (ns1 == ns0) continue;
+    std::vector<int> dg;
+    const int w = poly_layout(ped, f, par->denovo ? 10 : 3, steps.data() + ns0, ns1 - ns0, poly_lay, dg);
+    if (w < 0) { E->es_poly = false; break; }
+    std::copy(dg.begin(), dg.end(), poly_deg.begin() + (size_t)ns0 * 4);
+    poly_w = std::max(poly_w, w);
+    for (int c = 0; c < 4; c++) poly_d = std::max(poly_d, poly_lay[poly_start[f] + 2 + c]);
+  }
+  poly_start[ped->n_fam] = (int)poly_lay.size();
+  auto fam_deg = [&](int f, int c) {   // the polynomial degree of family f in chromosome class c (0: no layout)
+    return poly_start[f + 1] > poly_start[f] ? poly_lay[poly_start[f] + 2 + c] : 0;
+  };
+  if (E->es_poly) {   // k_es_hoist temporaries: the largest step's out-of-place phases (wave_poly_peel)
+    const int ns = par->denovo ? 10 : 3;
+    for (size_t s = 0; s < steps.size(); s++)
+      for (int cls = 0; cls < 4; cls++) {
+        const int dg = poly_deg[s * 4 + cls], type = steps[s].x & 255;
+        const int a = dg & 127, b = (dg >> 7) & 127, c = (dg >> 14) & 127, e = (dg >> 21) & 127;
+        int need;
+        if (type == 1) need = ns * ns * (a + 1) + ns * ns * (a + b + 1);
+        else if (type == 2) need = ns * (a + b + 1) + ns * (a + b + c + 1);
+        else need = ns * ns * (a + b + c + 1) + ns * (a + b + c + 1) + ns * (a + b + c + e + 1);
+        E->hoist_tmp = std::max(E->hoist_tmp, need);
+      }
+    // 4 waves per block when their LDS slices fit, else fewer; none: the reference-order peel per evaluation
+    const size_t stat = (256 + 5 * 27 + (par->denovo ? 2000 : 2)) * sizeof(double);
+    const size_t per_wave = (size_t)(poly_w + E->hoist_tmp) * sizeof(double);
+    E->hoist_waves = 0;
+    for (int w = 4; w >= 1 && !E->hoist_waves; w--)
+      if (stat + per_wave * w <= 150 * 1024) E->hoist_waves = w;
+    if (!E->hoist_waves) E->es_poly = false;
+  }
   // plan
   std::vector<int4> units;
   bool planned = false;
@@ -373,7 +444,8 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
     // (polynomial form: up to PM_EPE families per lane, their coefficients in registers, one wave per item)
     // (--denovo too: the 10-state peels are hoisted by the schedule compiler's es_hoist_wave, and k_brent only
     // evaluates their coefficients; the reference-order 10-state peel of PRODUCT / EXACT numerics keeps one per lane)
-    const int per_lane = (par->numerics == PM_NUM_POLY && !getenv("PM_EP_DN_ONE")) ? PM_EPE : 1;
+    // (PM_EP_DN_ONE=1: one per lane under --denovo -- an experiment switch)
+    const int per_lane = (E->es_poly && !(par->denovo && getenv("PM_EP_DN_ONE"))) ? PM_EPE : 1;
     int tmin = 1;
     while (tmin < std::min((E->n_ext + per_lane - 1) / per_lane, 256)) tmin *= 2;
     const int npref = gen ? 9 : 8;
@@ -446,65 +518,12 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
   HIP_TRY(hipMemcpy(E->d_syn, &syn, sizeof(syn), hipMemcpyHostToDevice));
   // --- Elston-Stewart data: packed schedules, per-lane family lists, transmission tables, workspace
   {
-    const int ns = par->denovo ? 10 : 3;
-    std::vector<int> peel_start(ped->n_fam + 1, 0);
-    std::vector<int2> steps;
-    std::vector<int> founders(ped->fam_founders, ped->fam_founders + ped->n_fam);
-    int wsmax = 0;
-    E->plan1_ok = E->vcf;
-    for (int f = 0; f < ped->n_fam; f++) {
-      peel_start[f] = (int)steps.size();
-      const int kind = ped->fam_kind[f];
-      if (kind == PM_FAM_FOUNDERS || (kind == PM_FAM_NUCLEAR && !E->vcf)) continue;
-      const size_t mark = steps.size();
-      const int w = pack_steps(ped, f, ns, steps);
-      if (w < 0 && kind == PM_FAM_EXTENDED) {
-        pm_engine_destroy(E);
-        pm_set_last_error("pm_engine_create: extended family without a usable peeling schedule (or > 255 members)");
-        return PM_EPED;
-      }
-      if (w < 0) { steps.resize(mark); E->plan1_ok = false; continue; }   // nuclear without a schedule: no plan 1
-      wsmax = std::max(wsmax, w);
-    }
-    peel_start[ped->n_fam] = (int)steps.size();
-    E->ws_per_lane = wsmax;
-    // polynomial-form layouts (PM_NUM_POLY): every family with a schedule.  Under --denovo the 10-state layout
-    // also serves the BA (cfg-7) items: the degrees do not depend on the state count, the slots are larger.
-    std::vector<int> poly_start(ped->n_fam + 1, 0), poly_lay, poly_deg((size_t)steps.size() * 4, 0);
-    int poly_w = 0, poly_d = 0;
-    E->es_poly = par->numerics == PM_NUM_POLY && !steps.empty();
-    for (int f = 0; f < ped->n_fam && E->es_poly; f++) {
-      poly_start[f] = (int)poly_lay.size();
-      const int ns0 = peel_start[f], ns1 = peel_start[f + 1];
-      if (ns1 == ns0) continue;
-      std::vector<int> dg;
-      const int w = poly_layout(ped, f, par->denovo ? 10 : 3, steps.data() + ns0, ns1 - ns0, poly_lay, dg);
-      if (w < 0) { E->es_poly = false; break; }
-      std::copy(dg.begin(), dg.end(), poly_deg.begin() + (size_t)ns0 * 4);
-      poly_w = std::max(poly_w, w);
-      for (int c = 0; c < 4; c++) poly_d = std::max(poly_d, poly_lay[poly_start[f] + 2 + c]);
-    }
-    poly_start[ped->n_fam] = (int)poly_lay.size();
-    if (E->es_poly) {   // k_es_hoist temporaries: the largest step's out-of-place phases (wave_poly_peel)
-      const int ns = par->denovo ? 10 : 3;
-      for (size_t s = 0; s < steps.size(); s++)
-        for (int cls = 0; cls < 4; cls++) {
-          const int dg = poly_deg[s * 4 + cls], type = steps[s].x & 255;
-          const int a = dg & 127, b = (dg >> 7) & 127, c = (dg >> 14) & 127, e = (dg >> 21) & 127;
-          int need;
-          if (type == 1) need = ns * ns * (a + 1) + ns * ns * (a + b + 1);
-          else if (type == 2) need = ns * (a + b + 1) + ns * (a + b + c + 1);
-          else need = ns * ns * (a + b + c + 1) + ns * (a + b + c + 1) + ns * (a + b + c + e + 1);
-          E->hoist_tmp = std::max(E->hoist_tmp, need);
+    if (E->es_poly)
+      for (int f = 0; f < ped->n_fam; f++)
+        for (int c = 0; c < 4; c++) {
+          if (ped->fam_kind[f] == PM_FAM_EXTENDED) E->ep_dmax[0][c] = std::max(E->ep_dmax[0][c], fam_deg(f, c));
+          if (ped->fam_kind[f] != PM_FAM_FOUNDERS) E->ep_dmax[1][c] = std::max(E->ep_dmax[1][c], fam_deg(f, c));
         }
-      // 4 waves per block when their LDS slices fit, else fewer; none: the reference-order peel per evaluation
-      const size_t stat = (256 + 5 * 27 + (par->denovo ? 2000 : 2)) * sizeof(double);
-      const size_t per_wave = (size_t)(poly_w + E->hoist_tmp) * sizeof(double);
-      E->hoist_waves = 0;
-      for (int w = 4; w >= 1 && !E->hoist_waves; w--)
-        if (stat + per_wave * w <= 150 * 1024) E->hoist_waves = w;
-      if (!E->hoist_waves) E->es_poly = false;
-    }
     const int T = E->T;
     E->max_ext = (E->n_ext + T - 1) / T;
     std::vector<int> ext_count(T, 0), ext_fam((size_t)std::max(1, E->max_ext) * T, -1);
@@ -622,7 +641,14 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
       E->es_chunk = (int)std::max<size_t>(1, std::min<size_t>(want, ((size_t)1 << 32) / per_item));
       if (const char* s = getenv("PM_ES_CHUNK"); s && atoi(s) > 0) E->es_chunk = std::min(E->es_chunk, atoi(s));
       if (E->es_chunk >= 12) E->es_chunk -= E->es_chunk % 12;   // whole sites of lists 0 and 1 per chunk (grouped tasks)
-      DALLOC(E->d_es_coef, (size_t)E->es_chunk * per_item / sizeof(double));
+      // (a full-batch chunk that does not fit -- several engines per GPU, a smaller device -- falls back to the 1 GiB
+      // chunk: launch_brent loops over chunks)
+      if (dalloc(&E->d_es_coef, (size_t)E->es_chunk * per_item / sizeof(double)) != PM_OK) {
+        (void)hipGetLastError();
+        E->es_chunk = (int)std::max<size_t>(1, std::min<size_t>(E->es_chunk, ((size_t)1 << 30) / per_item));
+        if (E->es_chunk >= 12) E->es_chunk -= E->es_chunk % 12;
+        DALLOC(E->d_es_coef, (size_t)E->es_chunk * per_item / sizeof(double));
+      }
     }
     // workspace: the Brent grids and the posterior grid are capped so each needs <= 1 GiB
     E->grid_post = E->n_cu * 8;
@@ -630,10 +656,10 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
       const size_t cap = (size_t)1 << 30, per_lane = (size_t)wsmax * sizeof(double);
       const size_t per_lane_b = (size_t)wsmax * sizeof(double);   // Brent grids (EP kernels use no workspace: k_es_hoist)
       E->grid_brent = (int)std::max<size_t>(E->n_cu, std::min<size_t>(E->grid_brent, cap / (per_lane_b * T)));
-      E->grid_brent -= E->grid_brent % 8;   // keep the XCD-aware item order exact
+      E->grid_brent = xcd_grid(E->grid_brent);   // keep the XCD-aware item order exact
       if (E->T1) {
         E->grid1 = (int)std::max<size_t>(E->n_cu, std::min<size_t>(E->grid1, cap / (per_lane_b * E->T1)));
-        E->grid1 -= E->grid1 % 8;
+        E->grid1 = xcd_grid(E->grid1);
       }
       E->grid_post = (int)std::max<size_t>(E->n_cu, std::min<size_t>(E->grid_post, cap / (per_lane * 256)));
       const size_t words = std::max({(size_t)E->grid_brent * T * (per_lane_b / sizeof(double)),
@@ -773,6 +799,7 @@ static DevArgs make_args(pm_engine* E, int n, const uint8_t* pl, const uint32_t*
   for (int l = 0; l < N_LISTS; l++) A.items[l] = E->d_items[l];
   A.counts = E->d_counts; A.eval_total = E->d_eval_total; A.phase = E->d_phase; A.row_site = E->d_row_site; A.row_blk = E->d_row_blk; A.counters = E->d_counters;
   A.carry_postprob = E->carry_postprob ? 1 : 0;
+  A.itmax = E->itmax;
   // (the QUAD plan's cfg-1 items form it from their hoisting: launch_brent takes the QUAD kernel for list 0 exactly when
   // E->quad and the plan is 64 x 8 / 64 x 16, and mono_dn_in_prep already implies the lean --denovo kernel)
   A.mono_dn = !mono_dn_in_prep(E) ? 0 : (E->quad && E->T == 64 && (E->S == 8 || E->S == 16) && !getenv("PM_MONO_DN_PREP")) ? 2 : 1;
@@ -782,15 +809,26 @@ static DevArgs make_args(pm_engine* E, int n, const uint8_t* pl, const uint32_t*
 typedef void (*BrentFn)(DevArgs, int);
 // numerics: PM_NUM_PRODUCT / PM_NUM_EXACT for every flavour; PM_NUM_POLY only for the lean kernel
 // (the generic and ES flavours fall back to PRODUCT numerics).
+// pd_hi: the plan's peeled families reach a polynomial degree above PM_PD_LO (one-wave EP plans then take the
+// PM_PD_HI register tile; degrees above that are evaluated from the coefficient buffer)
 static BrentFn brent_kernel(int T, int S, int num, bool gen, bool es, bool dn = false, bool pf = false, bool ep = false, bool trio = false,
-                            bool epo = false) {
+                            bool epo = false, bool pd_hi = false) {
   const int n = (num == PM_NUM_POLY && gen) ? PM_NUM_PRODUCT : num;
   if (es && ep && epo && T == 64 && (S == 1 || S == 2 || S == 4)) {   // ep_only plans: the nuclear machinery compiled out
 #define PMKEO(s) \
+  if (S == s && pd_hi) return dn ? k_brent<64, s, PM_NUM_PRODUCT, true, true, true, false, true, false, 1, PM_PD_HI> \
+                                 : k_brent<64, s, PM_NUM_PRODUCT, true, true, false, false, true, false, 1, PM_PD_HI>; \
   if (S == s) return dn ? k_brent<64, s, PM_NUM_PRODUCT, true, true, true, false, true, false, 1> \
                         : k_brent<64, s, PM_NUM_PRODUCT, true, true, false, false, true, false, 1>;
     PMKEO(1) PMKEO(2) PMKEO(4)
 #undef PMKEO
+  }
+  if (es && ep && pd_hi && T == 64) {
+#define PMKEH(s) \
+  if (S == s) return dn ? k_brent<64, s, PM_NUM_PRODUCT, true, true, true, false, true, false, 0, PM_PD_HI> \
+                        : k_brent<64, s, PM_NUM_PRODUCT, true, true, false, false, true, false, 0, PM_PD_HI>;
+    PMKEH(1) PMKEH(2) PMKEH(4) PMKEH(8)
+#undef PMKEH
   }
   if (es && ep) {   // extended families in polynomial form (PM_NUM_POLY); DN: with the 10-state (--denovo) hoisting
 #define PMKEP(t, s) \
@@ -924,7 +962,7 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
       if (getenv("PM_QD_BPC")) bpc = std::max(1, atoi(getenv("PM_QD_BPC")));
     }
     grid = E->n_cu * bpc;
-    grid -= grid % 8;   // (the XCD-aware item order)
+    grid = xcd_grid(grid);   // (the XCD-aware item order)
   }
   if (!quad && !gen && !unrelated && n_ext == 0 && A.denovo && E->par.numerics == PM_NUM_POLY && E->max_nuc <= 4 && S % DN_PF_C == 0 &&
       E->n_person % 16 == 0 && E->n_person >= 16 && !getenv("PM_NO_PREFETCH")) {
@@ -935,7 +973,8 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
   const bool ep_only = ep && (E->use_plan1 ? E->units1_empty : E->units_empty) && !getenv("PM_NO_EP_ONLY");
   BrentFn fn = quad ? qfn
                    : brent_kernel(T, S, E->par.numerics, gen, !unrelated && n_ext > 0, A.denovo != 0, A.pf_npad > 0 || A.dn_pf, ep,
-                                  E->all_trio && !unrelated && !getenv("PM_NO_TRIO"), ep_only && !getenv("PM_NO_EPO"));
+                                  E->all_trio && !unrelated && !getenv("PM_NO_TRIO"), ep_only && !getenv("PM_NO_EPO"),
+                                  ep && E->ep_dmax[E->use_plan1 ? 1 : 0][E->chrom] > PM_PD_LO && !getenv("PM_NO_PD_HI"));
   if (!fn) { pm_set_last_error("launch_brent: no kernel variant for the lane plan"); return PM_EINVAL; }
   // multi-wave de novo plans (T = 512 / 1024: more than 1024 families) stage 2 buffers per wave: above the
   // default 64 KB dynamic-LDS limit the kernel must opt in, and the block (plus its static LDS: lane plan,
@@ -977,7 +1016,7 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
       E->ep_bpc.push_back({(const void*)fn, n});
     }
     grid = std::min(grid, E->n_cu * bpc);
-    grid -= grid % 8;
+    grid = xcd_grid(grid);
   }
   // HIP events around every Brent launch (and, for EP, every hoisting launch: pm_kernel_stats reports the two apart)
   auto mark = [&](std::vector<std::pair<hipEvent_t, hipEvent_t>>& v, bool begin) -> int {
@@ -1068,8 +1107,9 @@ static int run_pipeline(pm_engine* E, int n, const uint8_t* pl, const uint32_t* 
   E->last_n = n;
   HIP_TRY(hipMemsetAsync(E->d_counts, 0, 16 * sizeof(int), E->stream));
   {
-    const int big = 0x7fffffff;   // counts[4] = first emitted site (atomicMin)
-    HIP_TRY(hipMemcpyAsync(E->d_counts + 4, &big, sizeof(int), hipMemcpyHostToDevice, E->stream));
+    // counts[4] = first emitted site, counts[6] = first stuck site (both atomicMin); counts[5] = any stuck
+    static const int init[3] = {0x7fffffff, 0, 0x7fffffff};
+    HIP_TRY(hipMemcpyAsync(E->d_counts + 4, init, sizeof(init), hipMemcpyHostToDevice, E->stream));
   }
   {   // persons per lane of k_prep: vector loads when n_person allows; the reference's serial mono order in EXACT
     const int np = E->n_person;
@@ -1214,8 +1254,22 @@ static int finish_batch(pm_engine* E, const int* counts) {
   }
   int rc = collect_stats(E);
   if (rc) return rc;
+  E->stuck_site = counts[5] ? counts[6] : -1;
   if (counts[5]) { pm_set_last_error("ScalarMinimizer::Brent got stuck"); return PM_EBRENT; }
   return PM_OK;
+}
+
+int pm_engine_stuck_site(pm_engine* E, int32_t* site) {
+  if (!E || !site) { pm_set_last_error("pm_engine_stuck_site: invalid arguments"); return PM_EINVAL; }
+  *site = E->stuck_site;
+  return PM_OK;
+}
+
+// rows written for the sites before the first stuck one (rows are numbered in site order)
+static int rows_before(const pm_site_result* res, int k) {
+  int r = 0;
+  for (int i = 0; i < k; i++) r += res[i].call_row >= 0;
+  return r;
 }
 
 int pm_engine_sync(pm_engine* E) {
@@ -1270,10 +1324,10 @@ int pm_engine_collect(pm_engine* E, pm_site_result* res, pm_geno_call* calls, in
   HIP_TRY(hipStreamSynchronize(E->stream));
   int counts[16];
   memcpy(counts, E->h_counts, sizeof(counts));
-  int rc = finish_batch(E, counts);
-  if (rc) return rc;
+  const int rc = finish_batch(E, counts);
+  if (rc && rc != PM_EBRENT) return rc;
   memcpy(res, E->h_res, sizeof(pm_site_result) * n);
-  *n_rows = counts[3];
+  *n_rows = rc ? rows_before(res, E->stuck_site) : counts[3];   // PM_EBRENT: the complete sites' rows only
   const size_t np = E->n_person;
   if (calls && counts[3] > 0) {
     if (E->vcf) {   // 4-B rows on the device (pm_vcf_call), expanded into the caller's pm_geno_call rows
@@ -1288,7 +1342,7 @@ int pm_engine_collect(pm_engine* E, pm_site_result* res, pm_geno_call* calls, in
       }
     } else HIP_TRY(hipMemcpy(calls, E->d_calls, sizeof(pm_geno_call) * np * counts[3], hipMemcpyDeviceToHost));
   }
-  return PM_OK;
+  return rc;
 }
 
 int pm_engine_run_vcf(pm_engine* E, int32_t n, const uint8_t* pl, const uint8_t* ref, pm_site_result* res, pm_vcf_call* calls,
@@ -1296,20 +1350,22 @@ int pm_engine_run_vcf(pm_engine* E, int32_t n, const uint8_t* pl, const uint8_t*
   if (!E || !E->vcf || n < 0 || n > E->max_batch || !res || !n_rows) { pm_set_last_error("pm_engine_run_vcf: invalid arguments"); return PM_EINVAL; }
   *n_rows = 0;
   if (n == 0) return PM_OK;
+  // (a pm_engine_submit batch still to be collected stays pending: the caller collects it)
+  if (E->pending_n >= 0) { pm_set_last_error("pm_engine_run_vcf: a submitted batch has not been collected"); return PM_EINVAL; }
   int rc = pm_engine_submit(E, n, pl, nullptr, ref);
-  if (rc) { E->pending_n = -1; return rc; }
-  E->pending_n = -1;
+  E->pending_n = -1;   // (this call's own batch: collected below, or abandoned with submit's error)
+  if (rc) return rc;
   HIP_TRY(hipSetDevice(E->device));
   HIP_TRY(hipStreamSynchronize(E->stream));
   int counts[16];
   memcpy(counts, E->h_counts, sizeof(counts));
   rc = finish_batch(E, counts);
-  if (rc) return rc;
+  if (rc && rc != PM_EBRENT) return rc;
   memcpy(res, E->h_res, sizeof(pm_site_result) * n);
-  *n_rows = counts[3];
+  *n_rows = rc ? rows_before(res, E->stuck_site) : counts[3];   // PM_EBRENT: the complete sites' rows only
   if (calls && counts[3] > 0)   // the device rows as they are (4 B per person)
     HIP_TRY(hipMemcpy(calls, E->d_calls, sizeof(pm_vcf_call) * E->n_person * (size_t)counts[3], hipMemcpyDeviceToHost));
-  return PM_OK;
+  return rc;
 }
 
 int pm_engine_run(pm_engine* E, int32_t n, const uint8_t* pl, const uint32_t* dm, const uint8_t* ref, int32_t on_device,
@@ -1329,11 +1385,11 @@ int pm_engine_run(pm_engine* E, int32_t n, const uint8_t* pl, const uint32_t* dm
   rc = run_pipeline(E, n, E->d_pl, dm, ref, E->d_res, E->d_calls);
   if (rc) return rc;
   rc = pm_engine_sync(E);
-  if (rc) return rc;
+  if (rc && rc != PM_EBRENT) return rc;
   HIP_TRY(hipMemcpy(res, E->d_res, sizeof(pm_site_result) * n, hipMemcpyDeviceToHost));
   int counts[16];
   HIP_TRY(hipMemcpy(counts, E->d_counts, sizeof(counts), hipMemcpyDeviceToHost));
-  *n_rows = counts[3];
+  *n_rows = rc ? rows_before(res, E->stuck_site) : counts[3];   // PM_EBRENT: the complete sites' rows only
   if (calls && counts[3] > 0) {
     if (E->vcf) {
       const size_t nr = np * (size_t)counts[3];
@@ -1347,7 +1403,7 @@ int pm_engine_run(pm_engine* E, int32_t n, const uint8_t* pl, const uint32_t* dm
       }
     } else HIP_TRY(hipMemcpy(calls, E->d_calls, sizeof(pm_geno_call) * np * counts[3], hipMemcpyDeviceToHost));
   }
-  return PM_OK;
+  return rc;
 }
 
 int pm_engine_to_planar(pm_engine* E, int32_t n, const uint8_t* d_src, uint8_t* d_dst) {

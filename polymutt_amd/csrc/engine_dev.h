@@ -166,7 +166,9 @@ struct DevArgs {
   int* evals;              // [n][8]
   double* mono_plain;      // [n] MonomorphismLogLikelihood
   int* items[N_LISTS];
-  int* counts;             // [0..2] list sizes, [3] rows, [4] first emitted site, [5] Brent stuck, [8]/[9] quick items/site visits
+  int* counts;             // [0..2] list sizes, [3] rows, [4] first emitted site, [5] Brent stuck, [6] first stuck site
+                           // (atomicMin), [8]/[9] quick items/site visits
+  int itmax;               // Brent's ITMAX (MathGold.cpp:98: 200; PM_TEST_ITMAX lowers it for the failure-path tests)
   unsigned long long* eval_total;
   unsigned long long* phase;   // PM_PHASE_TIMING: [0] hoisting, [1] evaluations, [2] items -- k_brent wave time (wall_clock64 ticks)
   int* row_site;           // [n] emitted row -> site
@@ -503,8 +505,11 @@ __device__ __forceinline__ double d_es_lk(const DevArgs& A, int f, const uint8_t
 // Brent item on coefficient vectors; each objective evaluation is then one Horner pass over D + 1 non-negative
 // coefficients (no cancellation: relative error ~ (D + 2) ulp, the class of PM_NUM_POLY's nuclear quartics).
 // The reference-order numeric peel stays in d_es_lk (PM_NUM_PRODUCT / PM_NUM_EXACT, and the posteriors).
-// register tiles of the evaluation: a polynomial of degree <= PDM as PDM + 1 coefficients (zero above its degree)
-#define PDM 8
+// register tiles of the evaluation: a polynomial of degree <= PD as PD + 1 coefficients (zero above its degree).  PD is a
+// template parameter of the EP k_brent instantiations: 8 (4 founders, ext10) or 12 (6 founders: config 4's 12-member
+// three-generation pedigrees), picked per launch from the plan's largest degree in the section's class (launch_brent)
+#define PM_PD_LO 8
+#define PM_PD_HI 12
 
 // L(f) from the coefficients: g^D sum_a c_a t^a (t = f / g <= 1) or f^D sum_a c_a s^(D - a) (s = g / f < 1)
 __device__ __forceinline__ double es_poly_eval(const double* c, size_t st, int D, double x) {
@@ -526,28 +531,29 @@ __device__ __forceinline__ double es_poly_eval(const double* c, size_t st, int D
   return acc * p;
 }
 
-// es_poly_eval on register-resident coefficients (c[a] = 0 above D <= PDM): the leading zeros leave the Horner
+// es_poly_eval on register-resident coefficients (c[a] = 0 above D <= PD): the leading zeros leave the Horner
 // sum's bits unchanged (0 * t + c = c)
 #ifndef PM_EPE
 #define PM_EPE 4   // extended families per lane whose coefficients stay in registers through an item's evaluations
 #endif
+template <int PD>
 __device__ __forceinline__ double es_poly_eval_r(const double* c, int D, double x) {
   const double g = 1 - x;
   double acc = 0.0, base;
   if (x <= 0.5) {
     const double t = x / g;
 #pragma unroll
-    for (int a = PDM; a >= 0; a--) acc = acc * t + c[a];
+    for (int a = PD; a >= 0; a--) acc = acc * t + c[a];
     base = g;
   } else {
     const double sr = g / x;
 #pragma unroll
-    for (int a = 0; a <= PDM; a++) acc = a <= D ? acc * sr + c[a] : acc;
+    for (int a = 0; a <= PD; a++) acc = a <= D ? acc * sr + c[a] : acc;
     base = x;
   }
   double p = 1.0;
 #pragma unroll
-  for (int a = 0; a < PDM; a++) p = a < D ? p * base : p;
+  for (int a = 0; a < PD; a++) p = a < D ? p * base : p;
   return acc * p;
 }
 
@@ -1811,9 +1817,13 @@ constexpr int brent_waves() { return (NUM == PM_NUM_POLY && !GEN && (T == 64 || 
 // NF: the lean PF kernel's persons per family when every unit is one size (3: trio plans); on EP kernels NF = 1 marks
 // the ep_only plans (every family peeled: no nuclear or founder unit), whose unit loads, nuclear hoisting and lane
 // products are compiled out -- fewer live registers (PM_EPO_WAVES per SIMD)
-template <int T, int S, int NUM, bool GEN, bool ES, bool DN = false, bool PF = false, bool EP = false, bool QD = false, int NF = 0>
-__global__ void __launch_bounds__(T, (EP ? (NF == 1 ? PM_EPO_WAVES : PM_EP_WAVES) : QD ? PM_QD_WAVES : brent_waves<T, S, NUM, GEN>()))
+// PD: EP kernels' register tile, the largest polynomial degree evaluated from registers (PM_PD_LO / PM_PD_HI)
+template <int T, int S, int NUM, bool GEN, bool ES, bool DN = false, bool PF = false, bool EP = false, bool QD = false, int NF = 0,
+          int PD = PM_PD_LO>
+__global__ void __launch_bounds__(T, (EP ? (NF == 1 ? (PD > PM_PD_LO ? PM_EP_WAVES : PM_EPO_WAVES) : PM_EP_WAVES)
+                                     : QD ? PM_QD_WAVES : brent_waves<T, S, NUM, GEN>()))
 k_brent(DevArgs A, int list) {
+  constexpr int PDM = PD;
   constexpr bool EPO = EP && NF == 1;
   constexpr bool PROD = NUM != PM_NUM_EXACT;
   constexpr bool POLYK = NUM == PM_NUM_POLY && !GEN;
@@ -2086,7 +2096,7 @@ k_brent(DevArgs A, int list) {
             for (int q = 0; q < EPE; q++)
               if (ed[q] >= 0) {
                 int e1, e2;
-                const double mv = frexp(es_poly_eval_r(ce[q], ed[q], x), &e1);
+                const double mv = frexp(es_poly_eval_r<PDM>(ce[q], ed[q], x), &e1);
                 m = frexp(m * mv, &e2);
                 e += e1 + e2;
               }
@@ -2141,7 +2151,7 @@ k_brent(DevArgs A, int list) {
           else if (fu <= fv || v == mn || v == w) { v = u; fv = fu; }
         }
       }
-      if (++iter > 200) break;   // ITMAX: numerror("ScalarMinimizer::Brent got stuck")
+      if (++iter > A.itmax) break;   // ITMAX: numerror("ScalarMinimizer::Brent got stuck")
       const double middle = 0.5 * (a + c);
       const double tol1 = tol * fabs(mn) + 3.0e-10;
       const double tol2 = 2.0 * tol1;
@@ -2177,7 +2187,7 @@ k_brent(DevArgs A, int list) {
         A.evals[site * 8 + cfg] = nev;
       }
       if (!single) ev_acc += nev - skipped;   // objective evaluations computed
-      if (!ok) atomicExch(&A.counts[5], 1);
+      if (!ok) { atomicExch(&A.counts[5], 1); atomicMin(&A.counts[6], site); }   // (the reference stops at the first)
     }
     if (A.phase) { ph_e += wall_clock64() - ph_t; ph_n++; }
   }

@@ -17,6 +17,16 @@ PM_CHR_AUTO, PM_CHR_X, PM_CHR_Y, PM_CHR_MT = 0, 1, 2, 3
 FAM_NUCLEAR, FAM_FOUNDERS, FAM_EXTENDED = 0, 1, 2
 PM_EBRENT = -4
 
+
+class BrentStuck(FloatingPointError):
+    """PM_EBRENT: a site's Brent maximisation hit ITMAX ("ScalarMinimizer::Brent got stuck", core/MathGold.cpp:98,175).
+    ``site`` = the batch index of the first such site; ``results`` / ``calls`` = the batch's results and the genotype
+    rows of the sites before it (complete, as the reference had written them before exiting)."""
+
+    def __init__(self, site, results=None, calls=None):
+        super().__init__("ScalarMinimizer::Brent got stuck")
+        self.site, self.results, self.calls = site, results, calls
+
 i32, i64, u64, f64, i8, i16 = C.c_int32, C.c_int64, C.c_uint64, C.c_double, C.c_int8, C.c_int16
 P = C.POINTER
 
@@ -105,6 +115,7 @@ EXPORTS = {
     "pm_engine_sync": (i32, [C.c_void_p]),
     "pm_engine_submit": (i32, [C.c_void_p, i32, C.c_void_p, C.c_void_p, C.c_void_p]),
     "pm_engine_collect": (i32, [C.c_void_p, C.c_void_p, C.c_void_p, P(i32)]),
+    "pm_engine_stuck_site": (i32, [C.c_void_p, P(i32)]),
     "pm_host_alloc": (i32, [u64, P(C.c_void_p)]),
     "pm_host_free": (i32, [C.c_void_p]),
     "pm_engine_to_planar": (i32, [C.c_void_p, i32, C.c_void_p, C.c_void_p]),
@@ -257,7 +268,7 @@ class Engine:
         calls = np.zeros((n, self.n_person), dtype=CALL_DTYPE)
         rows = i32(0)
         self._check(self.lib.pm_engine_run(self.h, n, _ptr(pl), _ptr(dm), _ptr(ref), 0, _ptr(res), _ptr(calls),
-                                           C.byref(rows)))
+                                           C.byref(rows)), res, calls, rows)
         return res, calls[: rows.value]
 
     def run_vcf(self, pl, ref):
@@ -268,7 +279,8 @@ class Engine:
         res = np.zeros(n, dtype=SITE_DTYPE)
         calls = np.zeros((n, self.n_person), dtype=VCF_CALL_DTYPE)
         rows = i32(0)
-        self._check(self.lib.pm_engine_run_vcf(self.h, n, _ptr(pl), _ptr(ref), _ptr(res), _ptr(calls), C.byref(rows)))
+        self._check(self.lib.pm_engine_run_vcf(self.h, n, _ptr(pl), _ptr(ref), _ptr(res), _ptr(calls), C.byref(rows)),
+                    res, calls, rows)
         return res, calls[: rows.value]
 
     def submit(self, pl, dm, ref):
@@ -286,8 +298,8 @@ class Engine:
         res = np.zeros(n, dtype=SITE_DTYPE)
         calls = np.zeros((n, self.n_person), dtype=CALL_DTYPE)
         rows = i32(0)
-        self._check(self.lib.pm_engine_collect(self.h, _ptr(res), _ptr(calls), C.byref(rows)))
         self._pending = None
+        self._check(self.lib.pm_engine_collect(self.h, _ptr(res), _ptr(calls), C.byref(rows)), res, calls, rows)
         return res, calls[: rows.value]
 
     def run_device(self, n, d_pl, d_dm, d_ref, d_res=None, d_calls=None):
@@ -338,9 +350,15 @@ class Engine:
         self._check(self.lib.pm_engine_kernel_stats(self.h, C.byref(s), 1 if reset else 0))
         return s
 
-    def _check(self, rc):
+    def stuck_site(self):
+        """pm_engine_stuck_site: the first site of the last finished batch whose Brent hit ITMAX (-1: none)."""
+        k = i32(0)
+        self._check(self.lib.pm_engine_stuck_site(self.h, C.byref(k)))
+        return k.value
+
+    def _check(self, rc, res=None, calls=None, rows=None):
         if rc == PM_EBRENT:
-            raise FloatingPointError("ScalarMinimizer::Brent got stuck")
+            raise BrentStuck(self.stuck_site(), res, None if calls is None else calls[: rows.value])
         if rc != 0:
             raise RuntimeError(f"engine call failed ({rc}): {_err(self.lib)}")
 

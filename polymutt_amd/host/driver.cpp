@@ -108,12 +108,20 @@ void SiteEvaluator::run_vcf(int n, int n_person, const uint8_t* pl, const uint8_
                             int* n_rows) {
   std::vector<uint32_t> dm((size_t)n * n_person, 0);
   std::vector<pm_geno_call> wide((size_t)n * n_person);
-  run(n, pl, dm.data(), ref, res, wide.data(), n_rows);
-  for (size_t i = 0; i < (size_t)*n_rows * n_person; i++) {   // (GQ <= 100, best <= 2 in vcf_mode: the device's 4-B form)
-    pm_vcf_call c;
-    c.best = (int8_t)wide[i].best; c.gq = (int8_t)wide[i].gq; c.label = wide[i].label; c.pad = 0;
-    calls[i] = c;
+  auto narrow = [&](int rows) {   // (GQ <= 100, best <= 2 in vcf_mode: the device's 4-B form)
+    for (size_t i = 0; i < (size_t)rows * n_person; i++) {
+      pm_vcf_call c;
+      c.best = (int8_t)wide[i].best; c.gq = (int8_t)wide[i].gq; c.label = wide[i].label; c.pad = 0;
+      calls[i] = c;
+    }
+  };
+  try {
+    run(n, pl, dm.data(), ref, res, wide.data(), n_rows);
+  } catch (const BrentError& e) {   // the rows of the sites before the stuck one are complete
+    narrow(e.rows);
+    throw;
   }
+  narrow(*n_rows);
 }
 
 int default_io_threads(const Options& opt) {
@@ -287,7 +295,11 @@ int run_polymutt_sharded(const Options& opt, const Pedigree& ped, SiteEvaluator&
   const int np = (int)ped.column_pid.size();
   Batch B;
   B.init(eval, opt.batch > 0 ? opt.batch : 4096, np);
-  enum { K_ENTRIES = 16, K_OUT, K_REC, K_START, K_END, K_FIRST_END, K };
+  enum { K_ENTRIES = 16, K_OUT, K_REC, K_START, K_END, K_FIRST_END, K_STUCK, K };
+  // A Brent stuck at ITMAX (core/MathGold.cpp:98,175) ends the reference's run at that site, every earlier record
+  // written, no summary for the section: the stuck shard writes its records before the site, the exchange tells every
+  // rank, and the merge takes this section's parts of the shards up to the first stuck one only.
+  int stuck_rank = -1;
   bool earlier = false;        // a site of an earlier section (any shard) reached CalcPostProb
   int64_t outputs = 0;         // OutputVCF calls over all shards: the header exists iff > 0
   std::vector<std::vector<int64_t>> secs;   // lead: every section's exchange (N x K)
@@ -317,12 +329,17 @@ int run_polymutt_sharded(const Options& opt, const Pedigree& ped, SiteEvaluator&
     std::vector<uint32_t> fdm(np);
     uint8_t fref = 0;
     int fpos = 0;
-    bool past = false;
+    bool past = false, stuck = false;
     auto flush = [&]() {
       if (B.n == 0) return;
-      int rows = 0;
-      eval.run(B.n, B.pl, B.dm, B.ref, B.res, B.calls, &rows);
-      for (int i = 0; i < B.n; i++) {
+      int rows = 0, nv = B.n;
+      try {
+        eval.run(B.n, B.pl, B.dm, B.ref, B.res, B.calls, &rows);
+      } catch (const BrentError& e) {   // the sites before the stuck one are complete
+        nv = e.valid;
+        stuck = true;
+      }
+      for (int i = 0; i < nv; i++) {
         const pm_site_result& r = B.res[i];
         if (!r.emit) continue;
         n_out++;
@@ -354,10 +371,10 @@ int run_polymutt_sharded(const Options& opt, const Pedigree& ped, SiteEvaluator&
       }
       src.fill(rowOf.data(), B.pl, B.dm);
       if (B.n == B.cap) flush();
-      if (past || src.ended()) break;
+      if (stuck || past || src.ended()) break;
     }
-    flush();
-    if (past) src.skipSection();   // the rest of the section belongs to later shards
+    if (!stuck) flush();
+    if (past && !stuck) src.skipSection();   // the rest of the section belongs to later shards
     if (getenv("PM_BLOCK_STATS") && blocks0 >= 0)
       fprintf(stderr, "PM_BLOCK_STATS shard %d section %s: blocks read %ld%s\n", R, label.c_str(), src.blocksRead() - blocks0,
               seeked ? " (seeked)" : "");
@@ -367,14 +384,17 @@ int run_polymutt_sharded(const Options& opt, const Pedigree& ped, SiteEvaluator&
     std::vector<int64_t> send(K), recv((size_t)N * K);
     memcpy(send.data(), &C, sizeof(C));
     send[K_ENTRIES] = entries; send[K_OUT] = n_out; send[K_REC] = n_rec;
-    send[K_START] = start; send[K_END] = ftell(fh); send[K_FIRST_END] = first_end;
+    send[K_START] = start; send[K_END] = ftell(fh); send[K_FIRST_END] = first_end; send[K_STUCK] = stuck;
     comm.allgather(send.data(), K, recv.data());
+    for (int q = N - 1; q >= 0; q--)
+      if (recv[(size_t)q * K + K_STUCK]) stuck_rank = q;
+    const int last_q = stuck_rank >= 0 ? stuck_rank : N - 1;   // this section's parts that reach the output
     auto needs_fix = [&](int q) {   // shard q's first record was formatted with the wrong famlk[0] state
       bool truth = earlier;
       for (int p = 0; p < q; p++) truth = truth || recv[(size_t)p * K + K_OUT] > 0;
       return recv[(size_t)q * K + K_REC] > 0 && truth != (earlier || q > 0);
     };
-    if (needs_fix(R)) {
+    if (R <= last_q && needs_fix(R)) {
       fprintf(stderr, "shard %d: section %s: first record re-run with famlk[0] posterior state %s\n", R, label.c_str(),
               (earlier || R > 0) ? "unset" : "set");
       eval.set_posterior_carry(!(earlier || R > 0));
@@ -404,16 +424,17 @@ int run_polymutt_sharded(const Options& opt, const Pedigree& ped, SiteEvaluator&
       for (int q = 0; q < N; q++) {
         for (int k = 0; k < 16; k++) s[k] += recv[(size_t)q * K + k];
         ent = std::max(ent, recv[(size_t)q * K + K_ENTRIES]);
-        fx[q] = needs_fix(q);
+        fx[q] = q <= last_q && needs_fix(q);
       }
-      print_summary(label, (int)ent, S, t0);
+      if (stuck_rank < 0) print_summary(label, (int)ent, S, t0);
       secs.push_back(recv);
       fixes.push_back(fx);
     } else secs.emplace_back();   // keeps the section numbering of the .fix files
-    for (int q = 0; q < N; q++) {
+    for (int q = 0; q <= last_q; q++) {
       outputs += recv[(size_t)q * K + K_OUT];
       earlier = earlier || recv[(size_t)q * K + K_OUT] > 0;
     }
+    if (stuck_rank >= 0) break;
   }
   fflush(fh);
   fclose(fh);
@@ -422,7 +443,7 @@ int run_polymutt_sharded(const Options& opt, const Pedigree& ped, SiteEvaluator&
     std::vector<int64_t> all(N);
     comm.allgather(&one, 1, all.data());
   }
-  if (!lead) return 0;
+  if (!lead) return stuck_rank >= 0 ? 1 : 0;   // (the lead prints the FATAL text once)
   FILE* out = fopen(opt.vcfOutFile.c_str(), "w");
   if (!out) throw FatalError("vcfOutFile can not be opened for output!\n");
   if (outputs > 0) { W.fh = out; W.header_written = false; W.header(); }
@@ -433,6 +454,7 @@ int run_polymutt_sharded(const Options& opt, const Pedigree& ped, SiteEvaluator&
   }
   for (size_t s = 0; s < secs.size(); s++)
     for (int q = 0; q < N; q++) {
+      if (stuck_rank >= 0 && s + 1 == secs.size() && q > stuck_rank) break;   // after the stuck site: never written
       const int64_t* v = secs[s].data() + (size_t)q * K;
       if (fixes[s][q]) {
         const std::string fxp = opt.vcfOutFile + ".part" + std::to_string(q) + ".fix" + std::to_string(s);
@@ -450,6 +472,7 @@ int run_polymutt_sharded(const Options& opt, const Pedigree& ped, SiteEvaluator&
     remove((opt.vcfOutFile + ".part" + std::to_string(q)).c_str());
   }
   fclose(out);
+  if (stuck_rank >= 0) throw BrentError();
   return 0;
 }
 
@@ -652,6 +675,11 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, c
       const double te = now_s();
       try {
         m.b->rows = eval.collect();
+      } catch (const BrentError& e) {   // the writer gets the sites before the stuck one, then the run ends
+        m.b->n = e.valid;
+        m.b->rows = e.rows;
+        toWriter.push(std::move(m));
+        throw;
       } catch (...) {
         freeq.push(m.b);
         throw;
@@ -723,12 +751,18 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, c
 
     auto flush = [&]() {
       if (B.n == 0) return;
-      int rows = 0;
+      int rows = 0, nv = B.n;
       const double t0 = now_s();
-      eval.run(B.n, B.pl, B.dm, B.ref, B.res, B.calls, &rows);
+      std::exception_ptr stuck;
+      try {
+        eval.run(B.n, B.pl, B.dm, B.ref, B.res, B.calls, &rows);
+      } catch (const BrentError& e) {   // write the sites before the stuck one, then end the run
+        nv = e.valid;
+        stuck = std::current_exception();
+      }
       const double t1 = now_s();
       t_eval += t1 - t0;
-      for (int i = 0; i < B.n && !stop; i++) {
+      for (int i = 0; i < nv && !stop; i++) {
         const pm_site_result& r = B.res[i];
         if (!r.emit) continue;
         W.output(label, B.pos[i], B.ref[i], r, r.call_row >= 0 ? B.calls + (size_t)r.call_row * np : nullptr, B.pl + (size_t)i * np * 10,
@@ -738,6 +772,10 @@ int run_polymutt(const Options& opt, const Pedigree& ped, SiteEvaluator& eval, c
       }
       B.n = 0;
       t_out += now_s() - t1;
+      if (stuck) {   // (after the records: the reference had written them before exiting)
+        fflush(vcf);
+        std::rethrow_exception(stuck);
+      }
     };
 
     std::vector<int> wpos(src.window()), rowOf(src.window());

@@ -50,22 +50,29 @@ class SiteEvaluator {
   // collect(), which returns its row count; batches are collected in submission order, and at most in_flight()
   // are outstanding.  The default runs the batch inside submit().
   virtual int in_flight() const { return 1; }
+  // (a BrentError of the batch surfaces at its collect(), after the batches before it, as the engine's does)
   virtual void submit(int n, const uint8_t* pl, const uint32_t* dm, const uint8_t* ref, pm_site_result* res, pm_geno_call* calls) {
-    int rows = 0;
-    run(n, pl, dm, ref, res, calls, &rows);
-    done_.push_back(rows);
+    int rows = 0, valid = -1;
+    try {
+      run(n, pl, dm, ref, res, calls, &rows);
+    } catch (const BrentError& e) {
+      valid = e.valid;
+      rows = e.rows;
+    }
+    done_.push_back({rows, valid});
   }
   virtual int collect() {
-    const int rows = done_.front();
+    const std::pair<int, int> d = done_.front();
     done_.erase(done_.begin());
-    return rows;
+    if (d.second >= 0) throw BrentError(d.second, d.first);
+    return d.first;
   }
   // Host memory for the batch buffers (the engine: page-locked, for asynchronous copies)
   virtual void* host_alloc(size_t bytes);
   virtual void host_free(void* p);
 
  private:
-  std::vector<int> done_;
+  std::vector<std::pair<int, int>> done_;   // (rows, first stuck site or -1) per submitted batch
 };
 
 // A run split over processes (one per GPU; polymutt_amd/launch.py): rank `rank` of `world` analyses a

@@ -54,7 +54,7 @@ class EngineEvaluator : public SiteEvaluator {
            int* n_rows) override {
     check(pm_engine_set_posterior_carry(eng_[0], seen_ ? 1 : 0));
     int rc = pm_engine_run(eng_[0], n, pl, dm, ref, 0, res, calls, n_rows);
-    if (rc == PM_EBRENT) throw BrentError();
+    if (rc == PM_EBRENT) throw stuck(eng_[0], *n_rows);
     check(rc);
     note(res, n);
   }
@@ -63,7 +63,7 @@ class EngineEvaluator : public SiteEvaluator {
     (void)n_person;
     check(pm_engine_set_posterior_carry(eng_[0], seen_ ? 1 : 0));
     int rc = pm_engine_run_vcf(eng_[0], n, pl, ref, res, calls, n_rows);
-    if (rc == PM_EBRENT) throw BrentError();
+    if (rc == PM_EBRENT) throw stuck(eng_[0], *n_rows);
     check(rc);
     note(res, n);
   }
@@ -94,7 +94,7 @@ class EngineEvaluator : public SiteEvaluator {
     q_.pop_front();
     int rows = 0;
     int rc = pm_engine_collect(j.e, j.res, j.calls, &rows);
-    if (rc == PM_EBRENT) throw BrentError();   // (the driver drains the writer first: no exit() with threads live)
+    if (rc == PM_EBRENT) throw stuck(j.e, rows);   // (the driver drains the writer first: no exit() with threads live)
     check(rc);
     note(j.res, j.n);
     return rows;
@@ -117,6 +117,12 @@ class EngineEvaluator : public SiteEvaluator {
     for (int i = 0; i < n && !seen_; i++) seen_ = res[i].emit != 0;
   }
   static void check(int rc) { if (rc) throw FatalError(std::string("GPU engine error: ") + pm_last_error() + "\n"); }
+  // PM_EBRENT: the batch's sites before the first stuck one are complete (pm_engine_stuck_site), `rows` their rows
+  static BrentError stuck(pm_engine* e, int rows) {
+    int32_t k = 0;
+    check(pm_engine_stuck_site(e, &k));
+    return BrentError(k < 0 ? 0 : k, rows);
+  }
   std::vector<pm_engine*> eng_;
   std::deque<Job> q_;
   std::vector<void*> pinned_;

@@ -16,9 +16,15 @@ namespace pmhost {
 
 // Thrown for conditions where the reference calls error() (prints "FATAL ERROR" and exits 1).
 struct FatalError : std::runtime_error { explicit FatalError(const std::string& m) : std::runtime_error(m) {} };
-// Thrown where the reference calls numerror("ScalarMinimizer::Brent got stuck") (MathGold.cpp): the driver writes every
-// record before the failing batch, then prints the reference's "FATAL NUMERIC ERROR" text and returns 1.
-struct BrentError : std::runtime_error { BrentError() : std::runtime_error("ScalarMinimizer::Brent got stuck") {} };
+// Thrown where the reference calls numerror("ScalarMinimizer::Brent got stuck") (core/MathGold.cpp:98,175), which exits
+// at the stuck site with every earlier record written (fflush per record, NucFamGenotypeLikelihood.cpp:1829): `valid`
+// = the batch index of the first stuck site (its earlier sites' results are complete), `rows` = their genotype rows.
+// The driver writes those records, then prints the reference's "FATAL NUMERIC ERROR" text and returns 1.
+struct BrentError : std::runtime_error {
+  int valid, rows;
+  explicit BrentError(int valid_ = 0, int rows_ = 0)
+      : std::runtime_error("ScalarMinimizer::Brent got stuck"), valid(valid_), rows(rows_) {}
+};
 
 struct Person {
   std::string famid, pid, fatid, motid;

@@ -74,6 +74,26 @@ bool synth_shape(const std::string& shape, int fam, std::vector<SynthMember>& ou
     add(0, 1, 2, 5); add(2, 3, 1, 6); add(7, 6, 1, 7); add(7, 6, 1, 8); add(4, 5, 2, 9); add(9, 10, 2, 10);
     return true;
   }
+  if (shape == "ext12") {
+    // 12 members, 6 founders (D = 12 on autosomes): GP1(m) x GP2(f) -> C1(m), C2(f); two roofs GP3 x GP4 -> C3(f),
+    // GP5 x GP6 -> C4(m); C1 x C3 -> K1(m); C4 x C2 -> K2(f).  Peels: two leaves, two type-3 roofs, two spouse
+    // steps, two more leaves, the founder couple.  path: founders 1,2,5,6,9,10 then 3,4,7,8,11,12
+    add(-1, -1, 1, 1); add(-1, -1, 2, 2); add(-1, -1, 1, 5); add(-1, -1, 2, 6); add(-1, -1, 1, 9); add(-1, -1, 2, 10);
+    add(0, 1, 1, 3); add(0, 1, 2, 4); add(2, 3, 2, 7); add(6, 8, 1, 8); add(4, 5, 1, 11); add(10, 7, 2, 12);
+    return true;
+  }
+  if (shape == "ext11") {
+    // 11 members, 5 founders (D = 10), mostly female middle generation: GP1(m) x GP2(f) -> C1(f), C2(m), C3(f);
+    // S1(m) x C1 -> K1(f); C2 x S2(f) -> K2(f); S3(m) x C3 -> K3(m).  path: founders 1,2,6,8,10 then 3,4,5,7,9,11
+    add(-1, -1, 1, 1); add(-1, -1, 2, 2); add(-1, -1, 1, 6); add(-1, -1, 2, 8); add(-1, -1, 1, 10);
+    add(0, 1, 2, 3); add(0, 1, 1, 4); add(0, 1, 2, 5); add(2, 5, 2, 7); add(6, 3, 2, 9); add(4, 7, 1, 11);
+    return true;
+  }
+  // config 4 at its stated range (8-12 members): five three-generation shapes dealt round-robin over the families
+  if (shape == "extmix") {
+    static const char* const mix[5] = {"ext10", "roof", "roof2", "ext12", "ext11"};
+    return synth_shape(mix[fam % 5], fam, out);
+  }
   if (shape == "single") { add(-1, -1, 1 + fam % 2, 1); return true; }
   // quads with an ext10 pedigree at families 256, 513, ...: a few extended families next to hundreds of
   // nuclear ones (the lane plan must pair nuclear slots with per-lane extended lists)

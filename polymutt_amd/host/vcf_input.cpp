@@ -529,6 +529,9 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
                 "loop %.3f s, flush wait %.3f s\n", t[0], t[1], t[2], t[3], t[4], t[5], t[6], t[7]);
     }
   } timing_out{tm};
+  // (declared before the writer: on unwinding, ~Writer joins its thread before the texts it writes are destroyed)
+  std::vector<std::string> texts[2];
+  std::vector<RecState> states;
   // one writer thread: fwrite of a formatted batch, in order, overlapped with the work on the next batch
   struct Writer {
     std::thread th;
@@ -545,37 +548,53 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
     }
     ~Writer() { if (th.joinable()) th.join(); }
   } writer;
-  std::vector<std::string> texts[2];
   int tcur = 0;
-  std::vector<RecState> states;
   TaskPool fpool(pool.threads());   // (the flusher's: the main thread's pool parses the next batch meanwhile)
   auto process = [&](BatchBuf& bb) {   // the flusher's work on one batch, in batch order
     std::vector<Pending*>& pend = bb.pend;
     const pm_vcf_call* calls = bb.calls;
     int rows = 0;
     double t0 = now();
-    if (bb.nb > 0) eval.run_vcf(bb.nb, np, bb.pl, bb.ref.data(), bb.res.data(), bb.calls, &rows);
+    // a Brent stuck at ITMAX (core/MathGold.cpp:98,175): the reference exits at that record, every earlier one written
+    // (PedVCF.cpp:103-160 prints record by record): the batch's records before the stuck computed one go out, then the
+    // error is raised
+    std::exception_ptr stuck;
+    size_t npend = pend.size();
+    if (bb.nb > 0) {
+      try {
+        eval.run_vcf(bb.nb, np, bb.pl, bb.ref.data(), bb.res.data(), bb.calls, &rows);
+      } catch (const BrentError& e) {
+        stuck = std::current_exception();
+        for (size_t k = 0; k < pend.size(); k++)
+          if (pend[k]->computed && pend[k]->slot >= e.valid) { npend = k; break; }
+      }
+    }
     double t1 = now();
     tm[3] += t1 - t0;
     // the state each record prints with (sequential: a record without data takes the last computed one's)
-    states.resize(pend.size());
+    states.resize(npend);
     RecState cur{st.qual, st.min, st.calls.data()};
-    for (size_t k = 0; k < pend.size(); k++) {
+    for (size_t k = 0; k < npend; k++) {
       const Pending& r = *pend[k];
       if (r.computed) cur = fresh_state(r, &bb.res[r.slot], calls + (size_t)bb.res[r.slot].call_row * np);
       states[k] = cur;
     }
     std::vector<std::string>& T = texts[tcur];
-    if (T.size() < pend.size()) T.resize(pend.size());
-    fpool.run((int)pend.size(), [&](int k) { format_record(T[k], *pend[k], states[k]); });
+    if (T.size() < npend) T.resize(npend);
+    fpool.run((int)npend, [&](int k) { format_record(T[k], *pend[k], states[k]); });
     const double t2 = now();
     tm[4] += t2 - t1;
     // the batch's text goes out on the writer thread while the next batch is read, parsed and computed; the
     // previous batch's write finishes first (file order), then the buffers alternate
     writer.wait();
     tm[5] += now() - t2;   // (write: the time this thread waited for the writer)
-    writer.start(out, &texts[tcur], (int)pend.size());
+    writer.start(out, &texts[tcur], (int)npend);
     tcur ^= 1;
+    if (stuck) {
+      writer.wait();
+      fflush(out);
+      std::rethrow_exception(stuck);
+    }
     if (!pend.empty()) {   // the last state carries into the next batch
       st.qual = cur.qual; st.min = cur.min;
       if (cur.calls != st.calls.data()) std::copy(cur.calls, cur.calls + np, st.calls.begin());
@@ -753,10 +772,11 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
     });
     copies.clear();
   };
-  bool eof = false;
+  bool eof = false, stuck = false;
   BlockReader br(in, &pool);
   std::vector<BlockReader::Line> lines;
   std::vector<char> keep(CH);
+  try {
   while (!eof) {
     // a chunk of lines from the block (in order), copied, split and classified in parallel, then the FORMAT
     // bookkeeping applied in file order
@@ -846,6 +866,10 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
   }
   flush();
   drain();
+  } catch (const BrentError&) {   // (process wrote the records before the stuck one; shards tell each other below)
+    if (!sharded) throw;
+    stuck = true;
+  }
   {
     const double tw = now();
     writer.wait();
@@ -858,12 +882,16 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
     return 0;
   }
 
-  // exchange: {computed any, QUAL, AF minimiser, skipped records, the genotype calls} of each rank's last computed record
-  const int K = 4 + np;
+  // exchange: {computed any, QUAL, AF minimiser, skipped records, Brent stuck, the genotype calls} of each rank's last
+  // computed record
+  const int K = 5 + np;
   std::vector<int64_t> send(K), recv((size_t)N * K);
-  send[0] = computed_any; send[1] = d2bits(st.qual); send[2] = d2bits(st.min); send[3] = bad_allele;
-  for (int p = 0; p < np; p++) send[4 + p] = pack_call(st.calls[p]);
+  send[0] = computed_any; send[1] = d2bits(st.qual); send[2] = d2bits(st.min); send[3] = bad_allele; send[4] = stuck;
+  for (int p = 0; p < np; p++) send[5 + p] = pack_call(st.calls[p]);
   comm->allgather(send.data(), K, recv.data());
+  int stuck_rank = -1;   // the first shard that met a stuck Brent: later shards' records come after it, never written
+  for (int q = N - 1; q >= 0; q--)
+    if (recv[(size_t)q * K + 4]) stuck_rank = q;
   fflush(out);
   fclose(out);
   if (lead) {   // this rank's leading no-data records, with the state of the nearest earlier rank that computed one
@@ -874,7 +902,7 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
       if (!v[0]) continue;
       carried.qual = bits2d(v[1]);
       carried.min = bits2d(v[2]);
-      for (int p = 0; p < np; p++) carried.calls[p] = unpack_call(v[4 + p]);
+      for (int p = 0; p < np; p++) carried.calls[p] = unpack_call(v[5 + p]);
       break;
     }
     std::swap(st, carried);
@@ -900,23 +928,25 @@ int run_polymutt_vcf(const Options& opt, const Pedigree& ped, SiteEvaluator& eva
     std::vector<int64_t> all(N);
     comm->allgather(&one, 1, all.data());
   }
-  if (R != 0) return 0;
+  if (R != 0) return stuck_rank >= 0 ? 1 : 0;   // (the lead prints the FATAL text once)
   FILE* fin = fopen(opt.vcfOutFile.c_str(), "w");
   if (!fin) throw FatalError("Open outpuf VCF file " + opt.vcfOutFile + " failed!\n");
   write_header(fin);
   int64_t bad = 0;
   for (int q = 0; q < N; q++) {
     const std::string pq = opt.vcfOutFile + ".part" + std::to_string(q);
+    const bool keep_q = stuck_rank < 0 || q <= stuck_rank;
     if (q > 0) {
-      copy_file_into(pq + ".leadvcf", fin);
+      if (keep_q) copy_file_into(pq + ".leadvcf", fin);
       remove((pq + ".leadvcf").c_str());
     }
-    copy_file_into(pq, fin);
+    if (keep_q) copy_file_into(pq, fin);
     remove(pq.c_str());
-    bad += recv[(size_t)q * K + 3];
+    if (keep_q) bad += recv[(size_t)q * K + 3];
   }
   fclose(fin);
   if (bad) fprintf(stderr, "%lld biallelic records with non-ACGT alleles were skipped\n", (long long)bad);
+  if (stuck_rank >= 0) throw BrentError();
   return 0;
 }
 

@@ -15,6 +15,10 @@ SYNTH = os.path.join(ROOT, "tests", "golden", "synth")
 CASES = json.load(open(os.path.join(SYNTH, "cases.json")))
 # cases with one section and no --pos: also compared site by site against the reference's --dump_sites records
 DUMP_CASES = sorted(n for n, c in CASES.items() if not c.get("cli_only"))
+# cases the serial CPU oracle needs minutes for (10-state peels of 200 pedigrees): the oracle is pinned on the same
+# shapes by their small cases (extmix_denovo), and the GPU engine is compared with these cases' reference dumps and
+# VCFs directly, without an oracle run
+ORACLE_SLOW = {"big_extmix_200_denovo"}
 
 
 def summary_block(stdout):

@@ -20,7 +20,7 @@ class OracleEvaluator : public pmhost::SiteEvaluator {
     int rows = 0;
     for (int i = 0; i < n; i++) {
       int rc = pmo_site(ctx_, pl + (size_t)i * np_ * 10, dm + (size_t)i * np_, ref[i], &res[i], calls + (size_t)rows * np_);
-      if (rc == PM_EBRENT) { printf("\nFATAL NUMERIC ERROR - ScalarMinimizer::Brent got stuck\n\n"); exit(1); }
+      if (rc == PM_EBRENT) throw pmhost::BrentError(i, rows);   // (the driver writes sites [0, i), then the FATAL text)
       res[i].call_row = res[i].emit == 1 ? rows++ : -1;
     }
     *n_rows = rows;

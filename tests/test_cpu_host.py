@@ -352,11 +352,12 @@ def test_sharded_vcf_input_matches_one_process_gloo(cpu_driver, tmp_path, case, 
                 assert dp_info != "DP=0" and "." not in dps, (k, c[7], dps)
 
 
-@pytest.mark.parametrize("shape", ["ext10", "roof", "roof2"])
-def test_schedule_compiler_builds_every_class(tmp_path, shape):
+@pytest.mark.parametrize("shape,n_shapes", [("ext10", 1), ("roof", 1), ("roof2", 1), ("extmix", 5)])
+def test_schedule_compiler_builds_every_class(tmp_path, shape, n_shapes):
     """The Elston-Stewart schedule compiler (polymutt_amd/csrc/es_jit.h) generates the hoisting kernel of a
     pedigree's extended families for every chromosome class and hipRTC compiles it for gfx950 (no device needed);
-    families of one shape share one device function; --denovo engines get the wave-cooperative variant."""
+    families of one shape share one device function, and a mixed pedigree file (extmix: five 8-12-member shapes)
+    gets one function per shape behind the kernel's shape switch; --denovo engines get the wave-cooperative variant."""
     exe = os.path.join(ROOT, "tests", "native", "build", "jit_check")
     if not os.path.exists(exe):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "polymutt_amd"), "../tests/native/build/jit_check"], check=True)
@@ -369,9 +370,10 @@ def test_schedule_compiler_builds_every_class(tmp_path, shape):
     assert occ and all(0.0 < float(l[-1]) <= 1.0 for l in occ), r.stderr[-2000:]
     lines = [l.split() for l in r.stdout.splitlines() if l.startswith("class")]
     assert [int(l[1]) for l in lines] == [0, 1, 2, 3] * 3   # bi-allelic engines, --denovo (grouped tasks, then all)
-    assert all(int(l[3]) == 1 and int(l[5]) == 5 and int(l[9]) > 0 for l in lines), r.stdout   # one shape, 5 families
+    assert all(int(l[3]) == n_shapes and int(l[5]) == 5 and int(l[9]) > 0 for l in lines), r.stdout   # shapes, 5 families
     src = (tmp_path / "k.hip").read_text()
-    assert "es_hoist_jit" in src and "fam0(" in src and "asm" not in src
+    assert "es_hoist_jit" in src and "asm" not in src
+    assert all(f"fam{i}(" in src for i in range(n_shapes)) and f"fam{n_shapes}(" not in src
     # --denovo kernels: the grouped-tasks-only kernel (lines 4-7) needs no larger a workspace slice than the one with
     # the whole 10-state / top variants (lines 8-11); per (item, family) the leaf prefix + 10-state rest does the
     # whole 10-state peel's operations or fewer (founder sparsity), and the top rest + leaf the top variant's

@@ -8,7 +8,7 @@ import subprocess
 import pytest
 
 import polymutt_amd as pm
-from fixtures import (CASES, DUMP_CASES, compare_to_dump, golden_dump, golden_vcf_body, make_dataset, params_and_chrom,
+from fixtures import (CASES, DUMP_CASES, ORACLE_SLOW, compare_to_dump, golden_dump, golden_vcf_body, make_dataset, params_and_chrom,
                       read_dataset, summary_block)
 from oracle_binding import Oracle
 from parity import compare_results
@@ -32,19 +32,22 @@ def test_engine_matches_reference_dump(built, tmp_path, name, numerics):
     par, chrom = params_and_chrom(case["flags"], numerics=numerics)
     (label, pos, ref, pl, dm), = secs
     eng = pm.Engine(ped.view, par, max_batch=128)
-    ora = Oracle(ped.view, par)
+    ora = None if name in ORACLE_SLOW else Oracle(ped.view, par)   # (ORACLE_SLOW: the reference dump alone)
     eng.begin_section(chrom)
-    ora.begin_section(chrom)
+    if ora:
+        ora.begin_section(chrom)
     res, calls = [], []
     for s in range(0, len(ref), 128):   # several batches: results must not depend on batching
         e, ec = eng.run(pl[s:s + 128], dm[s:s + 128], ref[s:s + 128])
-        o, oc = ora.run(pl[s:s + 128], dm[s:s + 128], ref[s:s + 128])
-        compare_results(e, o, ec, oc, label=f"{name}[{s}] ")
+        if ora:
+            o, oc = ora.run(pl[s:s + 128], dm[s:s + 128], ref[s:s + 128])
+            compare_results(e, o, ec, oc, label=f"{name}[{s}] ")
         res.append(e)
     import numpy as np
     res = np.concatenate(res)
     compare_to_dump(res, golden_dump(name), label=name + " ")
-    assert (eng.counters().as_array() == ora.counters().as_array()).all()
+    if ora:
+        assert (eng.counters().as_array() == ora.counters().as_array()).all()
     eng.close()
 
 
@@ -65,7 +68,8 @@ def test_cli_matches_reference_vcf(built, tmp_path, name, numerics):
         assert summary_block(r.stdout) == case["summary"]
 
 
-_ES_CASES = [n for n in DUMP_CASES if n.startswith(("ext10", "roof", "roof2", "big_ext10", "big_quadext")) and "denovo" not in n]
+_ES_CASES = [n for n in DUMP_CASES if n.startswith(("ext10", "roof", "roof2", "extmix", "big_ext10", "big_extmix", "big_quadext"))
+             and "denovo" not in n]
 
 
 @pytest.mark.parametrize("name", _ES_CASES)

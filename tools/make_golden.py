@@ -67,6 +67,13 @@ CASES = {
     "big_quad_1000_denovo": ("quad", 1000, 256, 7, ["--denovo"]),
     "big_ext10_200": ("ext10", 200, 256, 17, []),
     "big_ext10_200_denovo": ("ext10+dn", 200, 256, 29, ["--denovo", "--rate_denovo", "1e-6"]),
+    # config 4 at its stated 8-12-member range: ext10, roof, roof2, ext12 (6 founders), ext11 (5 founders) dealt
+    # round-robin, so every launch mixes schedules and polynomial degrees D = 8, 10, 12
+    "extmix_auto": ("extmix", 15, 300, 151, []),
+    "extmix_denovo": ("extmix+dn", 10, 300, 157, ["--denovo", "--rate_denovo", "1e-6"]),
+    "extmix_chrX": ("extmix", 15, 300, 163, ["--chrX", "1"]),
+    "big_extmix_200": ("extmix", 200, 256, 167, []),
+    "big_extmix_200_denovo": ("extmix+dn", 200, 256, 173, ["--denovo", "--rate_denovo", "1e-6"]),
     # a few extended pedigrees next to > 512 nuclear families
     "big_quadext_600": ("quadext", 600, 256, 97, []),
     "big_quadext_600_denovo": ("quadext", 600, 200, 101, ["--denovo", "--rate_denovo", "1e-6"]),
