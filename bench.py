@@ -433,8 +433,12 @@ def main():
     ep = n_ext > 0
     ext_eval_ops = ep_eval_ops(ped) if ep else ext_ops
 
+    def fused(st):   # ep_brent_jit: the peel's hoisting runs inside the Brent kernel (no hoisting launches)
+        return ep and st.es_hoist_launches == 0 and st.es_hoist_ops > 0
+
     def brent_ops(st):
-        return st.evals * (19 * n_nuc + 17 + ext_eval_ops) + st.items * (18 * n_nuc + 36 * kid_sum)
+        o = st.evals * (19 * n_nuc + 17 + ext_eval_ops) + st.items * (18 * n_nuc + 36 * kid_sum)
+        return o + (st.es_hoist_ops if fused(st) else 0.0)
 
     ops = brent_ops(ks)
     # one-engine calibration: k_brent's own launch times (nothing overlaps a launch on a single stream)
@@ -472,7 +476,8 @@ def main():
                        "distinct_sites_per_gpu": B * P, "parallelism": f"site-shard x{world}",
                        "inputs": "host (PCIe-inclusive)" if args.host_inputs else "HBM-resident",
                        "engines": 1 if args.host_inputs else len(engines)},
-            "roofline": {"bound": "fp64-valu", "kernel": "k_brent", "achieved": achieved_tops, "peak": FP64_NONFMA_TOPS,
+            "roofline": {"bound": "fp64-valu", "kernel": "ep_brent_jit" if fused(ref_st) else "k_brent", "achieved": achieved_tops,
+                         "peak": FP64_NONFMA_TOPS,
                          "unit": "TFLOP/s (non-FMA FP64 ops)", "frac": achieved_tops / FP64_NONFMA_TOPS,
                          "traffic": traffic, "traffic_unit": "HBM bytes per k_brent dispatch (PMC)",
                          "traffic_source": pmc_file, "ops_per_launch": ops_launch, "avg_launch_ms": avg_launch_s * 1e3,
@@ -482,6 +487,9 @@ def main():
                          "achieved_wall": ops / elapsed / 1e12, "frac_wall": ops / elapsed / 1e12 / FP64_NONFMA_TOPS,
                          "peak_measured_issue_rate": peak_meas,
                          "op_model": ("executed: evals x (19 nNuc + 17 + sum over extended families of (3 D + 5)) + items x "
+                                      "(18 nNuc + 36 kids) + the generated peels' hoisting operations (fused: ep_brent_jit "
+                                      "hoists and runs Brent in one kernel)") if fused(ref_st) else
+                                     ("executed: evals x (19 nNuc + 17 + sum over extended families of (3 D + 5)) + items x "
                                       "(18 nNuc + 36 kids); the coefficient hoisting is roofline_es_hoist") if ep else
                                      "SURVEY 8(d): evals x (19 nNuc + 17 + peel ops) + items x (18 nNuc + 36 kids)",
                          "peel_ops_per_eval": ext_ops, "ext_eval_ops": ext_eval_ops if ep else None,
@@ -498,7 +506,7 @@ def main():
                          "transitions": int(counters[10]), "transversions": int(counters[11]),
                          "nocall": int(counters[15])},
         }
-        if ep:   # the EP hoisting kernel (es_hoist_wave / es_hoist_jit): ops counted by the schedule compiler
+        if ep and not fused(ref_st):   # the EP hoisting kernel (es_hoist_wave / es_hoist_jit): ops counted by the schedule compiler
             hs = ref_st
             h_ms = hs.es_hoist_ms / max(1, hs.es_hoist_launches)
             h_ops = hs.es_hoist_ops / max(1, hs.es_hoist_launches)

@@ -77,6 +77,10 @@ struct pm_engine {
   pmjit::Kernel jit[2][4];
   int jit_state[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
   int* d_jit_slots[2][4] = {{nullptr, nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr, nullptr}};   // e | sig | p0
+  // the fused hoisting + Brent kernel (es_jit.h ep_brent_jit) per plan and class: 0 not tried, 1 built, -1 unavailable
+  pmjit::FusedKernel fused[2][4];
+  int fused_state[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+  int* d_fused_tab[2][4] = {{nullptr, nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr, nullptr}};
   int *d_poly_start = nullptr, *d_poly_lay = nullptr, *d_poly_deg = nullptr;
   int *d_es_pers = nullptr, *d_es_pers1 = nullptr;   // (family << 8 | member) of peeled families: plan 0 / plan 1
   int* d_fam_perm = nullptr;   // families by (kind, size) for k_posterior
@@ -292,6 +296,8 @@ void pm_engine_destroy(pm_engine* E) {
                   E->d_counters, E->d_row_blk};
   for (void* b : bufs) if (b) hipFree(b);
   for (auto& pl : E->d_jit_slots)
+    for (int* b : pl) if (b) hipFree(b);
+  for (auto& pl : E->d_fused_tab)
     for (int* b : pl) if (b) hipFree(b);
   for (auto& pr : E->brent_events) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
   for (auto& pr : E->es_events) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
@@ -873,6 +879,26 @@ static BrentFn brent_kernel(int T, int S, int num, bool gen, bool es, bool dn = 
   return nullptr;
 }
 
+// The extended families of the current plan as the schedule compiler sees them (slot order e = q * T + lane).
+static std::vector<pmjit::Family> jit_families(const pm_engine* E, int plan) {
+  const std::vector<int>& ef = plan ? E->ext_fam1_h : E->ext_fam_h;
+  std::vector<pmjit::Family> fams;
+  for (size_t e = 0; e < ef.size(); e++) {
+    const int f = ef[e];
+    if (f < 0) continue;
+    pmjit::Family F;
+    F.e = (int)e;
+    F.p0 = E->fam_start_h[f];
+    F.n = E->fam_start_h[f + 1] - F.p0;
+    F.nf = E->fam_founders_h[f];
+    F.sex.assign(E->sex_h.begin() + F.p0, E->sex_h.begin() + F.p0 + F.n);
+    F.founder.assign(E->founder_h.begin() + F.p0, E->founder_h.begin() + F.p0 + F.n);
+    F.steps.assign(E->steps_h.begin() + E->peel_start_h[f], E->steps_h.begin() + E->peel_start_h[f + 1]);
+    fams.push_back(F);
+  }
+  return fams;
+}
+
 // The schedule compiler's kernels for the current plan and chromosome class (es_jit.h), built on first use; nullptr
 // when it is off (PM_NO_JIT) or failed to build (then the generic k_es_hoist / k_posterior_es run).
 static const pmjit::Kernel* jit_kernel(pm_engine* E) {
@@ -881,21 +907,7 @@ static const pmjit::Kernel* jit_kernel(pm_engine* E) {
   int& st = E->jit_state[plan][cls];
   if (st == 0) {
     st = -1;
-    const std::vector<int>& ef = plan ? E->ext_fam1_h : E->ext_fam_h;
-    std::vector<pmjit::Family> fams;
-    for (size_t e = 0; e < ef.size(); e++) {
-      const int f = ef[e];
-      if (f < 0) continue;
-      pmjit::Family F;
-      F.e = (int)e;
-      F.p0 = E->fam_start_h[f];
-      F.n = E->fam_start_h[f + 1] - F.p0;
-      F.nf = E->fam_founders_h[f];
-      F.sex.assign(E->sex_h.begin() + F.p0, E->sex_h.begin() + F.p0 + F.n);
-      F.founder.assign(E->founder_h.begin() + F.p0, E->founder_h.begin() + F.p0 + F.n);
-      F.steps.assign(E->steps_h.begin() + E->peel_start_h[f], E->steps_h.begin() + E->peel_start_h[f + 1]);
-      fams.push_back(F);
-    }
+    const std::vector<pmjit::Family> fams = jit_families(E, plan);
     std::string err;
     pmjit::Kernel& K = E->jit[plan][cls];
     // (--denovo outside vcf_mode: every de novo item is hoisted in a grouped task, launch_brent)
@@ -912,6 +924,27 @@ static const pmjit::Kernel* jit_kernel(pm_engine* E) {
       fprintf(stderr, "polymutt: peeling-schedule compiler unavailable (%s); using the generic hoisting kernel\n", err.c_str());
   }
   return st == 1 ? &E->jit[plan][cls] : nullptr;
+}
+
+// The fused hoisting + Brent kernel for the current plan and class (bi-allelic engines, every family peeled), built on
+// first use; nullptr when off (PM_NO_FUSED, PM_NO_JIT) or unavailable (then es_hoist_jit + k_brent run).
+static const pmjit::FusedKernel* fused_kernel(pm_engine* E) {
+  const int plan = E->use_plan1 ? 1 : 0, cls = E->chrom;
+  if (!E->es_poly || getenv("PM_NO_JIT") || getenv("PM_NO_FUSED")) return nullptr;
+  int& st = E->fused_state[plan][cls];
+  if (st == 0) {
+    st = -1;
+    const std::vector<pmjit::Family> fams = jit_families(E, plan);
+    std::string err;
+    pmjit::FusedKernel& F = E->fused[plan][cls];
+    if (!fams.empty() && pmjit::build_fused(E->device, cls, fams, kTBA, &F, &err) && F.blocks_per_cu > 0) {
+      if (dalloc(&E->d_fused_tab[plan][cls], F.lane_tab.size()) == PM_OK &&
+          hipMemcpy(E->d_fused_tab[plan][cls], F.lane_tab.data(), sizeof(int) * F.lane_tab.size(), hipMemcpyHostToDevice) == hipSuccess)
+        st = 1;
+    } else if (!fams.empty() && getenv("PM_JIT_LAYOUT"))
+      fprintf(stderr, "polymutt: fused Brent kernel unavailable (%s); hoisting + k_brent\n", err.c_str());
+  }
+  return st == 1 ? &E->fused[plan][cls] : nullptr;
 }
 
 static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelated = false) {
@@ -1030,7 +1063,26 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
     return PM_OK;
   };
   int mrc;
-  if (ep) {   // chunks of the list (the coefficient buffer holds es_chunk items): k_es_hoist, then the chunk's Brent items
+  // bi-allelic engines whose every family is peeled (config 4): one fused launch per list -- each lane hoists its
+  // families' polynomials into registers and the wave runs the item's Brent (es_jit.h ep_brent_jit)
+  const pmjit::FusedKernel* FK = (ep && ep_only && !A.denovo && T == 64) ? fused_kernel(E) : nullptr;
+  if (FK) {
+    E->es_ops_known = true;   // (finish_batch: every item is bi-allelic, o[0] = one item's hoisting over every family)
+    for (int v = 0; v < 6; v++) E->es_item_ops[v] = v == 0 ? FK->item_ops : 0.0;
+    const int plan = E->use_plan1 ? 1 : 0;
+    pmjit::FusedArgs F;
+    F.items = A.items[list]; F.counts = A.counts; F.ref = A.ref; F.res = (const int*)A.res; F.pl = A.pl; F.lktab = A.lktab;
+    F.lane_tab = E->d_fused_tab[plan][E->chrom];
+    F.raw = A.raw; F.minv = A.minv; F.evals = A.evals; F.eval_total = A.eval_total;
+    F.precision = A.precision;
+    F.list = list; F.it0 = 0; F.it1 = INT_MAX; F.np = A.n_person; F.vcf = A.vcf; F.res_words = sizeof(pm_site_result) / 4;
+    F.res_a1 = offsetof(pm_site_result, allele1) / 4; F.res_a2 = offsetof(pm_site_result, allele2) / 4;
+    F.itmax = A.itmax; F.pad = 0;
+    void* params[] = {&F};
+    if ((mrc = mark(E->brent_events, true))) return mrc;
+    HIP_TRY(hipModuleLaunchKernel(FK->fn, xcd_grid(E->n_cu * FK->blocks_per_cu), 1, 1, 64, 1, 1, 0, E->stream, params, nullptr));
+    if ((mrc = mark(E->brent_events, false))) return mrc;
+  } else if (ep) {   // chunks of the list (the coefficient buffer holds es_chunk items): k_es_hoist, then the chunk's Brent items
     void (*hoist)(DevArgs, int) = A.denovo ? k_es_hoist<true> : k_es_hoist<false>;
     const size_t hlds = (size_t)E->hoist_waves * (E->poly_coef + E->hoist_tmp) * sizeof(double);
     if (hlds > 64 * 1024) HIP_TRY(hipFuncSetAttribute((const void*)hoist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hlds));

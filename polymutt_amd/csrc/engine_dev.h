@@ -33,6 +33,7 @@
 #include "../../include/polymutt_engine.h"
 #include "synth_core.h"
 #include "es_jit.h"
+#include "brent_core.h"   // pos_div, wave_prod, log10_mant_u, the Brent state machine (shared with the JIT kernels)
 
 #define MALE 1
 #define FEMALE 2
@@ -189,7 +190,6 @@ __device__ __forceinline__ int d_gi(int b1, int b2) {
 __device__ __forceinline__ int d_ts(int r) { return r == 1 ? 3 : r == 2 ? 4 : r == 3 ? 1 : 2; }
 __device__ __forceinline__ int d_tv1(int r) { return (r == 1 || r == 3) ? 2 : 1; }
 __device__ __forceinline__ int d_tv2(int r) { return (r == 1 || r == 3) ? 4 : 3; }
-__device__ __forceinline__ double d_sign(double a, double b) { return b >= 0 ? fabs(a) : -fabs(a); }
 
 __device__ __forceinline__ void cfg_alleles(int cfg, int r, int* a1, int* a2) {
   const int ts = d_ts(r), tv1 = d_tv1(r), tv2 = d_tv2(r);
@@ -631,8 +631,6 @@ __device__ __forceinline__ double lane_loglik(double f, const int4* unit, const 
 // reduces the pairs by multiplication, and one log10 per evaluation turns the product into
 // CalcAllFamLogLikelihood.  Sum-of-logs == log-of-product exactly in real arithmetic; the floating-point
 // result is at least as accurate as the reference's serial sum (DESIGN.md "Numerics").
-#define PM_LOG10_2_HI 0x1.3441350800000p-2
-#define PM_LOG10_2_LO 0x1.f79fef311f12bp-34
 
 template <int S, bool GEN>
 __device__ __forceinline__ void lane_prod(double f, const int4* unit, const double (*cond)[9], const int* fl, int pmode, double& m,
@@ -1416,41 +1414,6 @@ __device__ __forceinline__ void lane_poly_r(double r, double g4, const double (*
 }
 
 
-// One step of the wave product reduction on the DPP crossbar (VALU latency, no LDS round trip): multiply
-// by the (mantissa, exponent) of the lane selected by CTRL; rows outside ROWMASK keep their value (the
-// DPP `old` operand is the identity 1.0 x 2^0).
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ void dpp_prod_step(double& m, int& e) {
-  const int lo = __double2loint(m), hi = __double2hiint(m);
-  int olo, ohi, oe;
-  if constexpr (ROWMASK == 0xF) {   // every row written: no identity `old` operand (saves its two v_mov per step)
-    olo = __builtin_amdgcn_mov_dpp(lo, CTRL, 0xF, 0xF, false);
-    ohi = __builtin_amdgcn_mov_dpp(hi, CTRL, 0xF, 0xF, false);
-    oe = __builtin_amdgcn_update_dpp(0, e, CTRL, ROWMASK, 0xF, false);   // (folds into one v_add_u32_dpp)
-  } else {
-    olo = __builtin_amdgcn_update_dpp(0, lo, CTRL, ROWMASK, 0xF, false);
-    ohi = __builtin_amdgcn_update_dpp(0x3FF00000, hi, CTRL, ROWMASK, 0xF, false);
-    oe = __builtin_amdgcn_update_dpp(0, e, CTRL, ROWMASK, 0xF, false);
-  }
-  m = m * __hiloint2double(ohi, olo);   // no renormalisation: 64 factors in [1/16, 1) stay >= 2^-256
-  e += oe;
-}
-
-// Product of the 64 lanes' (m, e), in a fixed order: quad xor 1, quad xor 2, half-row mirror, row mirror
-// (every lane of a row of 16 then holds the row product), row_bcast15 / row_bcast31 (lane 63 ends with
-// ((R3 R2)(R1 R0))), broadcast from lane 63.  Deterministic for any batch, identical in every lane.
-__device__ __forceinline__ void wave_prod(double& m, int& e) {
-  dpp_prod_step<0xB1, 0xF>(m, e);    // quad_perm [1,0,3,2]
-  dpp_prod_step<0x4E, 0xF>(m, e);    // quad_perm [2,3,0,1]
-  dpp_prod_step<0x141, 0xF>(m, e);   // row_half_mirror
-  dpp_prod_step<0x140, 0xF>(m, e);   // row_mirror
-  dpp_prod_step<0x142, 0xA>(m, e);   // row_bcast:15 -> rows 1, 3
-  dpp_prod_step<0x143, 0xC>(m, e);   // row_bcast:31 -> rows 2, 3
-  const int lo = __builtin_amdgcn_readlane(__double2loint(m), 63), hi = __builtin_amdgcn_readlane(__double2hiint(m), 63);
-  int ev;
-  m = frexp(__hiloint2double(hi, lo), &ev);   // one normalisation (exact: the mantissa bits are those of the
-  e = __builtin_amdgcn_readlane(e, 63) + ev;  // step-wise normalised product, scalings by 2^k being exact)
-}
 
 // Sum of the 64 lanes' doubles in the same DPP order as wave_prod, broadcast from lane 63 (exact for integer values
 // whose partial sums stay below 2^53: k_prep's read statistics and PL sums)
@@ -1480,18 +1443,6 @@ __device__ __forceinline__ double sgpr_const(double c) {
   asm volatile("" : "+s"(c));
   return c;
 }
-// n / d for a finite n and a positive d in the normal range, from the hardware reciprocal: two Newton steps and one
-// residual correction (within an ulp of the IEEE quotient; 8 dependent operations instead of the 11 of the IEEE
-// division sequence, which matters on the serial per-evaluation path of Brent)
-__device__ __forceinline__ double pos_div(double n, double d) {
-  double y = __builtin_amdgcn_rcp(d);
-  double e = fma(-d, y, 1.0);
-  y = fma(y, e, y);
-  e = fma(-d, y, 1.0);
-  y = fma(y, e, y);
-  const double q = n * y;
-  return fma(fma(-d, q, n), y, q);
-}
 
 __device__ __forceinline__ double log10_mant(double m, int e) {
   if (m == 0.0) return -INFINITY;   // an underflowed family product: log10(0), as the reference
@@ -1515,25 +1466,6 @@ __device__ __forceinline__ double log10_mant(double m, int e) {
   return ln * PM_INV_LN10 + (de * PM_LOG10_2_HI + de * PM_LOG10_2_LO);
 }
 
-// log10(m * 2^e) for a WAVE-UNIFORM normalised mantissa m in [0.5, 1) (or 0): the top 7 fraction bits of m pick
-// c_i ~ 1 / m and L_i = -log10(c_i) (log_table.h, scalar loads at a uniform index), z = m c_i - 1 (one rounding, |z|
-// < 2^-8), log10(1 + z) by a degree-6 Horner series (truncation < 5e-19); absolute error ~1e-16, like log10_mant's,
-// in ~12 VALU operations instead of ~40 and without the division.  (Brent's serial path: every objective evaluation.)
-#include "log_table.h"
-static __constant__ double c_log10_tab[256] = PM_LOG10_TAB_VALUES;
-__device__ __forceinline__ double log10_mant_u(double m, int e) {
-  if (m == 0.0) return -INFINITY;
-  const int i = (__builtin_amdgcn_readfirstlane(__double2hiint(m)) >> 13) & 0x7F;
-  const double c = c_log10_tab[2 * i], L = c_log10_tab[2 * i + 1];
-  const double z = fma(m, c, -1.0);
-  double p = fma(z, PM_LOG10_SER_6, PM_LOG10_SER_5);
-  p = fma(z, p, PM_LOG10_SER_4);
-  p = fma(z, p, PM_LOG10_SER_3);
-  p = fma(z, p, PM_LOG10_SER_2);
-  p = fma(z, p, PM_LOG10_SER_1);
-  const double de = (double)e;
-  return fma(z, p, L) + (de * PM_LOG10_2_HI + de * PM_LOG10_2_LO);
-}
 #ifndef PM_LOG10_TAB
 #define PM_LOG10_TAB 1   // block_logprod's log10: the table form (0: the atanh series of log10_mant)
 #endif

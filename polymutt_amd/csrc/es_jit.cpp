@@ -10,6 +10,7 @@
 #include <map>
 #include <mutex>
 #include "../../include/polymutt_engine.h"
+#include "jit_headers.inc"   // kBrentCoreH, kLogTableH: csrc/brent_core.h and csrc/log_table.h as text
 
 namespace pmjit {
 namespace {
@@ -103,7 +104,10 @@ int g_bapf = 0;           // es_hoist_jit: PL bytes of the thread's next (item, 
                           // largest family (0: off, the default -- PM_ES_BAPF=1 turns it on for families of <= 12)
 
 // One family shape's hoisting as a device function: the polynomial of FamilyLikelihoodES' BA peel in (f, g).
-std::string gen_family(const Family& F, int chrom, const double (*T)[27], const std::string& name, double* ops) {
+// fused: the ep_brent_jit form -- inlined, the D + 1 coefficients into the caller's register array out[0..D] (no degree
+// word); *deg = D.
+std::string gen_family(const Family& F, int chrom, const double (*T)[27], const std::string& name, double* ops,
+                       bool fused = false, int* deg = nullptr) {
   Gen G;
   const int n = F.n;
   const bool X = chrom == PM_CHR_X, Y = chrom == PM_CHR_Y, MT = chrom == PM_CHR_MT;
@@ -182,6 +186,15 @@ std::string gen_family(const Family& F, int chrom, const double (*T)[27], const 
   }
   // CalculateLikelihood_BA (:1013-1032): the final person's partials summed
   Poly L = G.add(G.add(P[fin][0], P[fin][1]), P[fin][2]);
+  if (deg) *deg = L.d;
+  *ops = (double)G.ops;
+  if (fused) {
+    std::string out = "__device__ __forceinline__ void " + name +
+                      "(const unsigned char* __restrict__ P11, const unsigned char* __restrict__ P12, "
+                      "const unsigned char* __restrict__ P22, int p0, const double* __restrict__ lk, double* out) {\n" + G.code;
+    for (int a = 0; a <= L.d; a++) out += "  out[" + std::to_string(a) + "] = " + (L.c[a].empty() ? "0.0" : L.c[a]) + ";\n";
+    return out + "}\n";
+  }
   std::string out = g_bapf ? "__device__ __forceinline__ void " + name +   // (inlined: b stays in registers)
                                  "(const unsigned int* b, const double* __restrict__ lk, double* __restrict__ out, int os, int dcap) {\n" +
                                  G.code
@@ -191,7 +204,6 @@ std::string gen_family(const Family& F, int chrom, const double (*T)[27], const 
                                  "int os, int dcap) {\n" + G.code;
   for (int a = 0; a <= L.d; a++) out += "  out[" + std::to_string(a) + " * os] = " + (L.c[a].empty() ? "0.0" : L.c[a]) + ";\n";
   out += "  out[(dcap - 1) * os] = " + std::to_string(L.d) + ".0;\n}\n";
-  *ops = (double)G.ops;
   return out;
 }
 
@@ -1664,7 +1676,10 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
 
 bool compile(const std::string& src, std::vector<char>* code, std::string* err, const std::string& arch) {
   hiprtcProgram prog;
-  if (hiprtcCreateProgram(&prog, src.c_str(), "es_hoist_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+  // the shared device headers (brent_core.h, log_table.h), embedded at build time (Makefile: build/jit_headers.inc)
+  const char* hdr[] = {kBrentCoreH, kLogTableH};
+  const char* hdr_names[] = {"brent_core.h", "log_table.h"};
+  if (hiprtcCreateProgram(&prog, src.c_str(), "es_hoist_jit.hip", 2, hdr, hdr_names) != HIPRTC_SUCCESS) {
     *err = "hiprtcCreateProgram failed";
     return false;
   }
@@ -1727,6 +1742,230 @@ bool build(int device, int chrom, const std::vector<Family>& fams, const double 
     out->blocks_per_cu = nb;
     if (getenv("PM_JIT_LAYOUT")) fprintf(stderr, "es_hoist_wave: wpb %d ws %d blocks/CU %d\n", out->wpb, out->ws, nb);
   }
+  out->compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return true;
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// ep_brent_jit: the fused hoisting + Brent kernel (es_jit.h FusedKernel).  Layout: families sorted by (degree
+// descending, shape), dealt row-major onto rows of `lanes` cells; each row's register tile holds its largest degree
+// + 1 coefficients.  The lane count is chosen by a cost model of one item: hoisting = the generated peels' operations
+// of every shape present in a row (a row's lanes run the shapes it holds one after the other), evaluations = about
+// 30 Brent evaluations x 2 (D_row + 1) Horner operations per row; a lane's degrees summed stay <= 64 (g^D >= 1e-256
+// at Brent's start b = 0.9999) and the tiles <= 64 doubles.
+std::string generate_fused(int chrom, const std::vector<Family>& fams, const double (*tba)[27], FusedKernel* out) {
+  const int n = (int)fams.size();
+  out->lane_tab.clear(); out->row_deg.clear(); out->rows = out->lanes = out->n_shapes = 0; out->item_ops = 0;
+  if (n == 0) return "";
+  std::map<std::string, int> shape_of;
+  std::vector<std::string> bodies;
+  std::vector<int> sdeg;
+  std::vector<double> sops;
+  std::vector<int> sig(n);
+  for (int i = 0; i < n; i++) {
+    const std::string key = shape_key(fams[i]);
+    auto it = shape_of.find(key);
+    if (it == shape_of.end()) {
+      const int id = (int)bodies.size();
+      shape_of[key] = id;
+      double o = 0;
+      int d = 0;
+      bodies.push_back(gen_family(fams[i], chrom, tba, "ffam" + std::to_string(id), &o, true, &d));
+      sdeg.push_back(d);
+      sops.push_back(o);
+      sig[i] = id;
+    } else sig[i] = it->second;
+  }
+  const int ns = (int)bodies.size();
+  if (ns > 127) return "";
+  std::vector<int> order(n);
+  for (int i = 0; i < n; i++) order[i] = i;
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+    return sdeg[sig[a]] != sdeg[sig[b]] ? sdeg[sig[a]] > sdeg[sig[b]] : sig[a] < sig[b];
+  });
+  const int kRowsMax = 8, kTile = 64, kEvals = 30;
+  double best = -1;
+  int best_nl = 0;
+  for (int nl = (n + kRowsMax - 1) / kRowsMax; nl <= 64; nl++) {
+    if (nl <= 0) continue;
+    const int rows = (n + nl - 1) / nl;
+    double cost = 0;
+    int tile = 0;
+    std::vector<int> lane_deg(nl, 0);
+    for (int r = 0; r < rows; r++) {
+      std::vector<char> seen(ns, 0);
+      int dmax = 0;
+      for (int k = r * nl; k < std::min(n, (r + 1) * nl); k++) {
+        const int sg = sig[order[k]];
+        if (!seen[sg]) { seen[sg] = 1; cost += sops[sg]; }
+        dmax = std::max(dmax, sdeg[sg]);
+        lane_deg[k - r * nl] += sdeg[sg];
+      }
+      tile += dmax + 1;
+      cost += kEvals * 2.0 * (dmax + 1);
+    }
+    if (tile > kTile || *std::max_element(lane_deg.begin(), lane_deg.end()) > 64) continue;
+    if (best < 0 || cost < best) { best = cost; best_nl = nl; }
+  }
+  if (best_nl == 0) return "";
+  const int nl = best_nl, rows = (n + nl - 1) / nl;
+  out->lanes = nl; out->rows = rows; out->n_shapes = ns;
+  out->lane_tab.assign((size_t)rows * 64 + 64, -1);
+  for (int l = 0; l < 64; l++) out->lane_tab[(size_t)rows * 64 + l] = 0;
+  std::vector<std::vector<int>> row_shapes(rows);
+  for (int r = 0; r < rows; r++) {
+    int dmax = 0;
+    for (int k = r * nl; k < std::min(n, (r + 1) * nl); k++) {
+      const Family& F = fams[order[k]];
+      const int sg = sig[order[k]], l = k - r * nl;
+      out->lane_tab[(size_t)r * 64 + l] = F.p0 | (sg << 24);
+      out->lane_tab[(size_t)rows * 64 + l] += sdeg[sg];
+      if (std::find(row_shapes[r].begin(), row_shapes[r].end(), sg) == row_shapes[r].end()) row_shapes[r].push_back(sg);
+      dmax = std::max(dmax, sdeg[sg]);
+    }
+    out->row_deg.push_back(dmax);
+  }
+  for (int i = 0; i < n; i++) out->item_ops += sops[sig[i]];
+  if (getenv("PM_JIT_LAYOUT")) {
+    fprintf(stderr, "ep_brent_jit: %d families, %d shapes, %d rows x %d lanes, tiles", n, ns, rows, nl);
+    for (int r = 0; r < rows; r++) fprintf(stderr, " %d(%zu)", out->row_deg[r], row_shapes[r].size());
+    fprintf(stderr, ", cost %.0f\n", best);
+  }
+  std::string src = kPrologue;
+  src += "#include \"brent_core.h\"\n";
+  src += R"(
+struct FusedArgs {
+  const int* items; int* counts; const uint8_t* ref; const int* res; const uint8_t* pl; const double* lktab; const int* lane_tab;
+  double* raw; double* minv; int* evals; unsigned long long* eval_total;
+  double precision;
+  int list, it0, it1, np, vcf, res_words, res_a1, res_a2, itmax, pad;
+};
+)";
+  for (auto& b : bodies) src += b;
+  const char* wpe = getenv("PM_FUSED_WPE");   // (experiments: amdgpu_waves_per_eu of the kernel)
+  src += std::string("extern \"C\" __global__ void __launch_bounds__(64) ") +
+         (wpe ? "__attribute__((amdgpu_waves_per_eu(" + std::string(wpe) + ", " + std::string(wpe) + "))) " : "") +
+         "ep_brent_jit(FusedArgs A) {\n";
+  src += R"(  __shared__ double lk[256];
+  for (int i = threadIdx.x; i < 256; i += 64) lk[i] = A.lktab[i];
+  __syncthreads();
+  const int lane = threadIdx.x;
+  const int nItems = min(A.counts[A.list], A.it1);
+  // XCD-aware item order (blocks go round-robin to the 8 XCDs): consecutive items -- one site's configurations, one
+  // PL block -- on blocks of one XCD
+  const int vb = (gridDim.x % 8 == 0) ? (blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8 : blockIdx.x;
+)";
+  src += "  int ltab[" + std::to_string(rows) + "];\n";
+  src += "#pragma unroll\n  for (int r = 0; r < " + std::to_string(rows) + "; r++) ltab[r] = A.lane_tab[r * 64 + lane];\n";
+  src += "  const int edl = A.lane_tab[" + std::to_string(rows * 64) + " + lane];   // g^edl: the lane's degrees summed\n";
+  src += R"(  unsigned long long ev_acc = 0;
+  for (int it = A.it0 + vb; it < nItems; it += gridDim.x) {
+    const int item = A.items[it];
+    const int site = item >> 3, cfg = item & 7, rb = A.ref[site];
+    int a1, a2;
+    if (A.vcf) { a1 = rb & 15; a2 = rb >> 4; }
+    else if (cfg == 7) { a1 = A.res[(size_t)site * A.res_words + A.res_a1]; a2 = A.res[(size_t)site * A.res_words + A.res_a2]; }
+    else cfg_alleles(cfg, rb, &a1, &a2);
+    const uint8_t* pls = A.pl + (size_t)site * A.np * 10;
+    const uint8_t* P11 = pls + (size_t)gi(a1, a1) * A.np;
+    const uint8_t* P12 = pls + (size_t)gi(a1, a2) * A.np;
+    const uint8_t* P22 = pls + (size_t)gi(a2, a2) * A.np;
+)";
+  for (int r = 0; r < rows; r++) {
+    const int D = out->row_deg[r];
+    const std::string c = "c" + std::to_string(r), R = std::to_string(r);
+    src += "    double " + c + "[" + std::to_string(D + 1) + "];\n";
+    src += "    if (ltab[" + R + "] < 0) {   // no family: the unit polynomial\n      " + c + "[0] = 1.0;\n";
+    for (int a = 1; a <= D; a++) src += "      " + c + "[" + std::to_string(a) + "] = 0.0;\n";
+    src += "    } else {\n      const int p0 = ltab[" + R + "] & 0xFFFFFF, sg = ltab[" + R + "] >> 24;\n";
+    for (size_t k = 0; k < row_shapes[r].size(); k++) {
+      const int sg = row_shapes[r][k];
+      src += std::string(k == 0 ? "      " : " else ") +
+             (k + 1 < row_shapes[r].size() ? "if (sg == " + std::to_string(sg) + ") " : "") + "{\n";
+      src += "        ffam" + std::to_string(sg) + "(P11, P12, P22, p0, lk, " + c + ");\n";
+      for (int a = sdeg[sg] + 1; a <= D; a++) src += "        " + c + "[" + std::to_string(a) + "] = 0.0;\n";
+      src += "      }";
+    }
+    src += "\n    }\n";
+  }
+  src += R"(    PmBrent B;
+    pm_brent_init(B, A.precision, A.itmax);
+    for (;;) {
+      // every family L = g^D sum_a c_a t^a, t = f / g (non-negative terms: no cancellation), FMA Horner over the row's
+      // tile (zeros above a family's own degree leave the sum's bits unchanged); the values split into mantissa and
+      // exponent, multiplied in one chain with g^edl, one renormalisation -- as k_brent's EP evaluation
+      const double g = 1.0 - B.x;
+      const double t = pos_div(B.x, g);
+      double gp = g, pw = 1.0;
+#pragma unroll
+      for (int b = 0; b < 7; b++) {
+        pw = ((edl >> b) & 1) ? pw * gp : pw;
+        gp = gp * gp;
+      }
+      int e = 0;
+)";
+  for (int r = 0; r < rows; r++) {
+    const int D = out->row_deg[r];
+    const std::string c = "c" + std::to_string(r), R = std::to_string(r);
+    src += "      double m" + R + ";\n      {\n        double acc = " + c + "[" + std::to_string(D) + "];\n";
+    for (int a = D - 1; a >= 0; a--) src += "        acc = fma(acc, t, " + c + "[" + std::to_string(a) + "]);\n";
+    src += "        int e1;\n        m" + R + " = frexp(acc, &e1);\n        e += e1;\n      }\n";
+  }
+  src += "      double m = m0";
+  for (int r = 1; r < rows; r++) src += " * m" + std::to_string(r);
+  src += R"(;
+      int e2;
+      m = frexp(m * pw, &e2);
+      e += e2;
+      wave_prod(m, e);
+      if (!pm_brent_feed(B, -log10_mant_u(m, e))) break;
+    }
+    if (lane == 0) {
+      A.raw[(size_t)site * 8 + cfg] = -B.fmin;
+      A.minv[(size_t)site * 8 + cfg] = B.mn;
+      A.evals[(size_t)site * 8 + cfg] = B.nev;
+      ev_acc += B.nev - 2;   // objective evaluations computed (f(a), f(c) counted only)
+      if (!B.ok) { atomicExch(&A.counts[5], 1); atomicMin(&A.counts[6], site); }   // (the reference stops at the first)
+    }
+  }
+  if (lane == 0 && ev_acc) atomicAdd(A.eval_total, ev_acc);
+}
+)";
+  return src;
+}
+
+bool build_fused(int device, int chrom, const std::vector<Family>& fams, const double (*tba)[27], FusedKernel* out,
+                 std::string* err) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const std::string src = generate_fused(chrom, fams, tba, out);
+  if (src.empty()) { *err = "the families do not fit the fused kernel's register tiles"; return false; }
+  std::lock_guard<std::mutex> lock(g_mu);
+  auto key = std::make_pair(device, src);
+  auto it = g_modules.find(key);
+  if (it == g_modules.end()) {
+    std::vector<char> code;
+    std::string arch = "gfx950";
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.gcnArchName[0]) {
+      arch = prop.gcnArchName;
+      arch = arch.substr(0, arch.find(':'));
+    }
+    if (!compile(src, &code, err, arch)) return false;
+    hipModule_t mod;
+    if (hipSetDevice(device) != hipSuccess || hipModuleLoadData(&mod, code.data()) != hipSuccess) {
+      *err = "hipModuleLoadData of the fused Brent kernel failed";
+      return false;
+    }
+    it = g_modules.emplace(key, mod).first;
+  }
+  if (hipModuleGetFunction(&out->fn, it->second, "ep_brent_jit") != hipSuccess) {
+    *err = "hipModuleGetFunction(ep_brent_jit) failed";
+    return false;
+  }
+  int nb = 0;
+  if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, out->fn, 64, 0) != hipSuccess) nb = 0;
+  out->blocks_per_cu = nb;
+  if (getenv("PM_JIT_LAYOUT")) fprintf(stderr, "ep_brent_jit: blocks/CU %d\n", nb);
   out->compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return true;
 }

@@ -78,6 +78,40 @@ struct Kernel {
   std::vector<int> pair_k;   // [2 npairs] slot indices of each pair (an unpaired slot: twice)
 };
 
+// The fused Elston-Stewart Brent kernel ep_brent_jit (bi-allelic engines whose every family is peeled: config 4): one wave
+// per Brent item, each lane hoisting its families' polynomials straight into registers (the shape's generated peel,
+// inlined) and then running the item's whole OptimizeFrequency + Brent on them -- no es_coef round trip through HBM and
+// one launch per list instead of a hoisting launch and a Brent launch.  Families sit on (row, lane) cells: sorted by
+// (degree, shape), rows of `lanes` cells, so a row's register tile is its largest degree + 1 and few shapes share a row.
+struct FusedArgs {
+  const int* items;          // the list's items (site << 3 | cfg)
+  int* counts;               // counts[list] = list size; [5] / [6] Brent stuck flag / first stuck site (atomics)
+  const uint8_t* ref;        // [site] refBase (vcf_mode: a1 | a2 << 4)
+  const int* res;            // pm_site_result as int32 words (cfg-7 items read allele1/allele2)
+  const uint8_t* pl;         // genotype-planar site blocks
+  const double* lktab;       // [256] phred -> likelihood
+  const int* lane_tab;       // [rows][64] p0 | shape << 24 (-1: no family), then [64] each lane's degrees summed
+  double* raw;               // [site][8] -fmin
+  double* minv;              // [site][8] minimiser
+  int* evals;                // [site][8] objective evaluations (the reference's count)
+  unsigned long long* eval_total;
+  double precision;
+  int list, it0, it1, np, vcf, res_words, res_a1, res_a2, itmax, pad;
+};
+struct FusedKernel {
+  hipFunction_t fn = nullptr;
+  std::vector<int> lane_tab;   // rows * 64 + 64 ints (FusedArgs::lane_tab)
+  std::vector<int> row_deg;    // each row's register tile degree
+  int rows = 0, lanes = 0, n_shapes = 0, blocks_per_cu = 0;
+  double item_ops = 0;         // FP64 operations of one item's hoisting over every family (the generated peels)
+  double compile_ms = 0;
+};
+// The generated source of ep_brent_jit for `fams` (fills out's layout; no device needed); "" when the families do not
+// fit the register tiles (then the engine keeps es_hoist_jit + k_brent).
+std::string generate_fused(int chrom, const std::vector<Family>& fams, const double (*tba)[27], FusedKernel* out);
+bool build_fused(int device, int chrom, const std::vector<Family>& fams, const double (*tba)[27], FusedKernel* out,
+                 std::string* err);
+
 // Packs family f's ES_Peeling schedule (pm_pedigree.steps) with its marriage-partial slots resolved the way the
 // reference's partial map behaves; appends to out; returns the workspace doubles of a reference-order peel with ns
 // states, -1 if it cannot be packed.
@@ -89,6 +123,7 @@ int pack_steps(const pm_pedigree* ped, int f, int ns, std::vector<int2>& out);
 // (no whole 10-state / top variants: their larger workspace would set every wave's LDS slice).
 std::string generate(int chrom, const std::vector<Family>& fams, const double (*tba)[27], Kernel* out, int denovo = 0);
 // hipRTC compile of a generated source for gfx950 (no device needed).
+// (the source may #include "brent_core.h" / "log_table.h": their text is embedded in the library)
 bool compile(const std::string& src, std::vector<char>* code, std::string* err, const std::string& arch = "gfx950");
 
 // Generates and compiles the hoisting and posterior kernels of `fams` for chromosome class `chrom` (PM_CHR_*); bi-allelic

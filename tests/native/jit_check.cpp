@@ -65,5 +65,26 @@ int main(int argc, char** argv) {
     printf("class %d shapes %d families %zu source %zu code %zu compile_ms %.0f%s ops%s\n", cls, K.n_shapes, fams.size(), src.size(),
            code.size(), ms, dn ? (" denovo wpb " + std::to_string(K.wpb) + " ws " + std::to_string(K.ws)).c_str() : "", ops.c_str());
   }
+  // the fused hoisting + Brent kernel of bi-allelic engines (ep_brent_jit), every class
+  for (int cls = 0; cls < 4; cls++) {
+    pmjit::FusedKernel F;
+    const std::string src = pmjit::generate_fused(cls, fams, kTBA, &F);
+    if (src.empty()) { printf("fused %d none\n", cls); continue; }
+    if (!emit.empty() && cls == 0) {
+      FILE* fh = fopen((emit + ".fused").c_str(), "w");
+      if (fh) { fputs(src.c_str(), fh); fclose(fh); }
+    }
+    std::vector<char> code;
+    std::string err;
+    if (!pmjit::compile(src, &code, &err)) { fprintf(stderr, "fused class %d: %s\n", cls, err.c_str()); return 1; }
+    if (!emit.empty() && cls == 0) {
+      FILE* fh = fopen((emit + ".fused.co").c_str(), "wb");
+      if (fh) { fwrite(code.data(), 1, code.size(), fh); fclose(fh); }
+    }
+    std::string tiles;
+    for (int d : F.row_deg) tiles += " " + std::to_string(d);
+    printf("fused %d shapes %d rows %d lanes %d item_ops %.0f code %zu tiles%s\n", cls, F.n_shapes, F.rows, F.lanes, F.item_ops,
+           code.size(), tiles.c_str());
+  }
   return 0;
 }

@@ -74,16 +74,20 @@ _ES_CASES = [n for n in DUMP_CASES if n.startswith(("ext10", "roof", "roof2", "e
 
 @pytest.mark.parametrize("name", _ES_CASES)
 def test_es_hoisting_kernels_agree(built, tmp_path, monkeypatch, name):
-    """The two hoisting paths of the polynomial-form Elston-Stewart peel -- the compiled schedule (es_jit, the
-    default for bi-allelic engines) and the generic wave-per-family kernel k_es_hoist (PM_NO_JIT=1) -- both match
-    the reference dump of every extended-pedigree case (all chromosome classes the fixtures hold)."""
+    """The three paths of the polynomial-form Elston-Stewart peel -- the fused compiled kernel (ep_brent_jit: hoisting
+    into registers + Brent in one launch, the default for bi-allelic engines whose every family is peeled), the
+    compiled hoisting kernel es_hoist_jit + k_brent (PM_NO_FUSED=1) and the generic wave-per-family kernel k_es_hoist
+    (PM_NO_JIT=1) -- all match the reference dump of every extended-pedigree case (all chromosome classes the fixtures
+    hold)."""
     import numpy as np
     case = make_dataset(name, str(tmp_path))
     ped, secs, _ = read_dataset(str(tmp_path))
     par, chrom = params_and_chrom(case["flags"], numerics=pm.NUM_POLY)
     (label, pos, ref, pl, dm), = secs
     out, rows = {}, {}
-    for mode in ("jit", "generic"):
+    for mode in ("fused", "jit", "generic"):
+        if mode == "jit":
+            monkeypatch.setenv("PM_NO_FUSED", "1")
         if mode == "generic":
             monkeypatch.setenv("PM_NO_JIT", "1")
         eng = pm.Engine(ped.view, par, max_batch=256)
@@ -94,7 +98,7 @@ def test_es_hoisting_kernels_agree(built, tmp_path, monkeypatch, name):
         rows[mode] = [r[1] for r in runs]
         compare_to_dump(out[mode], golden_dump(name), label=f"{name} {mode} ")
     for k in ("status", "n_cfg", "maxidx", "emit"):
-        assert (out["jit"][k] == out["generic"][k]).all(), k
+        assert (out["jit"][k] == out["generic"][k]).all() and (out["fused"][k] == out["jit"][k]).all(), k
     # genotype rows: the compiled posterior peels follow the reference-order peel term by term -- bit-identical
     # (unless a flat-objective minimiser divergence moved the posterior frequency: af compared to the dump above)
     if (out["jit"]["af"] == out["generic"]["af"]).all():
