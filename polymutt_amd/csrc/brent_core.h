@@ -66,6 +66,24 @@ __device__ __forceinline__ void wave_prod(double& m, int& e) {
   e = __builtin_amdgcn_readlane(e, 63) + ev;  // step-wise normalised product, scalings by 2^k being exact)
 }
 
+// The same product over each half-wave (lanes 0-31 and 32-63: two Brent items per wave): the first five steps (rows 0+1
+// end in lane 31, rows 2+3 in lane 63), then each half takes its own lane's product -- the order of wave_prod's first
+// five steps.  Every lane of a half ends with that half's (m, e), m normalised.
+__device__ __forceinline__ void wave_prod_pair(double& m, int& e) {
+  dpp_prod_step<0xB1, 0xF>(m, e);    // quad_perm [1,0,3,2]
+  dpp_prod_step<0x4E, 0xF>(m, e);    // quad_perm [2,3,0,1]
+  dpp_prod_step<0x141, 0xF>(m, e);   // row_half_mirror
+  dpp_prod_step<0x140, 0xF>(m, e);   // row_mirror
+  dpp_prod_step<0x142, 0xA>(m, e);   // row_bcast:15 -> rows 1, 3
+  const double mA = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(m), 31), __builtin_amdgcn_readlane(__double2loint(m), 31));
+  const double mB = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(m), 63), __builtin_amdgcn_readlane(__double2loint(m), 63));
+  const int eA = __builtin_amdgcn_readlane(e, 31), eB = __builtin_amdgcn_readlane(e, 63);
+  const bool hi = (__lane_id() >> 5) != 0;
+  int ev;
+  m = frexp(hi ? mB : mA, &ev);
+  e = (hi ? eB : eA) + ev;
+}
+
 // log10(m * 2^e) for a WAVE-UNIFORM normalised mantissa m in [0.5, 1) (or 0): the top 7 fraction bits of m pick
 // c_i ~ 1 / m and L_i = -log10(c_i) (log_table.h, scalar loads at a uniform index), z = m c_i - 1 (one rounding, |z|
 // < 2^-8), log10(1 + z) by a degree-6 Horner series (truncation < 5e-19); absolute error ~1e-16, like log10_mant's,
@@ -83,6 +101,25 @@ __device__ __forceinline__ double log10_mant_u(double m, int e) {
   p = fma(z, p, PM_LOG10_SER_1);
   const double de = (double)e;
   return fma(z, p, L) + (de * PM_LOG10_2_HI + de * PM_LOG10_2_LO);
+}
+
+// log10_mant_u for a mantissa uniform over each half-wave (wave_prod_pair): the two halves' table entries by scalar loads
+// at their (uniform) indices, each lane computing with its half's -- the same operations as log10_mant_u
+__device__ __forceinline__ double log10_mant_pair(double m, int e) {
+  const int hA = __builtin_amdgcn_readlane(__double2hiint(m), 31), hB = __builtin_amdgcn_readlane(__double2hiint(m), 63);
+  const int iA = (hA >> 13) & 0x7F, iB = (hB >> 13) & 0x7F;
+  const bool hi = (__lane_id() >> 5) != 0;
+  const double c = hi ? c_log10_tab[2 * iB] : c_log10_tab[2 * iA];
+  const double L = hi ? c_log10_tab[2 * iB + 1] : c_log10_tab[2 * iA + 1];
+  const double z = fma(m, c, -1.0);
+  double p = fma(z, PM_LOG10_SER_6, PM_LOG10_SER_5);
+  p = fma(z, p, PM_LOG10_SER_4);
+  p = fma(z, p, PM_LOG10_SER_3);
+  p = fma(z, p, PM_LOG10_SER_2);
+  p = fma(z, p, PM_LOG10_SER_1);
+  const double de = (double)e;
+  const double r = fma(z, p, L) + (de * PM_LOG10_2_HI + de * PM_LOG10_2_LO);
+  return m == 0.0 ? -__builtin_inf() : r;
 }
 
 // OptimizeFrequency + Brent as a state machine (the same operations, in the same order, as k_brent's loop):

@@ -97,6 +97,7 @@ struct pm_engine {
   bool units_empty = false, units1_empty = false;   // a lane plan with no nuclear or founder unit (every family peeled)
   std::vector<std::pair<const void*, int>> ep_bpc;   // EP one-wave k_brent blocks resident per CU, per instantiation
   bool all_trio = false;   // every unit of the lane plan is a 3-person nuclear family (or empty): k_brent's NF = 3
+  bool split34 = false;    // plan_split34: quads in the first half of the slot rows, trios in the second (NF = 34)
   int4* d_units_q = nullptr;
   int* d_items[N_LISTS] = {nullptr, nullptr, nullptr};
   int* d_counts = nullptr;
@@ -184,6 +185,25 @@ static bool plan_units(const pm_pedigree* ped, int T, int S, std::vector<int4>& 
     lane = (lane + 1) % T;
   }
   return true;
+}
+
+// Split plan for pedigrees of trios and quads only (config 5's 2000 mixed families): quads dealt round-robin over the lanes
+// of slot rows [0, S/2), trios over rows [S/2, S), so the lean PF kernel hoists each half with its family size known
+// (k_brent NF = 34).  false when either kind does not fit its half.
+static bool plan_split34(const pm_pedigree* ped, int T, int S, std::vector<int4>& units) {
+  if (S < 2 || S % 2) return false;
+  units.assign((size_t)T * S, make_int4(U_NONE, -1, 0, 0));
+  int nq = 0, nt = 0;
+  for (int f = 0; f < ped->n_fam; f++) {
+    const int p0 = ped->fam_start[f], n = ped->fam_start[f + 1] - p0;
+    if (ped->fam_kind[f] != PM_FAM_NUCLEAR || (n != 3 && n != 4)) return false;
+    int& c = n == 4 ? nq : nt;
+    const int row = (n == 4 ? 0 : S / 2) + c / T;
+    if (c / T >= S / 2) return false;
+    units[(size_t)row * T + c % T] = make_int4(U_NUC, f, p0, n);
+    c++;
+  }
+  return nq > 0 && nt > 0;
 }
 
 // pack_steps: es_jit.cpp (pmjit::pack_steps), shared with the schedule compiler.
@@ -459,6 +479,12 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
       if (pref[i].x >= tmin && plan_units(ped, pref[i].x, pref[i].y, units)) { E->T = pref[i].x; E->S = pref[i].y; planned = true; }
   }
   if (!planned) { pm_engine_destroy(E); pm_set_last_error("pm_engine_create: pedigree too large for the lane plan"); return PM_EPED; }
+  // mixed trio / quad pedigrees on the lean one- or two-wave 16-slot plans: the split layout (PM_NO_SPLIT34=1: off)
+  if (!par->denovo && par->numerics == PM_NUM_POLY && !E->has_fp && E->n_ext == 0 && E->S == 16 && (E->T == 64 || E->T == 128) &&
+      !getenv("PM_NO_SPLIT34")) {
+    std::vector<int4> u2;
+    if (plan_split34(ped, E->T, E->S, u2)) { units.swap(u2); E->split34 = true; }
+  }
   {   // QUAD plan: each nuclear family's four PL bytes of a genotype plane form one aligned dword
     bool q = E->n_person % 16 == 0 && !E->has_fp && E->T == 64;
     int full = E->S;
@@ -818,7 +844,7 @@ typedef void (*BrentFn)(DevArgs, int);
 // pd_hi: the plan's peeled families reach a polynomial degree above PM_PD_LO (one-wave EP plans then take the
 // PM_PD_HI register tile; degrees above that are evaluated from the coefficient buffer)
 static BrentFn brent_kernel(int T, int S, int num, bool gen, bool es, bool dn = false, bool pf = false, bool ep = false, bool trio = false,
-                            bool epo = false, bool pd_hi = false) {
+                            bool epo = false, bool pd_hi = false, bool split34 = false) {
   const int n = (num == PM_NUM_POLY && gen) ? PM_NUM_PRODUCT : num;
   if (es && ep && epo && T == 64 && (S == 1 || S == 2 || S == 4)) {   // ep_only plans: the nuclear machinery compiled out
 #define PMKEO(s) \
@@ -845,6 +871,10 @@ static BrentFn brent_kernel(int T, int S, int num, bool gen, bool es, bool dn = 
   }
   if (dn && !gen && !es && n == PM_NUM_POLY && pf && T == 64 && S == 16)   // lean --denovo, LDS-staged hoisting only
     return k_brent<64, 16, PM_NUM_POLY, false, false, true, true>;
+  if (pf && !dn && split34 && S == 16) {   // mixed trio / quad split plans
+    if (T == 64) return k_brent<64, 16, PM_NUM_POLY, false, false, false, true, false, false, 34>;
+    if (T == 128) return k_brent<128, 16, PM_NUM_POLY, false, false, false, true, false, false, 34>;
+  }
   if (pf && !dn) {   // lean autosomal kernel with LDS plane prefetch
 #define PMKP(s) if (T == 64 && S == s) return trio ? k_brent<64, s, PM_NUM_POLY, false, false, false, true, false, false, 3> \
                                                    : k_brent<64, s, PM_NUM_POLY, false, false, false, true>;
@@ -980,6 +1010,14 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
   const bool quad = !gen && !unrelated && n_ext == 0 && A.denovo && E->par.numerics == PM_NUM_POLY && E->quad && T == 64 &&
                     (S == 8 || S == 16);
   if (quad) shmem = QWAVE;
+  // QUAD: list 0 holds cfgs 1-3 of each called site and list 1 cfgs 4-6, consecutive and site-aligned (k_prep / k_select
+  // reserve them three at a time): one wave takes a site's three in turn (PM_QD_GROUP=1: one item per step of the grid)
+  A.qd_group = 1;
+  if (quad && A.mono_dn == 2 && (list == 0 || list == 1)) {
+    const char* eg = getenv("PM_QD_GROUP");
+    A.qd_group = eg ? std::max(1, atoi(eg)) : 1;
+    if (A.qd_group != 1 && A.qd_group != 3) A.qd_group = 3;
+  }
   BrentFn qfn = nullptr;
   if (quad) {   // persistent grid = the blocks that are resident at once (PM_QD_WAVES per SIMD): no partial second round
     qfn = S == 16 ? k_brent<64, 16, PM_NUM_POLY, false, false, true, false, false, true>
@@ -1007,7 +1045,8 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
   BrentFn fn = quad ? qfn
                    : brent_kernel(T, S, E->par.numerics, gen, !unrelated && n_ext > 0, A.denovo != 0, A.pf_npad > 0 || A.dn_pf, ep,
                                   E->all_trio && !unrelated && !getenv("PM_NO_TRIO"), ep_only && !getenv("PM_NO_EPO"),
-                                  ep && E->ep_dmax[E->use_plan1 ? 1 : 0][E->chrom] > PM_PD_LO && !getenv("PM_NO_PD_HI"));
+                                  ep && E->ep_dmax[E->use_plan1 ? 1 : 0][E->chrom] > PM_PD_LO && !getenv("PM_NO_PD_HI"),
+                                  E->split34 && !gen && !unrelated && !E->use_plan1);
   if (!fn) { pm_set_last_error("launch_brent: no kernel variant for the lane plan"); return PM_EINVAL; }
   // multi-wave de novo plans (T = 512 / 1024: more than 1024 families) stage 2 buffers per wave: above the
   // default 64 KB dynamic-LDS limit the kernel must opt in, and the block (plus its static LDS: lane plan,
@@ -1166,7 +1205,9 @@ static int run_pipeline(pm_engine* E, int n, const uint8_t* pl, const uint32_t* 
   {   // persons per lane of k_prep: vector loads when n_person allows; the reference's serial mono order in EXACT
     const int np = E->n_person;
     int vmax = 8;   // measured best on 1000 quads (16 and 4 within 1%)
-    void (*prep)(DevArgs, int) = E->par.numerics == PM_NUM_EXACT ? k_prep<1, true>
+    void (*prep)(DevArgs, int) = E->par.numerics == PM_NUM_EXACT ? (E->vcf ? k_prep<1, true, true> : k_prep<1, true>)
+                          : E->vcf ? ((np % 16 == 0 && vmax >= 16) ? k_prep<16, false, true> : (np % 8 == 0 && vmax >= 8) ? k_prep<8, false, true>
+                                      : (np % 4 == 0 && vmax >= 4) ? k_prep<4, false, true> : k_prep<1, false, true>)
                           : (np % 16 == 0 && vmax >= 16) ? k_prep<16, false> : (np % 8 == 0 && vmax >= 8) ? k_prep<8, false>
                           : (np % 4 == 0 && vmax >= 4) ? k_prep<4, false> : k_prep<1, false>;
     // sites per wave: PREP_SPW (PM_PREP_SPW = 1..8 overrides it; fewer sites per wave on config 4's 16 384-site

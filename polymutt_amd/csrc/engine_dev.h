@@ -169,6 +169,7 @@ struct DevArgs {
   int* items[N_LISTS];
   int* counts;             // [0..2] list sizes, [3] rows, [4] first emitted site, [5] Brent stuck, [6] first stuck site
                            // (atomicMin), [8]/[9] quick items/site visits
+  int qd_group;            // QUAD kernel: items per site group of the list (a wave takes a site's items in turn)
   int itmax;               // Brent's ITMAX (MathGold.cpp:98: 200; PM_TEST_ITMAX lowers it for the failure-path tests)
   unsigned long long* eval_total;
   unsigned long long* phase;   // PM_PHASE_TIMING: [0] hoisting, [1] evaluations, [2] items -- k_brent wave time (wall_clock64 ticks)
@@ -736,7 +737,7 @@ __device__ __forceinline__ void fam_poly4(const uint32_t* by, int nn, const doub
     double D[2][3];
 #pragma unroll
     for (int q = 0; q < 2; q++) {
-      const bool kid = NF == 3 ? q == 0 : 2 + q < nn;
+      const bool kid = NF == 3 ? q == 0 : NF == 4 ? true : 2 + q < nn;   // (NF = 4: quads or empty slots)
 #pragma unroll
       for (int k = 0; k < 3; k++) D[q][k] = kid ? lk[by[3 * (2 + q) + k]] : 1.0;
     }
@@ -859,6 +860,28 @@ __device__ __forceinline__ void prefetch_planes(const DevArgs& A, const int* ite
 #ifndef PM_HOIST_CHUNK_LDS
 #define PM_HOIST_CHUNK_LDS 2
 #endif
+// NF = 34: a split plan (plan_split34): slot rows [0, S/2) hold quads (or nothing), rows [S/2, S) trios (or nothing), so
+// each half is hoisted with its family size known -- the quads without the missing-kid selects, the trios without the
+// second kid -- mixed trio / quad pedigrees (config 5's) get the trio plans' saving on half their slots
+template <int NF, int S, int C, int S0, int S1>
+__device__ __forceinline__ void hoist_poly4_lds_rows(const int* uu, const uint8_t* buf, int npad, const double* lk, double (*a)[5]) {
+#pragma unroll
+  for (int s = S0; s < S1; s++) {
+    if (s % C == 0) __builtin_amdgcn_sched_barrier(0);   // chunks of C slots: bounded registers in flight
+    const int u = uu[s];
+    const int nn = unit_nn(u);
+    uint32_t by[12];
+#pragma unroll
+    for (int q = 0; q < (NF == 3 ? 3 : 4); q++) {
+      // in range for every lane: no branch around the read (NF = 4: an empty slot reads persons 0-3, then the phantom)
+      const int pp = unit_first(u) + (NF == 4 ? q : q < nn ? q : 0);
+      by[3 * q + 0] = buf[pp];
+      by[3 * q + 1] = buf[npad + pp];
+      by[3 * q + 2] = buf[2 * npad + pp];
+    }
+    fam_poly4<NF>(by, nn, lk, a[s]);
+  }
+}
 template <int S, int T, int NF = 0>
 __device__ __forceinline__ void hoist_poly4_lds(const DevArgs& A, const int* su, const uint8_t* buf, const double* lk,
                                                 double (*a)[5]) {
@@ -866,21 +889,10 @@ __device__ __forceinline__ void hoist_poly4_lds(const DevArgs& A, const int* su,
   constexpr int C = S < PM_HOIST_CHUNK_LDS ? S : PM_HOIST_CHUNK_LDS;
   int uu[S];
   load_units<S>(su, uu);
-#pragma unroll
-  for (int s = 0; s < S; s++) {
-    if (s % C == 0) __builtin_amdgcn_sched_barrier(0);   // chunks of C slots: bounded registers in flight
-    const int u = uu[s];
-    const int nn = unit_nn(u);
-    uint32_t by[12];
-#pragma unroll
-    for (int q = 0; q < (NF == 3 ? 3 : 4); q++) {
-      const int pp = unit_first(u) + (q < nn ? q : 0);   // in range for every lane: no branch around the read
-      by[3 * q + 0] = buf[pp];
-      by[3 * q + 1] = buf[npad + pp];
-      by[3 * q + 2] = buf[2 * npad + pp];
-    }
-    fam_poly4<NF>(by, nn, lk, a[s]);
-  }
+  if constexpr (NF == 34) {
+    hoist_poly4_lds_rows<4, S, C, 0, S / 2>(uu, buf, npad, lk, a);
+    hoist_poly4_lds_rows<3, S, C, S / 2, S>(uu, buf, npad, lk, a);
+  } else hoist_poly4_lds_rows<NF, S, C, 0, S>(uu, buf, npad, lk, a);
 }
 
 // De novo variant of hoist_poly4 (autosomal --denovo items, families of <= 4 persons): the kid terms are
@@ -1802,22 +1814,30 @@ k_brent(DevArgs A, int list) {
   // waited for at the top of an item.  Issue order per item: ref dword, slot 0, slot 1, next item index.
   __shared__ __attribute__((aligned(16))) int s_qaux[QD ? 128 : 1];
   int q_item = 0;
+  // QD: a wave takes the grp consecutive items of one site (its configurations: one PL block) one after the other,
+  // then the site grp * gridDim.x items further on, so a site's block is re-read while it is still in the XCD's L2
+  // (one wave per item had the site's three reads drift apart over a persistent grid's items; qd_group 1: that order)
+  const int grp = QD ? A.qd_group : 1;
+  auto next_it = [&](int i) {
+    if (grp <= 1) return i + (int)gridDim.x;
+    return (i - A.es_it0) % grp + 1 < grp ? i + 1 : i + 1 + ((int)gridDim.x - 1) * grp;
+  };
+  const int it_first = A.es_it0 + vb * grp;
   if constexpr (QD) {
 #pragma unroll
     for (int i = 0; i < 3; i++) qvoff[i] = quad_voff(i, A.n_person);
-    if (A.es_it0 + vb < itEnd) {
-      q_item = items[A.es_it0 + vb];
+    if (it_first < itEnd) {
+      q_item = items[it_first];
       quad_aux(A.ref + ((q_item >> 3) & ~3), s_qaux);
       quad_prefetch(A, q_item, qvoff, qring);
-      if (A.es_it0 + vb + (int)gridDim.x < itEnd) quad_aux(items + A.es_it0 + vb + gridDim.x, s_qaux + 64);
+      if (next_it(it_first) < itEnd) quad_aux(items + next_it(it_first), s_qaux + 64);
     }
   }
   // QD: an item's results wait in LDS and are stored after the next item's hoisting, so that they are older
   // than that item's prefetch in vmcnt order
   __shared__ double s_pend[QD ? 2 : 1];
   __shared__ int s_pendi[QD ? 3 : 1];
-  const int it_first = A.es_it0 + vb;
-  for (int it = A.es_it0 + vb; it < itEnd; it += gridDim.x) {
+  for (int it = it_first; it < itEnd; it = next_it(it)) {
     if (A.phase) ph_t = wall_clock64();
     const int item = QD ? q_item : items[it];
     const int site = item >> 3, cfg = item & 7;
@@ -1865,7 +1885,7 @@ k_brent(DevArgs A, int list) {
       if constexpr (QD) {
         hoist_quad<S, NC>(A, I, pl, s_lk, s_M, cond, qring, qvoff, lm0, le0);
         hoisted = true;
-        const int itn = it + gridDim.x;   // the next item's first slots land during this item's Brent
+        const int itn = next_it(it);   // the next item's first slots land during this item's Brent
         // (landed: the hoisting ended with vmcnt(0)); uniform, so the next site's addresses are scalar
         const int nitem = __builtin_amdgcn_readfirstlane(((const volatile __attribute__((address_space(3))) int*)s_qaux)[64]);
         // MonomorphismLogLikelihood_denovo (the cfg-0 item, CalcAllFamLogLikelihood at f = 1,
@@ -1894,7 +1914,7 @@ k_brent(DevArgs A, int list) {
           __builtin_amdgcn_sched_barrier(0);
           quad_aux(A.ref + ((nitem >> 3) & ~3), s_qaux);
           quad_prefetch(A, nitem, qvoff, qring);
-          if (itn + (int)gridDim.x < itEnd) quad_aux(items + itn + gridDim.x, s_qaux + 64);
+          if (next_it(itn) < itEnd) quad_aux(items + next_it(itn), s_qaux + 64);
           q_item = nitem;
         }
       }
@@ -2166,7 +2186,9 @@ __device__ __forceinline__ void load_dwords(const uint32_t* p, uint32_t* out) {
 // same-address atomic per site serialised k_prep: 262 144 returning atomics on counts[0] per batch.)  spw is a
 // launch argument (engine.hip: PREP_SPW unless PM_PREP_SPW says otherwise).
 #define PREP_SPW 8
-template <int VEC, bool SERIAL>
+// VC: vcf_mode engines -- no read depth or mapping quality (PedVCF / FamilyLikelihoodSeq_VCF): dm is neither read nor
+// summed, the lanes sum only the hom-ref plane's PL bytes
+template <int VEC, bool SERIAL, bool VC = false>
 __global__ void __launch_bounds__(256) k_prep(DevArgs A, int spw) {
   __shared__ unsigned long long s_c[9];
   __shared__ double s_lk[256];
@@ -2212,21 +2234,25 @@ __global__ void __launch_bounds__(256) k_prep(DevArgs A, int spw) {
       auto chunk = [&](int p0, uint8_t* hr) {
         uint32_t x[VEC];
         if (p0 < np) {   // np % VEC == 0: a lane's VEC persons are all present or all absent
-          if (!A.vcf) load_dwords<VEC>(dm + p0, x);
-          else {   // the VCF path has no read depth or mapping quality (PedVCF / FamilyLikelihoodSeq_VCF): dm is not read
-#pragma unroll
-            for (int k = 0; k < VEC; k++) x[k] = 0;
-          }
+          if constexpr (!VC) load_dwords<VEC>(dm + p0, x);
           load_bytes<VEC>(plane_h + p0, hr);
         } else {
 #pragma unroll
           for (int k = 0; k < VEC; k++) { x[k] = 0; hr[k] = 0; }
         }
+        // a chunk's sums in 32 bits (VEC persons: depths < 2^24 each, mapping qualities and PL bytes < 2^8), widened once
+        uint32_t cp = 0;
 #pragma unroll
-        for (int k = 0; k < VEC; k++) {
-          const int d = (int)(x[k] & 0xFFFFFF);
-          dsum += d; mqsum += (x[k] >> 24); nsd += d > 0;
-          plsum += hr[k];
+        for (int k = 0; k < VEC; k++) cp += hr[k];
+        plsum += cp;
+        if constexpr (!VC) {
+          uint32_t cd = 0, cm = 0, cn = 0;
+#pragma unroll
+          for (int k = 0; k < VEC; k++) {
+            const uint32_t d = x[k] & 0xFFFFFF;
+            cd += d; cm += x[k] >> 24; cn += d > 0;
+          }
+          dsum += cd; mqsum += cm; nsd += cn;
         }
         if constexpr (SERIAL) {   // VEC == 1: lanes in ascending person order
           unsigned long long m = __ballot(hr[0] != 0);   // zero terms add -0.0: no change to a sum starting at +0.0

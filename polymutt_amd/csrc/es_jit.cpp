@@ -562,6 +562,9 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
   std::vector<int> d0(n), dP(n), capP(n);
   std::map<int, int> dM, capM;
   int tmp = 1;
+  // founder-sparse type-3 steps (see sp3): 10 states, one item per call, not switched off (PM_ES_SP3=0)
+  const char* es3 = getenv("PM_ES_SP3");
+  const bool sp3_on = NS == 10 && !(part == 2 && std::max(1, multi) > 1) && !(es3 && es3[0] == '0');
   struct StepDeg { int a, b, c, e; };
   std::vector<StepDeg> sd;
   for (int pass = (part && top) ? 0 : 1; pass < 2; pass++) {   // (pass 0: the 10-state variant's capacities)
@@ -590,7 +593,14 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
       g.a = dP[from0]; g.b = slot == 255 ? 0 : dM[slot]; g.c = dP[from1]; g.e = dP[to0];
       dP[to0] = g.a + g.b + g.c + g.e;
       capP[to0] = std::max(capP[to0], dP[to0] + 1);
-      tmp = std::max(tmp, NS * NS * (g.a + g.b + g.c + 1));
+      // (the W(i, j) products: a founder-sparse step -- sp3 below -- keeps only its supports' pairs; pterms' sizes)
+      auto supp = [&](int f) {
+        if (!(NS == 10 && sp3_on && F.founder[f] && f < F.nf)) return NS;
+        const int sx = F.sex[f];
+        const int dfull = (Y && sx == FEMALE) ? 0 : (((X || Y) && sx == MALE) || MT) ? 1 : 2;
+        return top ? (dfull > 0 ? 1 : 3) : dfull == 1 ? 2 : 3;
+      };
+      tmp = std::max(tmp, supp(from0) * supp(from1) * (g.a + g.b + g.c + 1));
     }
     sd.push_back(g);
   }
@@ -842,6 +852,12 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
     const int t = chrom == PM_CHR_X ? (csex == MALE ? 2 : 1) : chrom == PM_CHR_Y ? (csex == MALE ? 3 : 5) : chrom == PM_CHR_MT ? 4 : 0;
     return "tb[" + S(t * 27) + " + (" + e + ") * 3 + " + k + "]";
   };
+  // founder-sparse type-3 steps (10 states, one item per call): a parent of the roof is a founder
+  std::vector<char> sp3(nst, 0);
+  for (int k = 0; k < nst && sp3_on; k++) {
+    const int f0 = (F.steps[k].x >> 8) & 255, f1 = (F.steps[k].x >> 16) & 255;
+    if ((F.steps[k].x & 255) == 3 && ((F.founder[f0] && f0 < F.nf) || (F.founder[f1] && f1 < F.nf))) sp3[k] = 1;
+  }
   size_t si = 0;
   int fin = -1;
   double nops = 0;
@@ -876,9 +892,14 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
         eff = eff2[kstep] > 0 ? eff2[kstep] : occ(mc ? M * ns : ns, g_wl);   // (a packed run's first step: corrected below)
       } else {
         const int dw = g.a + g.b + g.c;
-        const double o1 = ns * ns * (g.a + 1) * (g.b + 1) * (g.c + 1) * (slot == 255 ? 1 : 2), o2 = ns * (ns * ns * (dw + 1) + (g.e + 1) * (dw + 1));
+        double np_ = ns * ns;   // (founder-sparse: the pairs of the founders' supports only)
+        if (sp3[kstep]) {
+          const int f0 = (St.x >> 8) & 255, f1 = (St.x >> 16) & 255;
+          np_ = (double)((F.founder[f0] && f0 < F.nf) ? (int)pterms(f0).size() : 10) * ((F.founder[f1] && f1 < F.nf) ? (int)pterms(f1).size() : 10);
+        }
+        const double o1 = np_ * (g.a + 1) * (g.b + 1) * (g.c + 1) * (slot == 255 ? 1 : 2), o2 = ns * (np_ * (dw + 1) + (g.e + 1) * (dw + 1));
         nops += o1 + o2;
-        eff = (o1 + o2) / (o1 / occ(ns * ns, g_wl) + o2 / occ(mc ? M * ns : ns, g_wl));
+        eff = (o1 + o2) / (o1 / occ(np_, g_wl) + o2 / occ(mc ? M * ns : ns, g_wl));
       }
       lane_slots += (nops - before) / eff;
       step_ops = nops - before;
@@ -1233,6 +1254,66 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
         code += "  {\n    const int q_ = lane >> 4, i = lane & 15;\n    if (q_ < " + S(run.size()) + " && i < " + nsS + ") {\n" + pre + b +
                 "    }\n  }\n  wave_sync();\n";
       else code += lanes(NS, "i", b) + "  wave_sync();\n";
+    } else if (sp3[kstep]) {
+      // founder-sparse type-3 step (10 states): a founder's partial is prior x penetrance times whatever multiplied into
+      // it -- zero outside the 1-3 states of its prior (the site's g11, g12, g22; pterms) -- so W(e) = P_fa[i] M(e) P_mo[j]
+      // is zero off those pairs, and so is every term T(e, k) W(e) they would add (+0: the sums keep their bits).  Only
+      // the nI x nJ pairs (i, j) in ascending e are formed (lanes over them) and summed (in the same ascending e order),
+      // instead of all 100.  The states of a founder's support are sorted at run time (wave-uniform).
+      regp.erase(to0);
+      const int fa = from0, mo_ = from1, off_ = to0, csex = F.sex[off_];
+      const int dw = g.a + g.b + g.c, ww = dw + 1;
+      auto support = [&](int f, const std::string& pre) -> std::pair<int, std::string> {
+        if (!(F.founder[f] && f < F.nf)) return {10, ""};
+        const auto t = pterms(f);
+        std::string c;
+        for (size_t q = 0; q < t.size(); q++)
+          c += "  int " + pre + S(q) + " = " + (t[q].first == 0 ? "g11" : t[q].first == 1 ? "g12" : "g22") + ";\n";
+        auto sw = [&](int a, int b2) {
+          return "  if (" + pre + S(a) + " > " + pre + S(b2) + ") { const int x_ = " + pre + S(a) + "; " + pre + S(a) + " = " + pre + S(b2) +
+                 "; " + pre + S(b2) + " = x_; }\n";
+        };
+        if (t.size() >= 2) c += sw(0, 1);
+        if (t.size() == 3) c += sw(1, 2) + sw(0, 1);
+        return {(int)t.size(), c};
+      };
+      const std::string pI = "sI" + S(kstep) + "_", pJ = "sJ" + S(kstep) + "_";
+      const auto sI = support(fa, pI), sJ = support(mo_, pJ);
+      const int nI = sI.first, nJ = sJ.first, NP = nI * nJ;
+      auto pick = [&](const std::string& pre, int nn, const std::string& idx) {   // the idx-th state of a support
+        if (nn == 10) return idx;
+        std::string r = pre + S(nn - 1);
+        for (int q = nn - 2; q >= 0; q--) r = "(" + idx + " == " + S(q) + " ? " + pre + S(q) + " : " + r + ")";
+        return r;
+      };
+      code += sI.second + sJ.second;
+      std::string b = "      const int ia = p / " + S(nJ) + ", jb = p - ia * " + S(nJ) + ";\n      const int i = " + pick(pI, nI, "ia") +
+                      ", j = " + pick(pJ, nJ, "jb") + ", e = i * " + nsS + " + j;\n      double w[" + S(ww) + "];\n";
+      for (int a = 0; a <= dw; a++) b += "      w[" + S(a) + "] = 0.0;\n";
+      for (int u = 0; u <= g.a; u++)
+        for (int v = 0; v <= g.b; v++)
+          for (int c = 0; c <= g.c; c++) {
+            const std::string m = slot == 255 ? "" : " * W[" + MOf(slot) + " + e * " + S(capM[slot]) + " + " + S(v) + "]";
+            b += "      w[" + S(u + v + c) + "] = fma(W[" + PO(fa) + " + i * " + S(capP[fa]) + " + " + S(u) + "]" + m + ", W[" +
+                 PO(mo_) + " + j * " + S(capP[mo_]) + " + " + S(c) + "], w[" + S(u + v + c) + "]);\n";
+          }
+      for (int a = 0; a <= dw; a++) b += "      W[" + TBs + " + p * " + S(ww) + " + " + S(a) + "] = w[" + S(a) + "];\n";
+      code += "#pragma unroll\n  for (int r = 0; r < " + S((NP + g_wl - 1) / g_wl) + "; r++) {\n    const int p = lane + " + WL + " * r;\n    if (p < " +
+              S(NP) + ") {\n" + b + "    }\n  }\n  wave_sync();\n";
+      std::string b2 = "    double s[" + S(ww) + "];\n";
+      for (int a = 0; a <= dw; a++) b2 += "    s[" + S(a) + "] = 0.0;\n";
+      b2 += "    for (int p = 0; p < " + S(NP) + "; p++) {\n      const int ia = p / " + S(nJ) + ", jb = p - ia * " + S(nJ) + ";\n      const int e = " +
+            pick(pI, nI, "ia") + " * " + nsS + " + " + pick(pJ, nJ, "jb") + ";\n      const double t = " + tt(csex, "e", "k", slot != 255) + ";\n";
+      for (int a = 0; a <= dw; a++) b2 += "      s[" + S(a) + "] = fma(t, W[" + TBs + " + p * " + S(ww) + " + " + S(a) + "], s[" + S(a) + "]);\n";
+      b2 += "    }\n    double t[" + S(g.e + 1) + "];\n";
+      for (int c = 0; c <= g.e; c++) b2 += "    t[" + S(c) + "] = W[" + PO(off_) + " + k * " + S(capP[off_]) + " + " + S(c) + "];\n";
+      for (int a = 0; a <= g.e + dw; a++) {
+        std::string acc;
+        for (int c = std::max(0, a - dw); c <= std::min(a, g.e); c++)
+          acc = acc.empty() ? "t[" + S(c) + "] * s[" + S(a - c) + "]" : "fma(t[" + S(c) + "], s[" + S(a - c) + "], " + acc + ")";
+        b2 += "    W[" + PO(off_) + " + k * " + S(capP[off_]) + " + " + S(a) + "] = " + acc + ";\n";
+      }
+      code += lanes(NS, "k", b2) + "  wave_sync();\n";
     } else {   // W(e) = P_fa[i] M(e) P_mo[j] -> LDS; lanes over k: S(k) = sum_e T(e, k) W(e), P_off[k] *= S(k) in place
       regp.erase(to0);
       const int fa = from0, mo_ = from1, off_ = to0, csex = F.sex[off_];
@@ -1783,33 +1864,45 @@ std::string generate_fused(int chrom, const std::vector<Family>& fams, const dou
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
     return sdeg[sig[a]] != sdeg[sig[b]] ? sdeg[sig[a]] > sdeg[sig[b]] : sig[a] < sig[b];
   });
+  // Two layouts: one item per wave (rows of up to 64 cells), or two (pair: each half-wave, 32 lanes, runs its own item
+  // on rows of up to 32 cells -- the evaluation's fixed part (division, power, reduction, log10, Brent's update) is then
+  // shared by two items, at the price of twice the rows and of the longer of the two Brent runs).  Per-item cost model:
+  // hoisting + kEvals x (2 (D_row + 1) per row + the fixed part), the pair layout's halved.
   const int kRowsMax = 8, kTile = 64, kEvals = 30;
+  const double kFixed1 = 150, kFixed2 = 230, kImb = 1.1;
+  const char* epair = getenv("PM_FUSED_PAIR");   // (0 / 1: force one layout)
   double best = -1;
   int best_nl = 0;
-  for (int nl = (n + kRowsMax - 1) / kRowsMax; nl <= 64; nl++) {
-    if (nl <= 0) continue;
-    const int rows = (n + nl - 1) / nl;
-    double cost = 0;
-    int tile = 0;
-    std::vector<int> lane_deg(nl, 0);
-    for (int r = 0; r < rows; r++) {
-      std::vector<char> seen(ns, 0);
-      int dmax = 0;
-      for (int k = r * nl; k < std::min(n, (r + 1) * nl); k++) {
-        const int sg = sig[order[k]];
-        if (!seen[sg]) { seen[sg] = 1; cost += sops[sg]; }
-        dmax = std::max(dmax, sdeg[sg]);
-        lane_deg[k - r * nl] += sdeg[sg];
+  bool pair = false;
+  for (int pm = 0; pm < 2; pm++) {
+    if (epair && atoi(epair) != pm) continue;
+    const int lmax = pm ? 32 : 64;
+    for (int nl = (n + kRowsMax - 1) / kRowsMax; nl <= lmax; nl++) {
+      if (nl <= 0) continue;
+      const int rows = (n + nl - 1) / nl;
+      double hoist = 0, eval = pm ? kFixed2 : kFixed1;
+      int tile = 0;
+      std::vector<int> lane_deg(nl, 0);
+      for (int r = 0; r < rows; r++) {
+        std::vector<char> seen(ns, 0);
+        int dmax = 0;
+        for (int k = r * nl; k < std::min(n, (r + 1) * nl); k++) {
+          const int sg = sig[order[k]];
+          if (!seen[sg]) { seen[sg] = 1; hoist += sops[sg]; }
+          dmax = std::max(dmax, sdeg[sg]);
+          lane_deg[k - r * nl] += sdeg[sg];
+        }
+        tile += dmax + 1;
+        eval += 2.0 * (dmax + 1);
       }
-      tile += dmax + 1;
-      cost += kEvals * 2.0 * (dmax + 1);
+      if (tile > kTile || *std::max_element(lane_deg.begin(), lane_deg.end()) > 64) continue;
+      const double cost = pm ? (hoist + kImb * kEvals * eval) / 2 : hoist + kEvals * eval;
+      if (best < 0 || cost < best) { best = cost; best_nl = nl; pair = pm; }
     }
-    if (tile > kTile || *std::max_element(lane_deg.begin(), lane_deg.end()) > 64) continue;
-    if (best < 0 || cost < best) { best = cost; best_nl = nl; }
   }
   if (best_nl == 0) return "";
   const int nl = best_nl, rows = (n + nl - 1) / nl;
-  out->lanes = nl; out->rows = rows; out->n_shapes = ns;
+  out->lanes = nl; out->rows = rows; out->n_shapes = ns; out->pair = pair;
   out->lane_tab.assign((size_t)rows * 64 + 64, -1);
   for (int l = 0; l < 64; l++) out->lane_tab[(size_t)rows * 64 + l] = 0;
   std::vector<std::vector<int>> row_shapes(rows);
@@ -1825,9 +1918,12 @@ std::string generate_fused(int chrom, const std::vector<Family>& fams, const dou
     }
     out->row_deg.push_back(dmax);
   }
+  if (pair)   // (both halves hoist the same families for their own items)
+    for (int r = 0; r <= rows; r++)
+      for (int l = 32; l < 64; l++) out->lane_tab[(size_t)r * 64 + l] = out->lane_tab[(size_t)r * 64 + l - 32];
   for (int i = 0; i < n; i++) out->item_ops += sops[sig[i]];
   if (getenv("PM_JIT_LAYOUT")) {
-    fprintf(stderr, "ep_brent_jit: %d families, %d shapes, %d rows x %d lanes, tiles", n, ns, rows, nl);
+    fprintf(stderr, "ep_brent_jit: %d families, %d shapes, %d rows x %d lanes%s, tiles", n, ns, rows, nl, pair ? " (two items per wave)" : "");
     for (int r = 0; r < rows; r++) fprintf(stderr, " %d(%zu)", out->row_deg[r], row_shapes[r].size());
     fprintf(stderr, ", cost %.0f\n", best);
   }
@@ -1858,9 +1954,21 @@ struct FusedArgs {
   src += "  int ltab[" + std::to_string(rows) + "];\n";
   src += "#pragma unroll\n  for (int r = 0; r < " + std::to_string(rows) + "; r++) ltab[r] = A.lane_tab[r * 64 + lane];\n";
   src += "  const int edl = A.lane_tab[" + std::to_string(rows * 64) + " + lane];   // g^edl: the lane's degrees summed\n";
-  src += R"(  unsigned long long ev_acc = 0;
+  if (!pair)
+    src += R"(  unsigned long long ev_acc = 0;
   for (int it = A.it0 + vb; it < nItems; it += gridDim.x) {
     const int item = A.items[it];
+)";
+  else   // half-wave h takes item it0 + 2 t + h (a missing second item: the first one's data, nothing written)
+    src += R"(  unsigned long long ev_acc = 0;
+  const int half = lane >> 5;
+  for (int t2 = vb; A.it0 + 2 * t2 < nItems; t2 += gridDim.x) {
+    const int it = A.it0 + 2 * t2 + half;
+    const bool valid = it < nItems;
+    const int item = A.items[valid ? it : it - 1];
+)";
+  src += R"(
+
     const int site = item >> 3, cfg = item & 7, rb = A.ref[site];
     int a1, a2;
     if (A.vcf) { a1 = rb & 15; a2 = rb >> 4; }
@@ -1890,20 +1998,37 @@ struct FusedArgs {
   }
   src += R"(    PmBrent B;
     pm_brent_init(B, A.precision, A.itmax);
-    for (;;) {
+)";
+  if (pair) src += "    bool done = !valid;\n";
+  src += R"(    for (;;) {
       // every family L = g^D sum_a c_a t^a, t = f / g (non-negative terms: no cancellation), FMA Horner over the row's
       // tile (zeros above a family's own degree leave the sum's bits unchanged); the values split into mantissa and
       // exponent, multiplied in one chain with g^edl, one renormalisation -- as k_brent's EP evaluation
       const double g = 1.0 - B.x;
       const double t = pos_div(B.x, g);
-      double gp = g, pw = 1.0;
-#pragma unroll
-      for (int b = 0; b < 7; b++) {
-        pw = ((edl >> b) & 1) ? pw * gp : pw;
-        gp = gp * gp;
-      }
-      int e = 0;
 )";
+  {   // g^edl: the layout's distinct lane degree sums are known here -- shared squarings, one power per value, a select
+    std::vector<int> vals;
+    for (int l = 0; l < 64; l++) {
+      const int v = out->lane_tab[(size_t)rows * 64 + l];
+      if (v > 0 && std::find(vals.begin(), vals.end(), v) == vals.end()) vals.push_back(v);
+    }
+    std::sort(vals.begin(), vals.end());
+    int top = 0;
+    for (int v : vals) top = std::max(top, v);
+    int nb = 0;
+    while ((1 << (nb + 1)) <= top) nb++;   // the highest bit of any value
+    src += "      double q0 = g;\n";
+    for (int b = 1; b <= nb; b++) src += "      const double q" + std::to_string(b) + " = q" + std::to_string(b - 1) + " * q" + std::to_string(b - 1) + ";\n";
+    src += "      double pw = 1.0;\n";
+    for (size_t k = 0; k < vals.size(); k++) {
+      std::string prod;
+      for (int b = 0; b <= nb; b++)   // (ascending bits: the order of the former square-and-multiply loop)
+        if ((vals[k] >> b) & 1) prod = prod.empty() ? "q" + std::to_string(b) : "(" + prod + ") * q" + std::to_string(b);
+      src += "      if (edl == " + std::to_string(vals[k]) + ") pw = " + prod + ";\n";
+    }
+  }
+  src += "      int e = 0;\n";
   for (int r = 0; r < rows; r++) {
     const int D = out->row_deg[r];
     const std::string c = "c" + std::to_string(r), R = std::to_string(r);
@@ -1917,18 +2042,29 @@ struct FusedArgs {
       int e2;
       m = frexp(m * pw, &e2);
       e += e2;
-      wave_prod(m, e);
+)";
+  if (!pair)
+    src += R"(      wave_prod(m, e);
       if (!pm_brent_feed(B, -log10_mant_u(m, e))) break;
     }
     if (lane == 0) {
-      A.raw[(size_t)site * 8 + cfg] = -B.fmin;
+)";
+  else   // (a half whose Brent has ended keeps its state; the wave goes on until both have)
+    src += R"(      wave_prod_pair(m, e);
+      const double fx = -log10_mant_pair(m, e);
+      if (!done && !pm_brent_feed(B, fx)) done = true;
+      if (__ballot(!done) == 0) break;
+    }
+    if ((lane & 31) == 0 && valid) {
+)";
+  src += R"(      A.raw[(size_t)site * 8 + cfg] = -B.fmin;
       A.minv[(size_t)site * 8 + cfg] = B.mn;
       A.evals[(size_t)site * 8 + cfg] = B.nev;
       ev_acc += B.nev - 2;   // objective evaluations computed (f(a), f(c) counted only)
       if (!B.ok) { atomicExch(&A.counts[5], 1); atomicMin(&A.counts[6], site); }   // (the reference stops at the first)
     }
   }
-  if (lane == 0 && ev_acc) atomicAdd(A.eval_total, ev_acc);
+  if ((lane & 31) == 0 && ev_acc) atomicAdd(A.eval_total, ev_acc);
 }
 )";
   return src;

@@ -103,6 +103,7 @@ struct FusedKernel {
   std::vector<int> lane_tab;   // rows * 64 + 64 ints (FusedArgs::lane_tab)
   std::vector<int> row_deg;    // each row's register tile degree
   int rows = 0, lanes = 0, n_shapes = 0, blocks_per_cu = 0;
+  bool pair = false;           // two Brent items per wave, one per half-wave (rows of <= 32 cells)
   double item_ops = 0;         // FP64 operations of one item's hoisting over every family (the generated peels)
   double compile_ms = 0;
 };

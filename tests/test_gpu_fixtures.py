@@ -104,3 +104,32 @@ def test_es_hoisting_kernels_agree(built, tmp_path, monkeypatch, name):
     if (out["jit"]["af"] == out["generic"]["af"]).all():
         for a, b in zip(rows["jit"], rows["generic"]):
             assert a.shape == b.shape and (a == b).all()
+
+
+_SP3_CASES = [n for n in DUMP_CASES if n.startswith(("roof", "roof2", "extmix", "big_extmix")) and "denovo" in n]
+
+
+@pytest.mark.parametrize("name", _SP3_CASES)
+def test_es_type3_founder_sparsity_is_bit_exact(built, tmp_path, monkeypatch, name):
+    """--denovo 10-state peels: the schedule compiler's founder-sparse type-3 steps (a roof parent that is a founder has
+    only its prior's 1-3 states; the pairs outside them add +0) give the same results bit for bit as the dense steps
+    (PM_ES_SP3=0), and both match the reference dump."""
+    import numpy as np
+    case = make_dataset(name, str(tmp_path))
+    ped, secs, _ = read_dataset(str(tmp_path))
+    par, chrom = params_and_chrom(case["flags"], numerics=pm.NUM_POLY)
+    (label, pos, ref, pl, dm), = secs
+    out = {}
+    for mode in ("sparse", "dense"):
+        if mode == "dense":
+            monkeypatch.setenv("PM_ES_SP3", "0")
+        eng = pm.Engine(ped.view, par, max_batch=256)
+        eng.begin_section(chrom)
+        runs = [eng.run(pl[s:s + 256], dm[s:s + 256], ref[s:s + 256]) for s in range(0, len(ref), 256)]
+        eng.close()
+        out[mode] = (np.concatenate([r[0] for r in runs]), [r[1] for r in runs])
+        compare_to_dump(out[mode][0], golden_dump(name), label=f"{name} {mode} ")
+    a, b = out["sparse"][0], out["dense"][0]
+    assert a.tobytes() == b.tobytes()
+    for x, y in zip(out["sparse"][1], out["dense"][1]):
+        assert x.tobytes() == y.tobytes()
