@@ -1000,8 +1000,9 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
       E->max_nuc <= 4 && (al16 || al4) && E->n_person >= 16 && (E->n_person + 1023) / 1024 * 1024 * 3 <= 60 * 1024 &&
       !getenv("PM_NO_PREFETCH")) {
     A.pf_npad = (E->n_person + 1023) / 1024 * 1024;
+    A.pf_stride = A.pf_npad + 16;
     A.pf_dw = al16 ? 0 : 1;
-    shmem = (size_t)3 * A.pf_npad;
+    shmem = (size_t)3 * A.pf_stride;
   }
   // lean --denovo kernel: QUAD plans load each family's PL dwords directly (hoist_quad); other plans stage the PL
   // windows through LDS by LDS-DMA (double buffer per wave)

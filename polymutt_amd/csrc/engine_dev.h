@@ -139,7 +139,9 @@ struct DevArgs {
   int mono_dn;             // lean --denovo: the de novo monomorphism item (cfg 0) is not enqueued; 1 = k_prep computes it,
                            // 2 = the site's cfg-1 QUAD item does (from its hoisted f^4 coefficients, no extra plane reads)
   int* row_blk;            // k_rows_count / k_rows: written records per 1024-site block
-  int pf_npad;             // lean kernel: > 0 = the item's 3 genotype planes are prefetched into LDS (stride)
+  int pf_npad;             // lean kernel: > 0 = the item's 3 genotype planes are prefetched into LDS (bytes copied per plane)
+  int pf_stride;           // ... at this stride (pf_npad + 16: each plane's last 16 bytes are never written -- zeros: the
+                           // persons of the virtual all-PL-0 family that fills a split plan's empty slots)
   int pf_dw;               // ... in 4-byte pieces (n_person % 16 != 0, n_person % 4 == 0)
   int dn_pf;               // lean --denovo kernel: PL windows staged through LDS by LDS-DMA (hoist_poly4_dn_pf)
   int quad_full;           // QUAD plan (hoist_quad): slot rows below this have no empty lane
@@ -729,8 +731,19 @@ __device__ __forceinline__ void load_units(const int* su, int* uu) {
 #define PM_FAM_FACTORED 1
 #endif
 __device__ __forceinline__ void quad_poly4(const double (*D)[3], const double* lF, const double* lM, double* a);
-template <int NF = 0>
+template <int NF = 0, bool VIRT = false>
 __device__ __forceinline__ void fam_poly4(const uint32_t* by, int nn, const double* lk, double* a) {
+  if constexpr (PM_FAM_FACTORED && VIRT) {   // every slot a real family or the virtual one (hoist_poly4_lds_rows)
+    double D[2][3];
+#pragma unroll
+    for (int q = 0; q < 2; q++)
+#pragma unroll
+      for (int k = 0; k < 3; k++) D[q][k] = (NF == 3 && q == 1) ? 1.0 : lk[by[3 * (2 + q) + k]];
+    const double lF[3] = {lk[by[0]], lk[by[1]], lk[by[2]]};
+    const double lM[3] = {lk[by[3]], lk[by[4]], lk[by[5]]};
+    quad_poly4(D, lF, lM, a);
+    return;
+  }
   if constexpr (PM_FAM_FACTORED) {
     // kid q's (l11, l12, l22); a missing kid is (1, 1, 1): its likelihoodONEKid terms are then exactly 1 (the factors
     // 2 and 4 of quad_poly4's sums are undone by its exact 0.5 / 0.25 scalings)
@@ -830,7 +843,7 @@ __device__ __forceinline__ void prefetch_planes(const DevArgs& A, const int* ite
   const int site = item >> 3, cfg = item & 7;
   int a1, a2;
   item_alleles(A, site, cfg, A.ref[site], &a1, &a2);
-  const int np = A.n_person, npad = A.pf_npad;
+  const int np = A.n_person, npad = A.pf_npad, stride = A.pf_stride;
   const int gs[3] = {d_gi(a1, a1), d_gi(a1, a2), d_gi(a2, a2)};
   const uint8_t* base = A.pl + (size_t)site * np * 10;
   const int lane = threadIdx.x & 63;
@@ -841,7 +854,7 @@ __device__ __forceinline__ void prefetch_planes(const DevArgs& A, const int* ite
       const uint8_t* plane = base + (size_t)gs[k] * np;
       for (int c = wv * 256; c < np; c += W * 256) {
         const int off = min(c + lane * 4, np - 4);
-        __builtin_amdgcn_global_load_lds((const void*)(plane + off), (void*)(buf + k * npad + c), 4, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(plane + off), (void*)(buf + k * stride + c), 4, 0, 0);
       }
     }
     return;
@@ -851,7 +864,7 @@ __device__ __forceinline__ void prefetch_planes(const DevArgs& A, const int* ite
     const uint8_t* plane = base + (size_t)gs[k] * np;
     for (int c = wv * 1024; c < npad; c += W * 1024) {
       const int off = min(c + lane * 16, np - 16);
-      __builtin_amdgcn_global_load_lds((const void*)(plane + off), (void*)(buf + k * npad + c), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(plane + off), (void*)(buf + k * stride + c), 16, 0, 0);
     }
   }
 }
@@ -863,7 +876,9 @@ __device__ __forceinline__ void prefetch_planes(const DevArgs& A, const int* ite
 // NF = 34: a split plan (plan_split34): slot rows [0, S/2) hold quads (or nothing), rows [S/2, S) trios (or nothing), so
 // each half is hoisted with its family size known -- the quads without the missing-kid selects, the trios without the
 // second kid -- mixed trio / quad pedigrees (config 5's) get the trio plans' saving on half their slots
-template <int NF, int S, int C, int S0, int S1>
+// (VIRT: the split plan's empty slots hold the virtual family -- persons at the planes' zero tail, every likelihood
+// lk[0] = 1.0 -- whose quartic is exactly the phantom (1, 4, 6, 4, 1): no empty-slot selects at all)
+template <int NF, int S, int C, int S0, int S1, bool VIRT = false>
 __device__ __forceinline__ void hoist_poly4_lds_rows(const int* uu, const uint8_t* buf, int npad, const double* lk, double (*a)[5]) {
 #pragma unroll
   for (int s = S0; s < S1; s++) {
@@ -879,19 +894,19 @@ __device__ __forceinline__ void hoist_poly4_lds_rows(const int* uu, const uint8_
       by[3 * q + 1] = buf[npad + pp];
       by[3 * q + 2] = buf[2 * npad + pp];
     }
-    fam_poly4<NF>(by, nn, lk, a[s]);
+    fam_poly4<NF, VIRT>(by, nn, lk, a[s]);
   }
 }
 template <int S, int T, int NF = 0>
 __device__ __forceinline__ void hoist_poly4_lds(const DevArgs& A, const int* su, const uint8_t* buf, const double* lk,
                                                 double (*a)[5]) {
-  const int npad = A.pf_npad;
+  const int npad = A.pf_stride;   // (the planes' stride in the buffer)
   constexpr int C = S < PM_HOIST_CHUNK_LDS ? S : PM_HOIST_CHUNK_LDS;
   int uu[S];
   load_units<S>(su, uu);
   if constexpr (NF == 34) {
-    hoist_poly4_lds_rows<4, S, C, 0, S / 2>(uu, buf, npad, lk, a);
-    hoist_poly4_lds_rows<3, S, C, S / 2, S>(uu, buf, npad, lk, a);
+    hoist_poly4_lds_rows<4, S, C, 0, S / 2, true>(uu, buf, npad, lk, a);
+    hoist_poly4_lds_rows<3, S, C, S / 2, S, true>(uu, buf, npad, lk, a);
   } else hoist_poly4_lds_rows<NF, S, C, 0, S>(uu, buf, npad, lk, a);
 }
 
@@ -1781,7 +1796,15 @@ k_brent(DevArgs A, int list) {
     for (int i = threadIdx.x; i < 100; i += T) s_M[i] = A.M[i];
   if constexpr (POLYK && !QD)   // (QUAD plans address families by slot and lane: no lane plan)
 #pragma unroll
-    for (int s = 0; s < S; s++) s_u[threadIdx.x * S + s] = unit_pack(A.units[s * T + threadIdx.x]);
+    for (int s = 0; s < S; s++) {
+      const int4 u = A.units[s * T + threadIdx.x];
+      // (NF = 34: an empty slot holds the virtual family at the planes' zero tail, pf_npad, of its half's size)
+      s_u[threadIdx.x * S + s] = (NF == 34 && u.x != U_NUC) ? (A.pf_npad | ((s < S / 2 ? 4 : 3) << 24)) : unit_pack(u);
+    }
+  if constexpr (PF && NF == 34) {   // the virtual persons' bytes: each plane's never-written tail
+    extern __shared__ uint8_t s_pf0[];
+    if (A.pf_npad > 0 && threadIdx.x < 48) s_pf0[(threadIdx.x >> 4) * A.pf_stride + A.pf_npad + (threadIdx.x & 15)] = 0;
+  }
   __syncthreads();
   int4 unit[S];
   if constexpr (!POLYK) {
@@ -2570,11 +2593,14 @@ __device__ __forceinline__ int8_t d_vcf_label(int chrom, int membersex) {
 // log10 guess g is within 1 of that count (its error is < 1e-4 on -10 log10 q <= 100): the count is g - 1 plus the
 // two tests q < thr[g - 1], q < thr[g] (adjacent thresholds: one ds_read2, no loop, no branch), the window clamped
 // to [0, 100).  Identical to the reference's glibc result for every double pb.
+// The guess is the bare v_log_f32 (log2, ~1 ulp) times -10 log10(2): error < 1e-5 on the range that matters; a float
+// q below the normal range (where the bare instruction may read 0: +inf guess) has pb > 0.9999999999, GQ 100 anyway,
+// so none of the library log10's denormal scaling and extended-precision product is needed (8 VALU instead of 16).
 static __constant__ double c_gq_thr[101];   // (uploaded by engine.hip, the only unit whose kernels read it)
 // (thr: the block's LDS copy of c_gq_thr -- the lookups' index diverges, so they are not scalar loads)
 __device__ __forceinline__ int d_gq(double pb, const double* thr) {
   const double q = 1. - pb;
-  const int g = (int)(-10.0f * __log10f((float)q) + 0.5f);   // (q = 0: +inf saturates; the select below wins)
+  const int g = (int)(-3.01029995664f * __builtin_amdgcn_logf((float)q) + 0.5f);   // (q = 0: +inf saturates; the select below wins)
   const int base = min(max(g - 1, 0), 98);
   const int k = base + (q < thr[base] ? 1 : 0) + (q < thr[base + 1] ? 1 : 0);
   return pb > 0.9999999999 ? 100 : k;

@@ -446,7 +446,7 @@ struct VcfCall { signed char best; signed char gq; signed char label; signed cha
 // d_gq (engine.hip): GQ of OutputVCF :1818-1820 from the host's glibc thresholds, exact for every double
 __device__ __forceinline__ int gq_of(double pb, const double* thr) {
   const double q = 1. - pb;
-  const int g = (int)(-10.0f * log10f((float)q) + 0.5f);
+  const int g = (int)(-3.01029995664f * __builtin_amdgcn_logf((float)q) + 0.5f);   // (bare v_log_f32: see d_gq)
   const int base = min(max(g - 2, 0), 96);
   int k = base;
   for (int i = 0; i < 4; i++) k += q < thr[base + i] ? 1 : 0;
