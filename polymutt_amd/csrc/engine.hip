@@ -101,6 +101,7 @@ struct pm_engine {
   int4* d_units_q = nullptr;
   int* d_items[N_LISTS] = {nullptr, nullptr, nullptr};
   int* d_counts = nullptr;
+  int* d_qctr = nullptr;     // QUAD dynamic item order: 8 per-XCD claim counters (k_brent DevArgs::qd_ctr)
   unsigned long long* d_eval_total = nullptr;
   unsigned long long* d_phase = nullptr;   // PM_PHASE_TIMING set at engine creation: k_brent hoisting / evaluation wave time
   int wall_khz = 100000;                   // wall_clock64() rate (hipDeviceAttributeWallClockRate)
@@ -313,7 +314,7 @@ void pm_engine_destroy(pm_engine* E) {
                   E->d_fam_start, E->d_fam_kind, E->d_fa, E->d_mo, E->d_sex, E->d_units, E->d_lktab, E->d_M, E->d_syn,
                   E->d_pl, E->d_stage, E->d_ref, E->d_dm, E->d_res, E->d_calls, E->d_raw, E->d_minv, E->d_mono, E->d_evals,
                   E->d_items[0], E->d_items[1], E->d_items[2], E->d_counts, E->d_eval_total, E->d_row_site,
-                  E->d_counters, E->d_row_blk};
+                  E->d_counters, E->d_row_blk, E->d_qctr};
   for (void* b : bufs) if (b) hipFree(b);
   for (auto& pl : E->d_jit_slots)
     for (int* b : pl) if (b) hipFree(b);
@@ -724,6 +725,7 @@ int pm_engine_create(const pm_pedigree* ped, const pm_params* par, int device, i
   DALLOC(E->d_mono, nb);
   for (int l = 0; l < N_LISTS; l++) DALLOC(E->d_items[l], nb * 4);
   DALLOC(E->d_counts, 16);
+  DALLOC(E->d_qctr, 8);
   DALLOC(E->d_eval_total, 1);
   DALLOC(E->d_row_site, nb);
   DALLOC(E->d_row_blk, nb / 1024 + 2);
@@ -832,6 +834,7 @@ static DevArgs make_args(pm_engine* E, int n, const uint8_t* pl, const uint32_t*
   A.counts = E->d_counts; A.eval_total = E->d_eval_total; A.phase = E->d_phase; A.row_site = E->d_row_site; A.row_blk = E->d_row_blk; A.counters = E->d_counters;
   A.carry_postprob = E->carry_postprob ? 1 : 0;
   A.itmax = E->itmax;
+  A.qd_ctr = nullptr;
   // (the QUAD plan's cfg-1 items form it from their hoisting: launch_brent takes the QUAD kernel for list 0 exactly when
   // E->quad and the plan is 64 x 8 / 64 x 16, and mono_dn_in_prep already implies the lean --denovo kernel)
   A.mono_dn = !mono_dn_in_prep(E) ? 0 : (E->quad && E->T == 64 && (E->S == 8 || E->S == 16) && !getenv("PM_MONO_DN_PREP")) ? 2 : 1;
@@ -1033,7 +1036,21 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
       bpc = n;
       if (getenv("PM_QD_BPC")) bpc = std::max(1, atoi(getenv("PM_QD_BPC")));
     }
-    grid = E->n_cu * bpc;
+    // PM_QD_ROUNDS = R rounds of the resident blocks (default 1): a block then takes 1 / R of the items it takes in a
+    // persistent grid, so the three items of a site -- started together on neighbouring blocks of one XCD -- drift
+    // apart by fewer items and find the site's planes still in that XCD's L2: FETCH per dispatch 4.81 GB at R = 1, 4.24
+    // at 2, 4.00 at 4, 3.96 at 8 (3.85 algorithmic), k_brent 3.19 -> 2.98 ms on one engine (profiles/r06l_*); but the
+    // default three engines then interleave their launches' blocks on every XCD and the bench's wall rate drops 1.5%
+    // (r06n_*), so R = 1 stays.  PM_QD_DYN=1: the per-XCD claimed item order (k_brent qd_ctr; slower, r06o_*).
+    const char* ed = getenv("PM_QD_DYN");
+    const bool dyn = ed && atoi(ed) != 0 && A.qd_group == 1;
+    if (dyn) {
+      HIP_TRY(hipMemsetAsync(E->d_qctr, 0, 8 * sizeof(int), E->stream));
+      A.qd_ctr = E->d_qctr;
+    }
+    const char* er = getenv("PM_QD_ROUNDS");
+    const int rounds = getenv("PM_QD_BPC") ? 1 : er ? std::max(1, atoi(er)) : 1;
+    grid = E->n_cu * bpc * rounds;
     grid = xcd_grid(grid);   // (the XCD-aware item order)
   }
   if (!quad && !gen && !unrelated && n_ext == 0 && A.denovo && E->par.numerics == PM_NUM_POLY && E->max_nuc <= 4 && S % DN_PF_C == 0 &&
@@ -1091,6 +1108,15 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
     grid = std::min(grid, E->n_cu * bpc);
     grid = xcd_grid(grid);
   }
+  // lean PF kernels: PM_PF_ROUNDS x the default grid (2 rounds of the resident blocks).  One-wave quad plans take 4 (8
+  // rounds): less drift between the items of a site, so its planes are re-read from L2 (plain quads 27.7 -> 28.7 M
+  // sites/s, k_brent frac 0.725 -> 0.76, profiles/r06m_*).  Trio plans lost 2% of wall rate with it (frac 0.70 -> 0.72:
+  // the engines' launches interleave, r06p_*) and the two-wave 128 x 16 plans (config 5) gained nothing: 1
+  if (A.pf_npad > 0 && !ep) {
+    const char* epr = getenv("PM_PF_ROUNDS");
+    const int r = epr ? std::max(1, atoi(epr)) : (T == 64 && !E->all_trio) ? 4 : 1;
+    grid = xcd_grid(grid * r);
+  }
   // HIP events around every Brent launch (and, for EP, every hoisting launch: pm_kernel_stats reports the two apart)
   auto mark = [&](std::vector<std::pair<hipEvent_t, hipEvent_t>>& v, bool begin) -> int {
     if (begin) {
@@ -1120,7 +1146,10 @@ static int launch_brent(pm_engine* E, const DevArgs& A0, int list, bool unrelate
     F.itmax = A.itmax; F.pad = 0;
     void* params[] = {&F};
     if ((mrc = mark(E->brent_events, true))) return mrc;
-    HIP_TRY(hipModuleLaunchKernel(FK->fn, xcd_grid(E->n_cu * FK->blocks_per_cu), 1, 1, 64, 1, 1, 0, E->stream, params, nullptr));
+    const char* efr = getenv("PM_FUSED_ROUNDS");   // (rounds of the resident blocks: measured)
+    const int frounds = efr ? std::max(1, atoi(efr)) : 1;
+    HIP_TRY(hipModuleLaunchKernel(FK->fn, xcd_grid(E->n_cu * FK->blocks_per_cu * frounds), 1, 1, 64, 1, 1, 0, E->stream, params,
+                                  nullptr));
     if ((mrc = mark(E->brent_events, false))) return mrc;
   } else if (ep) {   // chunks of the list (the coefficient buffer holds es_chunk items): k_es_hoist, then the chunk's Brent items
     void (*hoist)(DevArgs, int) = A.denovo ? k_es_hoist<true> : k_es_hoist<false>;

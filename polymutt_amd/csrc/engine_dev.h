@@ -173,6 +173,7 @@ struct DevArgs {
                            // (atomicMin), [8]/[9] quick items/site visits
   int qd_group;            // QUAD kernel: items per site group of the list (a wave takes a site's items in turn)
   int itmax;               // Brent's ITMAX (MathGold.cpp:98: 200; PM_TEST_ITMAX lowers it for the failure-path tests)
+  int* qd_ctr;             // QUAD kernel: the 8 per-XCD claim counters of the dynamic item order (zeroed per launch), or null
   unsigned long long* eval_total;
   unsigned long long* phase;   // PM_PHASE_TIMING: [0] hoisting, [1] evaluations, [2] items -- k_brent wave time (wall_clock64 ticks)
   int* row_site;           // [n] emitted row -> site
@@ -1845,22 +1846,69 @@ k_brent(DevArgs A, int list) {
     if (grp <= 1) return i + (int)gridDim.x;
     return (i - A.es_it0) % grp + 1 < grp ? i + 1 : i + 1 + ((int)gridDim.x - 1) * grp;
   };
-  const int it_first = A.es_it0 + vb * grp;
+  // QD dynamic order (A.qd_ctr): the list is cut into 8 contiguous ranges, one per XCD, and the waves of XCD x
+  // (block % 8, the dispatch order the static map assumes as well) claim positions from range x's counter, one per
+  // item, then from the other ranges once theirs is drained.  The items in flight on an XCD are then always a
+  // window of consecutive positions, where the static stride lets blocks drift apart by many items over a persistent
+  // grid (FETCH 1.25x algorithmic).  Measured slower (opt-in, PM_QD_DYN=1): a site's three items then start up to an
+  // item apart on three waves, and the traffic rose to 1.50x (profiles/r06o_*).  A claim is issued one item before it is resolved (its return lands under that item's Brent, and
+  // an extra vector-memory operation only makes the kernel's vmcnt waits stricter), so no wait is added; the
+  // blocking claims are the steals at the end.  (Grids of whole XCD rounds only: the static positions need it.)
+  const bool qdyn = QD && A.qd_ctr != nullptr && gridDim.x % 8 == 0;
+  const int q_len = (itEnd - A.es_it0 + 7) / 8;
+  int q_x = blockIdx.x & 7, q_tries = 0, q_pend = 0;
+  bool q_pend_ok = false;
+  auto q_issue = [&]() {   // a speculative claim on range q_x (lane 0's VGPR)
+    int v = 0;
+    if (threadIdx.x == 0) v = atomicAdd(A.qd_ctr + q_x, 1);
+    return v;
+  };
+  // (a block's first two items are static -- range positions b / 8 and nb + b / 8, nb = blocks per XCD -- so the
+  // claims count from 2 nb in the home range; a steal from another range counts from 2 nb as well, its static
+  // positions belonging to that range's own blocks)
+  const int q_nb = (int)gridDim.x / 8;
+  auto q_resolve = [&](int v) {   // the claimed list position, or -1 once every range is drained
+    int p = A.es_it0 + q_x * q_len + 2 * q_nb + __builtin_amdgcn_readfirstlane(v);
+    while (p >= min(A.es_it0 + (q_x + 1) * q_len, itEnd)) {
+      if (++q_tries >= 8) return -1;
+      q_x = (q_x + 1) & 7;
+      p = A.es_it0 + q_x * q_len + 2 * q_nb + __builtin_amdgcn_readfirstlane(q_issue());
+    }
+    return p;
+  };
+  auto q_next_pos = [&]() {   // resolve the pending claim, issue the next one
+    const int p = q_pend_ok ? q_resolve(q_pend) : -1;
+    q_pend_ok = p >= 0 && q_tries < 8;
+    if (q_pend_ok) q_pend = q_issue();
+    return p;
+  };
+  int it_first = A.es_it0 + vb * grp;
+  int q_pos1 = -1, q_next = -1;   // QD: the list positions of the next item and of the one after the current
   if constexpr (QD) {
 #pragma unroll
     for (int i = 0; i < 3; i++) qvoff[i] = quad_voff(i, A.n_person);
+    if (qdyn) {   // (the static first two; a block whose first is past its range takes no item -- the claims of
+                  // the blocks that do take items cover every other position, the steals included)
+      const int lo = A.es_it0 + q_x * q_len, hi = min(lo + q_len, itEnd);
+      it_first = lo + (int)blockIdx.x / 8 < hi ? lo + (int)blockIdx.x / 8 : itEnd;
+      q_pos1 = lo + q_nb + (int)blockIdx.x / 8 < hi ? lo + q_nb + (int)blockIdx.x / 8 : -1;
+    } else q_pos1 = next_it(it_first) < itEnd ? next_it(it_first) : -1;
     if (it_first < itEnd) {
       q_item = items[it_first];
       quad_aux(A.ref + ((q_item >> 3) & ~3), s_qaux);
       quad_prefetch(A, q_item, qvoff, qring);
-      if (next_it(it_first) < itEnd) quad_aux(items + next_it(it_first), s_qaux + 64);
+      if (q_pos1 >= 0) quad_aux(items + q_pos1, s_qaux + 64);
+      if (qdyn && q_pos1 >= 0) {   // the first claim (the block's third item), resolved one item from now
+        q_pend_ok = true;
+        q_pend = q_issue();
+      }
     }
   }
   // QD: an item's results wait in LDS and are stored after the next item's hoisting, so that they are older
   // than that item's prefetch in vmcnt order
   __shared__ double s_pend[QD ? 2 : 1];
   __shared__ int s_pendi[QD ? 3 : 1];
-  for (int it = it_first; it < itEnd; it = next_it(it)) {
+  for (int it = it_first; it >= 0 && it < itEnd; it = QD ? q_next : next_it(it)) {
     if (A.phase) ph_t = wall_clock64();
     const int item = QD ? q_item : items[it];
     const int site = item >> 3, cfg = item & 7;
@@ -1872,6 +1920,11 @@ k_brent(DevArgs A, int list) {
     } else r = A.ref[site];
     ItemCtx I;
     item_alleles(A, site, cfg, r, &I.a1, &I.a2);
+    if constexpr (QD) {   // (wave-uniform: the mutation-matrix rows are scalar operands even when the claims' atomics
+                          // keep the cfg-7 result fields from being scalar loads)
+      I.a1 = __builtin_amdgcn_readfirstlane(I.a1);
+      I.a2 = __builtin_amdgcn_readfirstlane(I.a2);
+    }
     I.g11 = d_gi(I.a1, I.a1); I.g12 = d_gi(I.a1, I.a2); I.g22 = d_gi(I.a2, I.a2);
     // the lean polynomial kernel also runs autosomal --denovo items (its hoisting has the de novo kid terms)
     I.denovo = (GEN || (POLYK && DN)) ? (A.denovo && cfg != 7) : 0;
@@ -1908,7 +1961,8 @@ k_brent(DevArgs A, int list) {
       if constexpr (QD) {
         hoist_quad<S, NC>(A, I, pl, s_lk, s_M, cond, qring, qvoff, lm0, le0);
         hoisted = true;
-        const int itn = next_it(it);   // the next item's first slots land during this item's Brent
+        const int itn = q_pos1;   // the next item's first slots land during this item's Brent
+        q_next = itn;
         // (landed: the hoisting ended with vmcnt(0)); uniform, so the next site's addresses are scalar
         const int nitem = __builtin_amdgcn_readfirstlane(((const volatile __attribute__((address_space(3))) int*)s_qaux)[64]);
         // MonomorphismLogLikelihood_denovo (the cfg-0 item, CalcAllFamLogLikelihood at f = 1,
@@ -1932,13 +1986,16 @@ k_brent(DevArgs A, int list) {
           }
           if (mdn) { A.raw[(size_t)site * 8] = mono_dn; A.minv[site * 8] = 0.0; A.evals[site * 8] = 1; }
         }
-        if (itn < itEnd) {
+        if (itn >= 0) {
+          // the position after the next item (dynamic order: the pending claim, and the next claim issued before the DMA)
+          const int itnn = qdyn ? q_next_pos() : (next_it(itn) < itEnd ? next_it(itn) : -1);
           __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): s_qaux has been read before the DMA refills it
           __builtin_amdgcn_sched_barrier(0);
           quad_aux(A.ref + ((nitem >> 3) & ~3), s_qaux);
           quad_prefetch(A, nitem, qvoff, qring);
-          if (next_it(itn) < itEnd) quad_aux(items + next_it(itn), s_qaux + 64);
+          if (itnn >= 0) quad_aux(items + itnn, s_qaux + 64);
           q_item = nitem;
+          q_pos1 = itnn;
         }
       }
       if constexpr (!QD) if (!PFK && !hoisted && A.max_nuc <= 4) {

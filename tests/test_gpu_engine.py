@@ -386,6 +386,44 @@ def test_headline_full_batch_properties(built, denovo):
         assert int(emitted.sum()) == int(c_big[10:15].sum())
 
 
+def test_quad_dynamic_item_order_matches_static(built, monkeypatch):
+    """The QUAD kernel's dynamic item order (per-XCD claim counters, steals at the end of a list) against the static
+    stride order (PM_QD_DYN=0) on a 65 536-site --denovo batch -- lists long enough for claims in every range and
+    for steals: bitwise-identical per-site results, section counters and evaluation counts (every item computed
+    exactly once, whatever wave took it)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    ped = bench.nuclear_pedigree(pm, 1000, 2)
+    B, np_ = 65536, ped.n_person
+    params = pm.Params.defaults(denovo=1)
+    out = []
+    for dyn in ("0", "1"):
+        monkeypatch.setenv("PM_QD_DYN", dyn)
+        eng = pm.Engine(ped, params, max_batch=B)
+        assert eng.plan() == (64, 16)
+        d_pl, d_dm, d_ref = eng.alloc(B * np_ * 10), eng.alloc(B * np_ * 4), eng.alloc(B)
+        eng.synth(B, 11, 0, d_pl, d_dm, d_ref)
+        rsz = pm.engine.SITE_DTYPE.itemsize
+        d_res = eng.alloc(B * rsz)
+        eng.kernel_stats(reset=True)
+        for _ in range(2):   # (twice: the counters are zeroed per launch)
+            eng.run_device(B, d_pl, d_dm, d_ref, d_res, None)
+            eng.sync()
+        r = np.zeros(B, pm.engine.SITE_DTYPE)
+        eng.to_host(r, d_res, B * rsz)
+        ks = eng.kernel_stats()
+        out.append((r, eng.counters().as_array(), ks.evals, ks.items, ks.launches))
+        for x in (d_pl, d_dm, d_ref, d_res):
+            eng.free(x)
+        eng.close()
+    (r0, c0, e0, i0, l0), (r1, c1, e1, i1, l1) = out
+    assert all((r0[f] == r1[f]).all() for f in pm.engine.SITE_DTYPE.names), \
+        [f for f in pm.engine.SITE_DTYPE.names if not (r0[f] == r1[f]).all()]
+    assert (c0 == c1).all() and (e0, i0, l0) == (e1, i1, l1)
+    assert int((r1["evals"] > 0).sum()) > 0
+
+
 def test_bench_rccl_group_of_one(built):
     """bench.py --rccl on the one GPU of the box: the RCCL ("nccl") process group is initialised at one rank and the
     section counters' all-reduce, the barriers and the max-over-ranks timing run through it on the device -- the
