@@ -44,11 +44,24 @@ E10="$BENCH --engines 1 --shape ext10 --families 200 --batch 16384 --no-denovo -
 step pmc_ext10_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_INSTS_VMEM_RD --output-format csv -d "$OUT/pmc_ext10_sq" -o run -- $E10
 step pmc_ext10_sq2 400 rocprofv3 --pmc SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA SQ_INSTS_VMEM_WR SQ_INSTS_SMEM --output-format csv -d "$OUT/pmc_ext10_sq2" -o run -- $E10
 step pmc_ext10_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_ext10_fetch" -o run -- $E10
+# config 4 --denovo's hoisting (es_hoist_wave) and config 5's kernels: SQ and FETCH passes (one engine)
+E10D="$BENCH --engines 1 --shape ext10 --families 200 --batch 4096 --steps 4 --warmup 1 --calib-steps 0"
+step pmc_ext10dn_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_INSTS_VMEM_RD --output-format csv -d "$OUT/pmc_ext10dn_sq" -o run -- $E10D
+step pmc_ext10dn_sq2 400 rocprofv3 --pmc SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA SQ_INSTS_VMEM_WR SQ_INSTS_SMEM --output-format csv -d "$OUT/pmc_ext10dn_sq2" -o run -- $E10D
+step pmc_ext10dn_sq3 400 rocprofv3 --pmc SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_ext10dn_sq3" -o run -- $E10D
+C5="$BENCH --engines 1 --shape mixed --families 2000 --vcf --no-denovo --batch 65536 --steps 4 --warmup 1 --calib-steps 0"
+step pmc_cfg5_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_INSTS_VMEM_RD --output-format csv -d "$OUT/pmc_cfg5_sq" -o run -- $C5
+step pmc_cfg5_sq2 400 rocprofv3 --pmc SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA SQ_INSTS_VMEM_WR SQ_INSTS_SMEM --output-format csv -d "$OUT/pmc_cfg5_sq2" -o run -- $C5
+step pmc_cfg5_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_cfg5_fetch" -o run -- $C5
+# config 4 at its 8-12-member range (extmix), one engine
+step trace_extmix 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_extmix" -o run -- $BENCH --engines 1 --shape extmix --families 200 --batch 16384 --no-denovo --steps 8
 # the other BASELINE configs' bench lines (default three engines)
 B="python3 $R/bench.py --no-cpu-baseline"
 step cfg2 300 $B --shape trio --families 1000 --no-denovo --steps 100
 step cfg4 300 $B --shape ext10 --families 200 --no-denovo --batch 16384 --steps 30
 step cfg4dn 300 $B --shape ext10 --families 200 --batch 4096 --steps 20
+step cfg4mix 300 $B --shape extmix --families 200 --no-denovo --batch 16384 --steps 30
+step cfg4mixdn 300 $B --shape extmix --families 200 --batch 4096 --steps 20
 step cfg5 300 $B --shape mixed --families 2000 --vcf --no-denovo --batch 65536 --steps 60
 step cfg3plain 300 $B --no-denovo --steps 200
 echo done >&2

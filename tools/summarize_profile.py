@@ -66,7 +66,7 @@ def main():
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
     for sub, suffix in (("trace", "_3engines"), ("trace1", "_1engine"), ("trace_ext10", "_ext10"), ("trace_ext10dn", "_ext10dn"),
-                        ("trace_cfg5", "_cfg5")):
+                        ("trace_cfg5", "_cfg5"), ("trace_extmix", "_extmix")):
         if not os.path.exists(os.path.join(src, sub, "run_kernel_stats.csv")):
             continue
         shutil.copy(os.path.join(src, sub, "run_kernel_stats.csv"), os.path.join(dst, f"{rnd}_kernel_stats{suffix}.csv"))
@@ -80,7 +80,7 @@ def main():
             with open(os.path.join(dst, f"{rnd}_bench.json"), "w") as fh:
                 fh.write(bench[-1] + "\n")
     others = []
-    for name in ("cfg2", "cfg3plain", "cfg4", "cfg4dn", "cfg5"):
+    for name in ("cfg2", "cfg3plain", "cfg4", "cfg4dn", "cfg4mix", "cfg4mixdn", "cfg5"):
         path = os.path.join(src, name + ".out")
         if os.path.exists(path):
             lines = [l for l in open(path).read().splitlines() if l.startswith("{")]
@@ -106,11 +106,14 @@ def main():
     out["revision"] = rev
     with open(os.path.join(dst, f"{rnd}_pmc.json"), "w") as fh:
         json.dump(out, fh, indent=1, sort_keys=True)
-    e10 = pmc_summary(src, ("pmc_ext10_fetch", "pmc_ext10_sq", "pmc_ext10_sq2"))   # config 4 BA: EP k_brent + hoisting
-    if e10:
-        e10["revision"] = rev
-        with open(os.path.join(dst, f"{rnd}_pmc_ext10.json"), "w") as fh:
-            json.dump(e10, fh, indent=1, sort_keys=True)
+    for tag, subs in (("ext10", ("pmc_ext10_fetch", "pmc_ext10_sq", "pmc_ext10_sq2")),   # config 4 BA: the fused kernel
+                      ("ext10dn", ("pmc_ext10dn_sq", "pmc_ext10dn_sq2", "pmc_ext10dn_sq3")),   # --denovo: es_hoist_wave
+                      ("cfg5", ("pmc_cfg5_fetch", "pmc_cfg5_sq", "pmc_cfg5_sq2"))):   # config 5
+        e = pmc_summary(src, subs)
+        if e:
+            e["revision"] = rev
+            with open(os.path.join(dst, f"{rnd}_pmc_{tag}.json"), "w") as fh:
+                json.dump(e, fh, indent=1, sort_keys=True)
     print(json.dumps({k: ({kk: round(vv, 1) for kk, vv in v.items()} if isinstance(v, dict) else v) for k, v in out.items()}, indent=1))
 
 
