@@ -532,6 +532,11 @@ bool g_pair = false;
 bool g_fence = true;      // PM_ES_FENCE=0: wave_sync without the wavefront-scope fences (measured 2% slower)
 bool g_xcd = true;        // PM_ES_XCD=0: units dealt to the blocks in plain order
 bool g_no_penp = false;   // PM_ES_PENP=0: leaf offspring partials stored and read from the workspace
+// dense 10-state type-3 steps with a marriage partial (the plain transmission, quirk :1391): each child state's sum runs
+// over its non-zero parent pairs from an LDS list (t3z / t3n, filled from kT3z / kT3n at kernel start); g_t3z: some
+// family of the kernel uses it (PM_ES_T3Z=0, g_no_t3z: the 100-pair loop over the global table)
+bool g_t3z = false;
+bool g_no_t3z = false;
 int g_wl = 64;
 // PM_ES_FACT=1 (opt-in experiment): a dense 10-state type-1 run through T10dn = T10 * M (SetTransmissionMatrix_denovo
 // :787-810) -- P' = M P per offspring coefficient (lanes over (genotype, coefficient)), then per pair 0.25 x the sum
@@ -1332,7 +1337,15 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
               "    }\n  }\n  wave_sync();\n";
       std::string b2 = "    double s[" + S(ww) + "];\n";
       for (int a = 0; a <= dw; a++) b2 += "    s[" + S(a) + "] = 0.0;\n";
-      b2 += "    for (int e = 0; e < " + nsq + "; e++) {\n      const double t = " + tt(csex, "e", "k", slot != 255) + ";\n";
+      if (NS == 10 && slot != 255 && !g_no_t3z) {
+        // the plain transmission (:1391) is the Mendelian table: 16-31 of a child state's 100 parent pairs are non-zero
+        // (1, 1/2 or 1/4).  Each lane k runs over its non-zero pairs only, in ascending e (the LDS list t3z, e << 2 |
+        // value code): the pairs skipped would add +0 (T = 0, W finite and >= 0), so every sum keeps its bits -- and no
+        // transmission load is waited for in the 100-step loop
+        g_t3z = true;
+        b2 += "    const int nz_ = t3n[k];\n    for (int q_ = 0; q_ < nz_; q_++) {\n      const int pk_ = t3z[k * 32 + q_], e = pk_ >> 2;\n"
+              "      const double t = (pk_ & 3) == 0 ? 1.0 : (pk_ & 3) == 1 ? 0.5 : 0.25;\n";
+      } else b2 += "    for (int e = 0; e < " + nsq + "; e++) {\n      const double t = " + tt(csex, "e", "k", slot != 255) + ";\n";
       for (int a = 0; a <= dw; a++) b2 += "      s[" + S(a) + "] = fma(t, W[" + TBs + " + e * " + S(ww) + " + " + S(a) + "], s[" + S(a) + "]);\n";
       b2 += "    }\n    double t[" + S(g.e + 1) + "];\n";
       for (int c = 0; c <= g.e; c++) b2 += "    t[" + S(c) + "] = W[" + PO(off_) + " + k * " + S(capP[off_]) + " + " + S(c) + "];\n";
@@ -1418,7 +1431,7 @@ extern "C" __global__ void __launch_bounds__(64 * WPB) WPEU es_hoist_wave(Args A
   __shared__ double ws[WPB][(PAIR ? 2 : 1) * (WSIZE + PENSZ)];
   for (int i = threadIdx.x; i < 256; i += blockDim.x) lk[i] = A.lktab[i];
   for (int i = threadIdx.x; i < 6 * 27; i += blockDim.x) tb[i] = i < 5 * 27 ? A.tba[i] : 1.0;
-  __syncthreads();
+T3FILL  __syncthreads();
   // PAIR: half-wave h = lane >> 5 hoists the pair's family h in its own slice; `lane` is the lane within the half
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & (PAIR ? 31 : 63);
   const int half = PAIR ? (threadIdx.x >> 5) & 1 : 0;
@@ -1446,16 +1459,35 @@ extern "C" __global__ void __launch_bounds__(64 * WPB) WPEU es_hoist_wave(Args A
   // the next task's penetrance bytes are loaded while this one is computed (NPF per lane: 10 n <= 64 NPF)
   unsigned pb[NPF > 0 ? NPF : 1];
   long long pf_u = -1;   // the task whose bytes pb holds
-  auto prefetch = [&](long long uu) {
+  // A task's words are loaded ahead, so no load is waited for when it starts: its G item words two tasks ahead, the
+  // sites' reference bytes one task ahead (both uniform); the family unit's slot words are constants of the generated
+  // source (kUP0 / kUE / kUSig, per unit and half), so the penetrance-byte prefetch below has no dependent load chain
+  int c_item[4], c_ref[4], n1_item[4], n1_ref[4], n2_item[4];
+  auto load_items = [&](long long uu, int* it4) {
+#pragma unroll
+    for (int t = 0; t < 4; t++) it4[t] = -1;
+    if (uu >= units) return;
+    const int itn = A.it0 + (int)(uu / nfu) * G;
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+      if (t < G && itn + t < nItems) it4[t] = A.items[itn + t];
+  };
+  auto load_refs = [&](const int* it4, int* r4) {
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      const int w = __builtin_amdgcn_readfirstlane(it4[t]);
+      r4[t] = w >= 0 ? (int)A.ref[w >> 3] : 0;
+    }
+  };
+  auto prefetch = [&](long long uu, int item_w) {   // (item_w: the task's first item word, landed)
     pf_u = -1;
     if (NPF == 0 || uu >= units) return;
     const int uqn = (int)(uu / nfu), kn0 = (int)(uu - (long long)uqn * nfu);
-    const int itn = A.it0 + uqn * G;
-    if (itn >= nItems) return;
-    const int sn = __builtin_amdgcn_readfirstlane(A.items[itn]) >> 3;
-    const int kn = PAIR ? A.pair_k[2 * kn0 + half] : kn0, ks = PAIR ? __builtin_amdgcn_readfirstlane(A.pair_k[2 * kn0]) : kn0;
-    const int p0n = PAIR ? A.slot_p0[kn] : __builtin_amdgcn_readfirstlane(A.slot_p0[kn]);
-    const int nn = shape_n(__builtin_amdgcn_readfirstlane(A.slot_sig[ks]));
+    const int w = __builtin_amdgcn_readfirstlane(item_w);
+    if (w < 0) return;
+    const int sn = w >> 3;
+    const int p0n = half ? kUP0[2 * kn0 + 1] : kUP0[2 * kn0];
+    const int nn = shape_n(kUSig[kn0]);
     if (10 * nn > LPF * NPF) return;
     const uint8_t* pln = A.pl + (size_t)sn * A.np * 10 + p0n;
 #pragma unroll
@@ -1471,18 +1503,28 @@ extern "C" __global__ void __launch_bounds__(64 * WPB) WPEU es_hoist_wave(Args A
   const long long u_first = (XCD && gridDim.x % 8 == 0)
       ? (long long)(blockIdx.x % 8) * (gridDim.x / 8) * WPB + (long long)(blockIdx.x / 8) * WPB + wave
       : (long long)blockIdx.x * WPB + wave;
-  prefetch(u_first);
+  load_items(u_first, c_item);
+  load_refs(c_item, c_ref);
+  load_items(u_first + stride, n1_item);
+  load_refs(n1_item, n1_ref);
+  load_items(u_first + 2 * stride, n2_item);
+  prefetch(u_first, c_item[0]);
   for (long long u = u_first; u < units; u += stride) {
     const int uq = (int)(u / nfu), k0 = (int)(u - (long long)uq * nfu);
-    // (PAIR: k is this half's slot -- per lane; ks the pair's first slot, whose shape both halves share)
-    const int k = PAIR ? A.pair_k[2 * k0 + half] : k0, ks = PAIR ? __builtin_amdgcn_readfirstlane(A.pair_k[2 * k0]) : k0;
+    if (u != u_first) {   // rotate: this task's words (landed a task ago), the next task's refs, the task after's items
+#pragma unroll
+      for (int t = 0; t < 4; t++) { c_item[t] = n1_item[t]; c_ref[t] = n1_ref[t]; n1_item[t] = n2_item[t]; }
+      load_refs(n1_item, n1_ref);
+      load_items(u + 2 * stride, n2_item);
+    }
+    // (PAIR: the unit's half -- per lane; both halves share the pair's shape)
     int leaf_site = -1, pen_site = -1;
     unsigned long long tq = PROF ? __builtin_readcyclecounter() : 0;
     for (int t = 0; t < G; t++) {
     const int it = A.it0 + uq * G + t;
-    if (it >= nItems) break;
-    const int item = __builtin_amdgcn_readfirstlane(A.items[it]);
-    const int site = item >> 3, cfg = item & 7, r = A.ref[site];
+    const int item = __builtin_amdgcn_readfirstlane(c_item[t]);
+    if (item < 0) break;
+    const int site = item >> 3, cfg = item & 7, r = __builtin_amdgcn_readfirstlane(c_ref[t]);
     int a1, a2;
     if (A.vcf) { a1 = r & 15; a2 = r >> 4; }
     else if (cfg == 7) { a1 = A.res[(size_t)site * A.res_words + A.res_a1]; a2 = A.res[(size_t)site * A.res_words + A.res_a2]; }
@@ -1492,8 +1534,8 @@ extern "C" __global__ void __launch_bounds__(64 * WPB) WPEU es_hoist_wave(Args A
     const uint8_t* P11 = pl + (size_t)g11 * A.np;
     const uint8_t* P12 = pl + (size_t)g12 * A.np;
     const uint8_t* P22 = pl + (size_t)g22 * A.np;
-    const int e = PAIR ? A.slot_e[k] : __builtin_amdgcn_readfirstlane(A.slot_e[k]), q = e / A.T;
-    const int sig = __builtin_amdgcn_readfirstlane(A.slot_sig[ks]), p0 = PAIR ? A.slot_p0[k] : __builtin_amdgcn_readfirstlane(A.slot_p0[k]);
+    const int e = half ? kUE[2 * k0 + 1] : kUE[2 * k0], q = e / A.T;
+    const int sig = kUSig[k0], p0 = half ? kUP0[2 * k0 + 1] : kUP0[2 * k0];
     double* out = A.coef + ((size_t)(it - A.it0) * A.max_ext + q) * A.dcap * A.T + (e - q * A.T);
     const int dn = A.denovo && cfg != 7, top = dn && cfg == 0 && !A.vcf;   // variant: 0 bi-allelic, 1 10-state, 2 top
     if (site != pen_site) {
@@ -1503,7 +1545,7 @@ extern "C" __global__ void __launch_bounds__(64 * WPB) WPEU es_hoist_wave(Args A
         for (int r = 0; r < (NPF > 0 ? NPF : 1); r++)
           if (lane + LPF * r < 10 * nn) PEN[lane + LPF * r] = lk[pb[r]];
         wave_sync();
-        prefetch(u + stride);
+        prefetch(u + stride, n1_item[0]);
       } else {
         switch (sig) {
 PENS        }
@@ -1548,6 +1590,8 @@ PARTS2      }
     leaf_site = -1;   // (the other variants' layouts overlay the leaf prefix's partials)
     switch (sig * 3 + (top ? 2 : dn ? 1 : 0)) {
 )";
+  k.replace(k.find("T3FILL"), 6, g_t3z ? "  for (int i = threadIdx.x; i < 330; i += blockDim.x) {\n    if (i < 320) t3z[i] = kT3z[i];\n"
+                                         "    else t3n[i - 320] = kT3n[i - 320];\n  }\n" : "");
   for (size_t at; (at = k.find("WSIZE")) != std::string::npos;) k.replace(at, 5, std::to_string(ws));
   for (size_t at; (at = k.find("PENSZ")) != std::string::npos;) k.replace(at, 5, std::to_string(pensz));
   for (size_t at; (at = k.find("NPF")) != std::string::npos;) k.replace(at, 3, std::to_string(npf));
@@ -1656,6 +1700,9 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
   g_fence = !(efn && efn[0] == '0');
   const char* exd = getenv("PM_ES_XCD");
   g_xcd = !(exd && exd[0] == '0');
+  const char* etz = getenv("PM_ES_T3Z");
+  g_no_t3z = etz && etz[0] == '0';
+  g_t3z = false;
   if (g_pair) { g_regp = 0; g_regf = false; g_tr_regs = false; }   // (cross-lane reads by LDS only in pair mode)
   {
     int nmax = 0;
@@ -1735,7 +1782,7 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
     out->wave = false;
   } else {
     // waves per block: as many workspace slices as fit the 64 KB of static LDS next to the tables
-    const int tables = (256 + 6 * 27) * 8;
+    const int tables = (256 + 6 * 27) * 8 + (g_t3z ? (320 + 10) * 4 : 0);
     // (one wave per SIMD: the occupancy comes from blocks per CU, build() asks the runtime for them)
     const int slice = (g_pair ? 2 : 1) * (ws + pensz) * 8;   // (a pair's two family slices per wave)
     // (at most 4: one wave per SIMD and block; measured on config 4 --denovo, 4 beat 1, 2, 5 and 6 even where those
@@ -1747,6 +1794,45 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
     std::string wk = gen_wave_kernel(wave_names, part_names, pen_names, shape_ns, pps, ws, pensz, std::max(1, out->wpb), denovo == 2);
     const size_t at = wk.find("extern \"C\"");   // device helpers first, then the family functions, then the kernel
     src += wk.substr(0, at);
+    {   // the family units' slot words (unit = slot pair in pair mode, else slot; both halves' entries): constants
+      const size_t nu = g_pair ? out->pair_k.size() / 2 : out->slot_e.size();
+      std::string p0 = "__constant__ int kUP0[" + std::to_string(2 * nu) + "] = {", e = "__constant__ int kUE[" + std::to_string(2 * nu) + "] = {",
+                  sg = "__constant__ int kUSig[" + std::to_string(nu) + "] = {";
+      for (size_t u = 0; u < nu; u++) {
+        const int k0 = g_pair ? out->pair_k[2 * u] : (int)u, k1 = g_pair ? out->pair_k[2 * u + 1] : (int)u;
+        p0 += std::to_string(out->slot_p0[k0]) + "," + std::to_string(out->slot_p0[k1]) + ",";
+        e += std::to_string(out->slot_e[k0]) + "," + std::to_string(out->slot_e[k1]) + ",";
+        sg += std::to_string(out->slot_sig[k0]) + ",";
+      }
+      src += p0 + "};\n" + e + "};\n" + sg + "};\n";
+    }
+    if (g_t3z) {   // the plain Mendelian T(e = i 10 + j, k)'s non-zero terms per child state k, ascending e: e << 2 | code
+      auto gi = [](int b1, int b2) { return b1 < b2 ? (b1 - 1) * (10 - b1) / 2 + (b2 - b1) : (b2 - 1) * (10 - b2) / 2 + (b1 - b2); };
+      std::vector<double> T(1000, 0.0);
+      for (int i = 1; i <= 4; i++)
+        for (int j = i; j <= 4; j++)
+          for (int k = 1; k <= 4; k++)
+            for (int m = k; m <= 4; m++) {
+              const int g[4] = {gi(i, k), gi(i, m), gi(j, k), gi(j, m)};
+              for (int t = 0; t < 4; t++) T[(gi(i, j) * 10 + gi(k, m)) * 10 + g[t]] += 0.25;
+            }
+      std::string z = "__shared__ int t3z[320], t3n[10];\n__device__ const int kT3z[320] = {", zn = "__device__ const int kT3n[10] = {";
+      for (int k = 0; k < 10; k++) {
+        int q = 0;
+        for (int e = 0; e < 100; e++) {
+          const double t = T[e * 10 + k];
+          if (t == 0.0) continue;
+          const int code = t == 1.0 ? 0 : t == 0.5 ? 1 : 2;
+          if (code == 2 && t != 0.25) { fprintf(stderr, "es_jit: unexpected Mendelian entry\n"); abort(); }
+          z += std::to_string(e << 2 | code) + ",";
+          q++;
+        }
+        if (q > 32) { fprintf(stderr, "es_jit: Mendelian list over 32\n"); abort(); }
+        for (; q < 32; q++) z += "0,";
+        zn += std::to_string([&] { int c = 0; for (int e = 0; e < 100; e++) c += T[e * 10 + k] != 0.0; return c; }()) + ",";
+      }
+      src += z + "};\n" + zn + "};\n";
+    }
     for (auto& b : wave_bodies) src += b;
     src += wk.substr(at);
     out->wave = true;

@@ -109,11 +109,14 @@ def test_es_hoisting_kernels_agree(built, tmp_path, monkeypatch, name):
 _SP3_CASES = [n for n in DUMP_CASES if n.startswith(("roof", "roof2", "extmix", "big_extmix")) and "denovo" in n]
 
 
+@pytest.mark.parametrize("switch", ["PM_ES_SP3", "PM_ES_T3Z"])
 @pytest.mark.parametrize("name", _SP3_CASES)
-def test_es_type3_founder_sparsity_is_bit_exact(built, tmp_path, monkeypatch, name):
-    """--denovo 10-state peels: the schedule compiler's founder-sparse type-3 steps (a roof parent that is a founder has
-    only its prior's 1-3 states; the pairs outside them add +0) give the same results bit for bit as the dense steps
-    (PM_ES_SP3=0), and both match the reference dump."""
+def test_es_type3_founder_sparsity_is_bit_exact(built, tmp_path, monkeypatch, name, switch):
+    """--denovo 10-state peels: the schedule compiler's sparse type-3 sums give the same results bit for bit as the
+    dense ones, and both match the reference dump.  PM_ES_SP3: founder-sparse steps (a roof parent that is a founder has
+    only its prior's 1-3 states; the pairs outside them add +0) against all 100 pairs; PM_ES_T3Z: the non-founder
+    steps' child sums over the Mendelian table's non-zero parent pairs only (the rest add +0) against the 100-pair
+    loop."""
     import numpy as np
     case = make_dataset(name, str(tmp_path))
     ped, secs, _ = read_dataset(str(tmp_path))
@@ -122,7 +125,7 @@ def test_es_type3_founder_sparsity_is_bit_exact(built, tmp_path, monkeypatch, na
     out = {}
     for mode in ("sparse", "dense"):
         if mode == "dense":
-            monkeypatch.setenv("PM_ES_SP3", "0")
+            monkeypatch.setenv(switch, "0")
         eng = pm.Engine(ped.view, par, max_batch=256)
         eng.begin_section(chrom)
         runs = [eng.run(pl[s:s + 256], dm[s:s + 256], ref[s:s + 256]) for s in range(0, len(ref), 256)]
