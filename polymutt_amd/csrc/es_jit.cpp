@@ -529,6 +529,9 @@ int g_expt = 0;        // PM_ES_EXPT=1/2: timing experiments only (results wrong
 // over 30 pairs, the final sum) does two families' work per instruction; g_wl = the lanes per family (64 or 32).
 // Pair mode reads partials across lanes through LDS only (no v_readlane from fixed lanes: PM_ES_REGP / REGF off).
 bool g_pair = false;
+// families per wave (PM_ES_FPW: 1, 2 -- the pair mode above -- or 4): g_wl = 64 / g_fpw lanes per family
+int g_fpw = 1;
+bool g_wspack = true;     // PM_ES_WSPACK=0: part-2 regions laid out in order instead of packed by live range
 bool g_fence = true;      // PM_ES_FENCE=0: wave_sync without the wavefront-scope fences (measured 2% slower)
 bool g_xcd = true;        // PM_ES_XCD=0: units dealt to the blocks in plain order
 bool g_no_penp = false;   // PM_ES_PENP=0: leaf offspring partials stored and read from the workspace
@@ -782,14 +785,108 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
       }
     if (L == 1) LSZ = off;
   }
-  const int TB = off, NSZ = off + tmp - LSZ;
+  int TB = off, NSZ = off + tmp - LSZ;
+  // Part 2 (the per-item rest, the top rest): its own regions packed by live range (g_wspack, PM_ES_WSPACK=0: in
+  // order).  A region is live from the phase of its first write to the phase of its last read; phases are counted
+  // conservatively (consecutive steps of one type share one, a type-3 step is one, the initial partials' phase is -1,
+  // the final sum the last), and a region may take the place of one whose live range ended in an earlier phase: a
+  // wave_sync lies between them.  Smaller slices -> more slices in a CU's LDS -> more waves in flight.
+  if (part == 2 && M == 1 && NS == 10 && !g_fact && g_wspack) {
+    std::vector<int> ph(nst, -2);
+    int cur = -1, prevt = -1;
+    for (int k = 0; k < nst; k++) {
+      if (!inpart(k)) continue;
+      const int t = F.steps[k].x & 255;
+      if (t != prevt || t == 3) cur++;
+      prevt = t;
+      ph[k] = cur;
+    }
+    struct Reg { int size = 0, lo = 1 << 30, hi = -3, off = 0; };
+    std::map<int, Reg> rg;   // person i, marriage slot (1000 + slot), the type-3 temporaries (-1)
+    auto touch = [&](int id, int size, int p) {
+      Reg& r = rg[id];
+      r.size = size;
+      r.lo = std::min(r.lo, p);
+      r.hi = std::max(r.hi, p);
+    };
+    auto stored = [&](int i) { return !leafp[i] && !regf[i] && !regn[i] && !penp[i]; };
+    auto msize = [&](int sl) { return (crows.count(sl) ? crows[sl] : NS * NS) * capM[sl]; };
+    for (int i = 0; i < n; i++)
+      if (stored(i) && !iinit[i]) touch(i, NS * capP[i], -1);   // (the initial partials written up front)
+    for (int k = 0; k < nst; k++) {
+      if (!inpart(k)) continue;
+      const int t = F.steps[k].x & 255, f0 = (F.steps[k].x >> 8) & 255, f1 = (F.steps[k].x >> 16) & 255, t0 = (F.steps[k].x >> 24) & 255;
+      const int sl = (F.steps[k].y >> 8) & 255;
+      if (stored(f0)) touch(f0, NS * capP[f0], ph[k]);
+      if (t == 3 && stored(f1)) touch(f1, NS * capP[f1], ph[k]);
+      if (t != 1 && stored(t0)) touch(t0, NS * capP[t0], ph[k]);
+      if (sl != 255 && !leafs.count(sl)) touch(1000 + sl, msize(sl), ph[k]);
+      if (t == 3) touch(-1, tmp, ph[k]);
+    }
+    const int fin_ = (F.steps.back().x >> 24) & 255;
+    if (stored(fin_)) touch(fin_, NS * capP[fin_], cur + 1);
+    // first fit over a few placement orders (the first write, the size, the live-range length; ties by the others),
+    // keeping the smallest footprint
+    std::vector<int> ids;
+    for (auto& r : rg) ids.push_back(r.first);
+    auto fit = [&](const std::vector<int>& order, bool commit) {
+      std::vector<std::pair<int, int>> pl;   // (id, offset)
+      int t_ = LSZ;
+      for (int id : order) {
+        const Reg& r = rg[id];
+        int o = LSZ;
+        for (bool moved = true; moved;) {
+          moved = false;
+          for (auto& q : pl) {
+            const Reg& a = rg[q.first];
+            const bool live = a.hi >= r.lo && r.hi >= a.lo;
+            if (live && o < q.second + a.size && q.second < o + r.size) { o = q.second + a.size; moved = true; }
+          }
+        }
+        pl.push_back({id, o});
+        t_ = std::max(t_, o + r.size);
+      }
+      if (commit)
+        for (auto& q : pl) rg[q.first].off = q.second;
+      return t_;
+    };
+    std::vector<std::vector<int>> orders;
+    for (int key = 0; key < 3; key++) {
+      std::vector<int> o = ids;
+      std::stable_sort(o.begin(), o.end(), [&](int a, int b) {
+        const Reg &x = rg[a], &y = rg[b];
+        if (key == 0 && x.lo != y.lo) return x.lo < y.lo;
+        if (key == 2 && x.hi - x.lo != y.hi - y.lo) return x.hi - x.lo > y.hi - y.lo;
+        if (x.size != y.size) return x.size > y.size;
+        return x.lo < y.lo;
+      });
+      orders.push_back(o);
+    }
+    size_t best = 0;
+    int top_ = fit(orders[0], false);
+    for (size_t q = 1; q < orders.size(); q++) {
+      const int t_ = fit(orders[q], false);
+      if (t_ < top_) { top_ = t_; best = q; }
+    }
+    fit(orders[best], true);
+    for (auto& r : rg) {
+      if (r.first == -1) TB = r.second.off;
+      else if (r.first >= 1000) mo[r.first - 1000] = r.second.off;
+      else po[r.first] = r.second.off;
+    }
+    if (!rg.count(-1)) TB = top_;   // (no type-3 step: tmp = 1, above the rest)
+    NSZ = std::max(1, (rg.count(-1) ? top_ : top_ + tmp) - LSZ);
+  }
   // (the leaf prefix writes its own regions only -- and with PM_ES_FACT its P' rows in the temporaries' region)
   *ws_doubles = part == 1 ? (g_fact && NS == 10 ? TB + tmp : LSZ) : LSZ + M * NSZ;
   if (getenv("PM_JIT_LAYOUT")) {
     fprintf(stderr, "layout %s NS %d part %d top %d: LSZ %d NSZ %d tmp %d ws %d |", name.c_str(), NS, part, (int)top, LSZ, NSZ, tmp, *ws_doubles);
     for (int i = 0; i < n; i++) fprintf(stderr, " p%d:%d%s", i, (!regf[i] && !regn[i]) ? NS * capP[i] : 0, leafp[i] ? "L" : "");
     for (auto& m : capM) fprintf(stderr, " m%d:%d", m.first, (crows.count(m.first) ? crows[m.first] : NS * NS) * m.second);
-    fprintf(stderr, "\n");
+    fprintf(stderr, " | offsets");
+    for (int i = 0; i < n; i++) fprintf(stderr, " p%d@%d", i, po[i]);
+    for (auto& m : capM) fprintf(stderr, " m%d@%d", m.first, mo[m.first]);
+    fprintf(stderr, " tb@%d\n", TB);
   }
   auto S = [](long v) { return std::to_string(v); };
   const std::string nsS = S(NS), nsq = S(NS * NS), R = S((NS * NS + g_wl - 1) / g_wl), WL = S(g_wl);
@@ -959,7 +1056,8 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
           nops -= (1.0 - fr) * 100.0 * ((g.a + 1) * 10.0 + (create ? 0 : (g.a + 1) * (g.b + 1)));
           for (int k2 : run) frac1[k2] = fr;
         }
-        const int npair = sparse ? 1 : (100 + g_wl - 1) / g_wl;
+        const int nsp = 10 * (int)sp_terms.size();   // (sparse: the rows, passes of g_wl lanes over them)
+        const int npair = sparse ? (nsp + g_wl - 1) / g_wl : (100 + g_wl - 1) / g_wl;
         bool fact = g_fact && !sparse;
         for (int k2 : run)
           if (regp.count((F.steps[k2].x >> 8) & 255)) fact = false;
@@ -979,12 +1077,17 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
           code += "  wave_sync();\n";
         }
         std::string c1 = "  {\n";
-        if (sparse) {
+        if (sparse) {   // pass pr: row p = lane + pr g_wl (state o of the spouse, term qi of the founder's support); rows past
+                        // the support compute an in-range pair and store nothing
           const std::string gq[3] = {"g11", "g12", "g22"};
-          std::string sF = gq[sp_terms.back().first];
-          for (int q = (int)sp_terms.size() - 2; q >= 0; q--) sF = "qi_ == " + S(q) + " ? " + gq[sp_terms[q].first] + " : " + sF;
-          c1 += "    const int qi_ = lane / 10, o_ = lane - qi_ * 10, sF_ = " + sF + ";\n    const int e = " +
-                (sp_father ? "sF_ * 10 + o_" : "o_ * 10 + sF_") + ";\n    if (lane < " + S(10 * sp_terms.size()) + ") {\n";
+          for (int pr = 0; pr < npair; pr++) {
+            const std::string P = S(pr), qi = "qi" + P;
+            std::string sF = gq[sp_terms.back().first];
+            for (int q = (int)sp_terms.size() - 2; q >= 0; q--) sF = qi + " == " + S(q) + " ? " + gq[sp_terms[q].first] + " : " + sF;
+            c1 += "    const int p" + P + " = lane + " + S(pr * g_wl) + ", " + qi + " = p" + P + " / 10, o" + P + " = p" + P + " - " + qi +
+                  " * 10, sF" + P + " = " + sF + ";\n    const int e" + P + " = " +
+                  (sp_father ? "sF" + P + " * 10 + o" + P : "o" + P + " * 10 + sF" + P) + ";\n";
+          }
         } else
           for (int pr = 1; pr < npair; pr++)
             c1 += "    const int e" + S(pr) + " = lane + " + S(pr * g_wl) + ", e" + S(pr) + "c = e" + S(pr) + " < 100 ? e" + S(pr) + " : lane;\n";
@@ -1011,7 +1114,11 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
         // spills)
         if (!fact) {
         c1 += "#pragma unroll 2\n    for (int k = 0; k < 10; k++) {\n";
-        if (sparse) c1 += "      const double t0 = t10dn[e * 10 + k];\n";
+        if (sparse) {
+          c1 += "      const double t0 = t10dn[e0 * 10 + k]";
+          for (int pr = 1; pr < npair; pr++) c1 += ", t" + S(pr) + " = t10dn[e" + S(pr) + " * 10 + k]";
+          c1 += ";\n";
+        }
         else if (npair > 2) {   // (pair mode: the rows of this lane's four pairs)
           c1 += "      const double t0 = t10dn[lane * 10 + k]";
           for (int pr = 1; pr < npair; pr++) c1 += ", t" + S(pr) + " = t10dn[e" + S(pr) + "c * 10 + k]";
@@ -1041,8 +1148,8 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
         }
         // per pair: each marriage partial chained through its steps in registers, one write
         for (int pr = 0; pr < npair; pr++) {
-          const std::string sp = "s" + S(pr) + "_", e = spi.compact ? "lane" : sparse ? "e" : pr ? "e" + S(pr) : "lane";
-          c1 += pr ? "    if (e" + S(pr) + " < 100) {\n" : "    {\n";
+          const std::string sp = "s" + S(pr) + "_", e = spi.compact ? "p" + S(pr) : sparse ? "e" + S(pr) : pr ? "e" + S(pr) : "lane";
+          c1 += sparse ? "    if (p" + S(pr) + " < " + S(nsp) + ") {\n" : pr ? "    if (e" + S(pr) + " < 100) {\n" : "    {\n";
           int cid = 0;
           for (int sl2 : slots) {
             const std::string mev = MOf(sl2) + " + " + e + " * " + S(capM[sl2]);
@@ -1076,7 +1183,6 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
           }
           c1 += "    }\n";
         }
-        if (sparse) c1 += "    }\n";
         c1 += "  }\n  wave_sync();\n";
         code += c1;
       } else
@@ -1388,7 +1494,8 @@ std::string gen_pen_fill(int n, const std::string& name) {
 // the top variant's rest and (pps == 4) the 10-state rest of three items at once
 std::string gen_wave_kernel(const std::vector<std::string>& fns, const std::vector<std::string>& parts, const std::vector<std::string>& pens,
                             const std::vector<int>& shape_ns, int pps, int ws, int pensz, int wpb, bool parts_only) {
-  const int npf = pensz <= 4 * g_wl ? (pensz + g_wl - 1) / g_wl : 0;   // prefetch registers per lane (0: families too large)
+  // prefetch registers per lane (0: families too large; up to 4, 8 at 16 lanes per family)
+  const int npf = pensz <= (g_wl >= 32 ? 4 : 8) * g_wl ? (pensz + g_wl - 1) / g_wl : 0;
   // wave_sync: the phases' LDS hand-over inside one wave.  A wave's LDS instructions execute in issue order, so a
   // read after a write sees it without waiting for the write; only the compiler must not move accesses across
   // (g_fence, the default: wavefront-scope release / acquire fences, which wait for the outstanding LDS accesses --
@@ -1428,13 +1535,14 @@ __device__ __forceinline__ void wave_sync() {
   std::string k = R"(
 extern "C" __global__ void __launch_bounds__(64 * WPB) WPEU es_hoist_wave(Args A) {   // blockDim = 64 WPB
   __shared__ double lk[256], tb[6 * 27];
-  __shared__ double ws[WPB][(PAIR ? 2 : 1) * (WSIZE + PENSZ)];
+  __shared__ double ws[WPB][FPW * (WSIZE + PENSZ)];
   for (int i = threadIdx.x; i < 256; i += blockDim.x) lk[i] = A.lktab[i];
   for (int i = threadIdx.x; i < 6 * 27; i += blockDim.x) tb[i] = i < 5 * 27 ? A.tba[i] : 1.0;
 T3FILL  __syncthreads();
-  // PAIR: half-wave h = lane >> 5 hoists the pair's family h in its own slice; `lane` is the lane within the half
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & (PAIR ? 31 : 63);
-  const int half = PAIR ? (threadIdx.x >> 5) & 1 : 0;
+  // FPW families per wave: lane group h (LPF lanes) hoists the unit's family h in its own slice; `lane` is the lane within
+  // the group (`half`: the group, from the pair mode of two)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & (LPF - 1);
+  const int half = FPW > 1 ? (threadIdx.x & 63) / LPF : 0;
   double* W = ws[wave] + half * (WSIZE + PENSZ);
   double* PEN = W + WSIZE;   // the current (site, family)'s penetrances
   // the de novo transmission rows of this lane's marriage-partial pairs (lane, lane + 64), for every 10-state step
@@ -1454,7 +1562,7 @@ T3FILL  __syncthreads();
   // a task: G consecutive items of the list -- with A.group, the de novo items of one site (list 0: cfgs 0-3, list 1:
   // cfgs 4-6), whose 10-state leaf steps are taken once per (site, family) -- on one family
   const int G = A.group > 1 ? A.group : 1;
-  const int nfu = PAIR ? A.npairs : A.nslots;   // family units per task: slots, or slot pairs
+  const int nfu = kNUnits;   // family units per task: slots, or units of FPW slots
   const long long units = ((long long)(nItems - A.it0) + G - 1) / G * nfu;
   // the next task's penetrance bytes are loaded while this one is computed (NPF per lane: 10 n <= 64 NPF)
   unsigned pb[NPF > 0 ? NPF : 1];
@@ -1486,7 +1594,7 @@ T3FILL  __syncthreads();
     const int w = __builtin_amdgcn_readfirstlane(item_w);
     if (w < 0) return;
     const int sn = w >> 3;
-    const int p0n = half ? kUP0[2 * kn0 + 1] : kUP0[2 * kn0];
+    const int p0n = kUP0[FPW * kn0 + half];
     const int nn = shape_n(kUSig[kn0]);
     if (10 * nn > LPF * NPF) return;
     const uint8_t* pln = A.pl + (size_t)sn * A.np * 10 + p0n;
@@ -1534,8 +1642,8 @@ T3FILL  __syncthreads();
     const uint8_t* P11 = pl + (size_t)g11 * A.np;
     const uint8_t* P12 = pl + (size_t)g12 * A.np;
     const uint8_t* P22 = pl + (size_t)g22 * A.np;
-    const int e = half ? kUE[2 * k0 + 1] : kUE[2 * k0], q = e / A.T;
-    const int sig = kUSig[k0], p0 = half ? kUP0[2 * k0 + 1] : kUP0[2 * k0];
+    const int e = kUE[FPW * k0 + half], q = e / A.T;
+    const int sig = kUSig[k0], p0 = kUP0[FPW * k0 + half];
     double* out = A.coef + ((size_t)(it - A.it0) * A.max_ext + q) * A.dcap * A.T + (e - q * A.T);
     const int dn = A.denovo && cfg != 7, top = dn && cfg == 0 && !A.vcf;   // variant: 0 bi-allelic, 1 10-state, 2 top
     if (site != pen_site) {
@@ -1597,6 +1705,7 @@ PARTS2      }
   for (size_t at; (at = k.find("NPF")) != std::string::npos;) k.replace(at, 3, std::to_string(npf));
   for (size_t at; (at = k.find("LPF")) != std::string::npos;) k.replace(at, 3, std::to_string(g_wl));
   for (size_t at; (at = k.find("PAIR")) != std::string::npos;) k.replace(at, 4, g_pair ? "true" : "false");
+  for (size_t at; (at = k.find("FPW")) != std::string::npos;) k.replace(at, 3, std::to_string(g_fpw));
   k.replace(k.find("XCD &&"), 3, g_xcd ? "true" : "false");
   {
     std::string cases;
@@ -1692,14 +1801,19 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
   const char* efc = getenv("PM_ES_FACT");
   g_fact = denovo != 0 && efc && efc[0] == '1';
   const char* epr = getenv("PM_ES_PAIR");
-  g_pair = denovo != 0 && !(epr && epr[0] == '0') && pps == 3;
-  g_wl = g_pair ? 32 : 64;
+  const char* efw = getenv("PM_ES_FPW");
+  g_fpw = (denovo != 0 && !(epr && epr[0] == '0') && pps == 3) ? 2 : 1;
+  if (g_fpw > 1 && efw) g_fpw = atoi(efw) >= 4 ? 4 : atoi(efw) >= 2 ? 2 : 1;
+  g_pair = g_fpw > 1;
+  g_wl = 64 / g_fpw;
   const char* epp = getenv("PM_ES_PENP");
   g_no_penp = epp && epp[0] == '0';
   const char* efn = getenv("PM_ES_FENCE");
   g_fence = !(efn && efn[0] == '0');
   const char* exd = getenv("PM_ES_XCD");
   g_xcd = !(exd && exd[0] == '0');
+  const char* ewp = getenv("PM_ES_WSPACK");
+  g_wspack = !(ewp && ewp[0] == '0');
   const char* etz = getenv("PM_ES_T3Z");
   g_no_t3z = etz && etz[0] == '0';
   g_t3z = false;
@@ -1764,12 +1878,14 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
   }
   // PAIR: consecutive slots of one shape form a pair; an odd one out is paired with itself (both halves compute the
   // same family and store the same values to the same coefficients)
+  // (g_fpw families per wave: consecutive slots of one shape form a unit of g_fpw, a short unit padded with its first slot)
   out->pair = g_pair;
+  out->fpw = g_fpw;
   for (size_t i = 0; g_pair && i < out->slot_sig.size();) {
-    const bool two = i + 1 < out->slot_sig.size() && out->slot_sig[i + 1] == out->slot_sig[i];
-    out->pair_k.push_back((int)i);
-    out->pair_k.push_back((int)(two ? i + 1 : i));
-    i += two ? 2 : 1;
+    size_t j = i + 1;
+    while (j < out->slot_sig.size() && (int)(j - i) < g_fpw && out->slot_sig[j] == out->slot_sig[i]) j++;
+    for (int f = 0; f < g_fpw; f++) out->pair_k.push_back((int)(i + f < j ? i + f : i));
+    i = j;
   }
   out->n_shapes = (int)names.size();
   std::string src = kPrologue;
@@ -1784,7 +1900,7 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
     // waves per block: as many workspace slices as fit the 64 KB of static LDS next to the tables
     const int tables = (256 + 6 * 27) * 8 + (g_t3z ? (320 + 10) * 4 : 0);
     // (one wave per SIMD: the occupancy comes from blocks per CU, build() asks the runtime for them)
-    const int slice = (g_pair ? 2 : 1) * (ws + pensz) * 8;   // (a pair's two family slices per wave)
+    const int slice = g_fpw * (ws + pensz) * 8;   // (a unit's family slices per wave)
     // (at most 4: one wave per SIMD and block; measured on config 4 --denovo, 4 beat 1, 2, 5 and 6 even where those
     // gave more waves per CU -- profiles/r05k_ab_es_wpb.txt)
     const int fit = (64 * 1024 - tables) / slice;
@@ -1795,16 +1911,19 @@ std::string generate(int chrom, const std::vector<Family>& fams, const double (*
     const size_t at = wk.find("extern \"C\"");   // device helpers first, then the family functions, then the kernel
     src += wk.substr(0, at);
     {   // the family units' slot words (unit = slot pair in pair mode, else slot; both halves' entries): constants
-      const size_t nu = g_pair ? out->pair_k.size() / 2 : out->slot_e.size();
-      std::string p0 = "__constant__ int kUP0[" + std::to_string(2 * nu) + "] = {", e = "__constant__ int kUE[" + std::to_string(2 * nu) + "] = {",
+      const size_t nu = g_pair ? out->pair_k.size() / g_fpw : out->slot_e.size();
+      const std::string nf = std::to_string(g_fpw * nu);
+      std::string p0 = "__constant__ int kUP0[" + nf + "] = {", e = "__constant__ int kUE[" + nf + "] = {",
                   sg = "__constant__ int kUSig[" + std::to_string(nu) + "] = {";
       for (size_t u = 0; u < nu; u++) {
-        const int k0 = g_pair ? out->pair_k[2 * u] : (int)u, k1 = g_pair ? out->pair_k[2 * u + 1] : (int)u;
-        p0 += std::to_string(out->slot_p0[k0]) + "," + std::to_string(out->slot_p0[k1]) + ",";
-        e += std::to_string(out->slot_e[k0]) + "," + std::to_string(out->slot_e[k1]) + ",";
-        sg += std::to_string(out->slot_sig[k0]) + ",";
+        for (int f = 0; f < g_fpw; f++) {
+          const int k = g_pair ? out->pair_k[g_fpw * u + f] : (int)u;
+          p0 += std::to_string(out->slot_p0[k]) + ",";
+          e += std::to_string(out->slot_e[k]) + ",";
+        }
+        sg += std::to_string(out->slot_sig[g_pair ? out->pair_k[g_fpw * u] : (int)u]) + ",";
       }
-      src += p0 + "};\n" + e + "};\n" + sg + "};\n";
+      src += p0 + "};\n" + e + "};\n" + sg + "};\n__device__ constexpr int kNUnits = " + std::to_string(nu) + ";\n";
     }
     if (g_t3z) {   // the plain Mendelian T(e = i 10 + j, k)'s non-zero terms per child state k, ascending e: e << 2 | code
       auto gi = [](int b1, int b2) { return b1 < b2 ? (b1 - 1) * (10 - b1) / 2 + (b2 - b1) : (b2 - 1) * (10 - b2) / 2 + (b1 - b2); };

@@ -75,7 +75,8 @@ struct Kernel {
   int wpb = 0, ws = 0;       // waves per block, workspace doubles per wave
   int blocks_per_cu = 0;     // es_hoist_wave blocks resident per CU (the runtime's occupancy; 0 unknown)
   bool pair = false;         // es_hoist_wave hoists two same-shape families per wave, one per half-wave (PM_ES_PAIR)
-  std::vector<int> pair_k;   // [2 npairs] slot indices of each pair (an unpaired slot: twice)
+  std::vector<int> pair_k;   // [fpw units] slot indices of each unit of fpw same-shape slots (a short unit: its first again)
+  int fpw = 1;               // families per wave (PM_ES_FPW; 2 = the pair mode)
 };
 
 // The fused Elston-Stewart Brent kernel ep_brent_jit (bi-allelic engines whose every family is peeled: config 4): one wave
