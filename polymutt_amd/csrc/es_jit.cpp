@@ -869,6 +869,13 @@ std::string gen_wave_family(const Family& F, int chrom, int NS, bool top, const 
       if (t_ < top_) { top_ = t_; best = q; }
     }
     fit(orders[best], true);
+    for (auto& a : rg)   // (the invariant the placement keeps: regions live in a common phase never share a double)
+      for (auto& b : rg)
+        if (a.first < b.first && a.second.hi >= b.second.lo && b.second.hi >= a.second.lo &&
+            a.second.off < b.second.off + b.second.size && b.second.off < a.second.off + a.second.size) {
+          fprintf(stderr, "es_jit: workspace regions %d and %d overlap while live (%s)\n", a.first, b.first, name.c_str());
+          abort();
+        }
     for (auto& r : rg) {
       if (r.first == -1) TB = r.second.off;
       else if (r.first >= 1000) mo[r.first - 1000] = r.second.off;
