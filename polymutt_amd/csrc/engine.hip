@@ -1235,11 +1235,15 @@ static int run_pipeline(pm_engine* E, int n, const uint8_t* pl, const uint32_t* 
   {   // persons per lane of k_prep: vector loads when n_person allows; the reference's serial mono order in EXACT
     const int np = E->n_person;
     int vmax = 8;   // measured best on 1000 quads (16 and 4 within 1%)
-    void (*prep)(DevArgs, int) = E->par.numerics == PM_NUM_EXACT ? (E->vcf ? k_prep<1, true, true> : k_prep<1, true>)
-                          : E->vcf ? ((np % 16 == 0 && vmax >= 16) ? k_prep<16, false, true> : (np % 8 == 0 && vmax >= 8) ? k_prep<8, false, true>
-                                      : (np % 4 == 0 && vmax >= 4) ? k_prep<4, false, true> : k_prep<1, false, true>)
-                          : (np % 16 == 0 && vmax >= 16) ? k_prep<16, false> : (np % 8 == 0 && vmax >= 8) ? k_prep<8, false>
-                          : (np % 4 == 0 && vmax >= 4) ? k_prep<4, false> : k_prep<1, false>;
+    // (the de novo monomorphism path compiled in only for engines that form it here: mono_dn == 1; vcf_mode never does)
+    const bool mdn = A.mono_dn == 1 && !E->vcf;
+    void (*prep)(DevArgs, int) = E->par.numerics == PM_NUM_EXACT ? (E->vcf ? k_prep<1, true, true, false> : mdn ? k_prep<1, true> : k_prep<1, true, false, false>)
+                          : E->vcf ? ((np % 16 == 0 && vmax >= 16) ? k_prep<16, false, true, false> : (np % 8 == 0 && vmax >= 8) ? k_prep<8, false, true, false>
+                                      : (np % 4 == 0 && vmax >= 4) ? k_prep<4, false, true, false> : k_prep<1, false, true, false>)
+                          : mdn ? ((np % 16 == 0 && vmax >= 16) ? k_prep<16, false> : (np % 8 == 0 && vmax >= 8) ? k_prep<8, false>
+                                   : (np % 4 == 0 && vmax >= 4) ? k_prep<4, false> : k_prep<1, false>)
+                          : (np % 16 == 0 && vmax >= 16) ? k_prep<16, false, false, false> : (np % 8 == 0 && vmax >= 8) ? k_prep<8, false, false, false>
+                          : (np % 4 == 0 && vmax >= 4) ? k_prep<4, false, false, false> : k_prep<1, false, false, false>;
     // sites per wave: PREP_SPW (PM_PREP_SPW = 1..8 overrides it; fewer sites per wave on config 4's 16 384-site
     // batches measured slower: 20.3 -> 19.7 M sites/s at 1, config 5 within noise, profiles/r05sp_ab_prep_spw.txt)
     int spw = PREP_SPW;

@@ -2266,9 +2266,15 @@ __device__ __forceinline__ void load_dwords(const uint32_t* p, uint32_t* out) {
 // same-address atomic per site serialised k_prep: 262 144 returning atomics on counts[0] per batch.)  spw is a
 // launch argument (engine.hip: PREP_SPW unless PM_PREP_SPW says otherwise).
 #define PREP_SPW 8
+#ifndef PREP_UNROLL
+#define PREP_UNROLL 4
+#endif
 // VC: vcf_mode engines -- no read depth or mapping quality (PedVCF / FamilyLikelihoodSeq_VCF): dm is neither read nor
 // summed, the lanes sum only the hom-ref plane's PL bytes
-template <int VEC, bool SERIAL, bool VC = false>
+// MDN: the de novo monomorphism product may be formed here (A.mono_dn == 1); false compiles that path out -- its ten
+// planes' bytes per chunk set the register allocation (138 -> fewer VGPRs: more waves per SIMD for the latency-bound
+// chunk loop)
+template <int VEC, bool SERIAL, bool VC = false, bool MDN = true>
 __global__ void __launch_bounds__(256) k_prep(DevArgs A, int spw) {
   __shared__ unsigned long long s_c[9];
   __shared__ double s_lk[256];
@@ -2276,7 +2282,7 @@ __global__ void __launch_bounds__(256) k_prep(DevArgs A, int spw) {
   __shared__ int s_nit[4 * PREP_SPW], s_pre[4 * PREP_SPW];   // items per site of the block (0: none), exclusive prefix
   __shared__ int s_base;
   if (threadIdx.x < 9) s_c[threadIdx.x] = 0;
-  if (A.mono_dn == 1) {
+  if (MDN && A.mono_dn == 1) {
     s_lk[threadIdx.x] = A.lktab[threadIdx.x];
     if (threadIdx.x < 100) s_M[threadIdx.x] = A.M[threadIdx.x];
   }
@@ -2305,7 +2311,7 @@ __global__ void __launch_bounds__(256) k_prep(DevArgs A, int spw) {
       // CalcDenovoMutLk(geno11)) * F11 * M11 (:1041-1132, :1553-1562): a product of per-person factors --
       // founders lk[geno11], kids their g11 dot product -- taken here as one normalised product per site.
       // (mono_dn == 2: the cfg-1 QUAD item forms it instead; k_prep then reads only dm and the hom-ref plane)
-      const bool mdn = A.mono_dn == 1 && okref;
+      const bool mdn = MDN && A.mono_dn == 1 && okref;
       double dm_m = 1.0;
       int dm_e = 0;
       const uint8_t* plane_h = pl + (size_t)h * np;
@@ -2345,8 +2351,9 @@ __global__ void __launch_bounds__(256) k_prep(DevArgs A, int spw) {
         }
       };
       if (!mdn) {
-        // unrolled: the loads of 4 chunks in flight together (one HBM round trip per chunk made k_prep latency-bound)
-#pragma unroll 4
+        // unrolled: the loads of PREP_UNROLL chunks in flight together (one HBM round trip per chunk made k_prep
+        // latency-bound)
+#pragma unroll PREP_UNROLL
         for (int base = 0; base < np; base += 64 * VEC) {
           uint8_t hr[VEC];
           chunk(base + lane * VEC, hr);
